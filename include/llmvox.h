@@ -1,0 +1,130 @@
+/*
+ * llmvox.h — C ABI of the MI355X-native LLMVoX streaming-TTS hot path
+ * (libllmvox_hip.so, built for gfx950).
+ *
+ * The reference has no native boundary: its hot path is reached through the
+ * duck-typed ModelHandler members that streaming_server.audio_generator_sync
+ * calls (reference: streaming_server.py:250-426, inference/model_handler.py:45-166).
+ * Each entry point below replaces one of those calls; the Python shim
+ * (llmvox_amd/handler.py) binds them with ctypes and keeps the reference
+ * signatures.
+ *
+ * Conventions
+ *   - Every function returns 0 on success, a negative LVX_E* code on error;
+ *     lvx_last_error() gives the message of the calling thread's last error.
+ *   - Pointers named *_dev are device pointers on the context's device
+ *     (e.g. torch tensor .data_ptr()); *_host are host pointers.
+ *   - `stream` is a hipStream_t passed as void* (NULL = legacy default stream).
+ *     All compute calls are asynchronous on that stream.
+ *   - Layouts are row-major, dtypes are fixed per argument (float32 / int32 /
+ *     int64) as named.
+ */
+#ifndef LLMVOX_H
+#define LLMVOX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LVX_OK 0
+#define LVX_E_ARG (-1)      /* bad argument / shape (reference: ValueError) */
+#define LVX_E_STATE (-2)    /* weights missing / not finalized */
+#define LVX_E_HIP (-3)      /* HIP runtime error */
+#define LVX_E_CAPACITY (-4) /* position >= block_size or KV capacity (reference: AssertionError,
+                               src/model.py:205) */
+#define LVX_E_NAME (-5)     /* unknown weight name */
+
+#define LVX_DTYPE_F32 0
+#define LVX_DTYPE_BF16 1
+
+typedef struct lvx_ctx lvx_ctx;
+
+typedef struct {
+  int device;           /* HIP device ordinal */
+  int weight_dtype;     /* LVX_DTYPE_F32 (parity mode; the reference runs fp32) or LVX_DTYPE_BF16 */
+  int kv_dtype;         /* LVX_DTYPE_F32 or LVX_DTYPE_BF16 */
+  int max_streams;      /* KV slots (concurrent utterance streams) */
+  int max_positions;    /* per-slot KV capacity, <= 8192 (GPTConfig.block_size) */
+  int max_codec_frames; /* max sum over streams of frames per codec call */
+} lvx_config;
+
+/* ---- lifetime ----------------------------------------------------------- */
+int lvx_create(const lvx_config* cfg, lvx_ctx** out);
+/* replaces ModelHandler.__init__'s device placement (model_handler.py:48-63) */
+void lvx_destroy(lvx_ctx* ctx);
+const char* lvx_last_error(void);
+int lvx_version(void);
+
+/* ---- weights (by reference state_dict key, fp32 host data) -------------
+ * replaces initialize_gpt_model / initialize_wavtokenizer / initialize_llm_model
+ * (model_handler.py:66-78,80-106,140-166). Keys: "transformer.*", "lm_head.weight",
+ * "backbone.*", "head.out.*", the codebook
+ * "feature_extractor.encodec.quantizer.vq.layers.0._codebook.embed", and
+ * "encoder.embed_tokens.weight" (the [386,256] text table). */
+int lvx_set_weight(lvx_ctx* ctx, const char* name, const float* data_host, int64_t numel);
+int lvx_finalize(lvx_ctx* ctx);
+/* number of required weights not yet set; fills *first_missing (may be NULL) */
+int lvx_missing_weights(lvx_ctx* ctx, const char** first_missing);
+
+/* ---- text / code embeddings -------------------------------------------- */
+/* ModelHandler.llm_model(ids): T5 encoder.embed_tokens gather
+ * (streaming_server.py:315,319). ids int64 [n] -> out float32 [n,256] */
+int lvx_text_embed(lvx_ctx* ctx, const int64_t* ids_dev, int n, float* out_dev, void* stream);
+/* WavTokenizer.codes_to_features (decoder/pretrained.py:209-239), n_q = 1:
+ * codes int64 [B,L] -> features float32 [B,512,L] */
+int lvx_codes_to_features(lvx_ctx* ctx, const int64_t* codes_dev, int B, int L, float* feats_dev,
+                          void* stream);
+
+/* ---- speech-token GPT ------------------------------------------------------ */
+/* Forget a stream's KV (the reference sets kvcache = None, streaming_server.py:412). */
+int lvx_stream_reset(lvx_ctx* ctx, int slot, void* stream);
+/* GPT.forward(emb, kvcache) for one stream (src/model.py:201-237): emb_row_dev is the LAST
+ * row of the caller's history (already normalised input, float32 [768]); pos is its index
+ * t-1. Appends K/V at pos in slot `slot`, attends over [0, pos], writes logits float32
+ * [4096]. */
+int lvx_ar_forward_row(lvx_ctx* ctx, int slot, int pos, const float* emb_row_dev, float* logits_dev,
+                       void* stream);
+/* One fused decode step for B batch rows (a2..a11 of the hot path). Row b drives slot
+ * slots[b] (-1 = idle row: computes nothing that is stored). With j = rowstep[b] and p the
+ * slot's device-side position: input = normalize(cat(text_table[text_plan[b][j]],
+ * p == 0 ? 0 : codebook[prev_token[slot]])) + wpe[p]  (streaming_server.py:325-338,
+ * src/model.py:206-217); runs the 4 blocks, ln_f, lm_head and the greedy argmax (first
+ * maximal index = argmax(softmax), streaming_server.py:342-346); writes tok_plan[b][j]
+ * (and margin_plan[b][j] = top1 - top2 logit, optional), stores the token as the slot's
+ * prev_token, advances the slot's position and rowstep[b]. text_plan / tok_plan /
+ * margin_plan are [B][plan_stride] device arrays, so a whole chunk of steps can be enqueued
+ * back to back (replayed as a HIP graph) and read back once. */
+int lvx_ar_step(lvx_ctx* ctx, int B, const int32_t* slots_dev, const int32_t* text_plan_dev,
+                int plan_stride, int32_t* rowstep_dev, int32_t* tok_plan_dev, float* margin_plan_dev,
+                void* stream);
+/* n_steps consecutive lvx_ar_step calls with the same arguments. */
+int lvx_ar_steps(lvx_ctx* ctx, int n_steps, int B, const int32_t* slots_dev, const int32_t* text_plan_dev,
+                 int plan_stride, int32_t* rowstep_dev, int32_t* tok_plan_dev, float* margin_plan_dev,
+                 void* stream);
+/* Synchronises the stream and reports (then clears) device-side capacity errors: a slot past
+ * max_positions (reference: the block_size AssertionError, src/model.py:205) or a row past
+ * the end of its plan. */
+int lvx_check_errors(lvx_ctx* ctx, void* stream);
+/* Set a slot's position and previous token (rewind after a speculative run-ahead, or jump). */
+int lvx_stream_set(lvx_ctx* ctx, int slot, int pos, int prev_token, void* stream);
+/* Host-side view of a slot's position (synchronises the stream). */
+int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
+/* Enable/disable HIP-graph replay of lvx_ar_step for a given B (default on). */
+int lvx_set_graphs(lvx_ctx* ctx, int enable);
+
+/* ---- codec decoder ------------------------------------------------------- */
+/* WavTokenizer.decode(features, bandwidth_id) (decoder/pretrained.py:192-207):
+ * features float32 [B,512,L] (the reference layout) -> pcm float32 [B, 320*L]. Streams are
+ * decoded independently (each one exactly as a separate reference call with its own L). */
+int lvx_codec_decode_features(lvx_ctx* ctx, const float* feats_dev, int B, int L, int bandwidth_id,
+                              float* pcm_dev, void* stream);
+/* codes_to_features + decode fused: codes int32 [B,L] -> pcm float32 [B,320*L] */
+int lvx_codec_decode_codes(lvx_ctx* ctx, const int32_t* codes_dev, int B, int L, int bandwidth_id,
+                           float* pcm_dev, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LLMVOX_H */

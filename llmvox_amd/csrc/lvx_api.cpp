@@ -1,0 +1,556 @@
+// C-ABI front end of libllmvox_hip.so (see include/llmvox.h).
+//
+// Owns: the device copies of all hot-path weights (converted / repacked for the kernels),
+// the KV pool (max_streams slots x max_positions), the per-step scratch, the codec scratch,
+// and the HIP graphs of the fused decode step.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "llmvox.h"
+#include "lvx_internal.h"
+
+using namespace lvx;
+
+static constexpr int kMaxCodecL = 4096;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    if (_e != hipSuccess)                                                                  \
+      return fail(LVX_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));         \
+  } while (0)
+
+struct WeightSpec {
+  std::vector<int64_t> shape;
+};
+
+std::map<std::string, WeightSpec> make_specs() {
+  std::map<std::string, WeightSpec> s;
+  s["transformer.wpe.weight"] = {{BLOCK_SIZE, D}};
+  for (int i = 0; i < N_LAYER; ++i) {
+    std::string p = "transformer.h." + std::to_string(i) + ".";
+    s[p + "ln_1.weight"] = {{D}};
+    s[p + "attn.c_attn.weight"] = {{3 * D, D}};
+    s[p + "attn.c_proj.weight"] = {{D, D}};
+    s[p + "ln_2.weight"] = {{D}};
+    s[p + "mlp.c_fc.weight"] = {{DFF, D}};
+    s[p + "mlp.c_proj.weight"] = {{D, DFF}};
+  }
+  s["transformer.ln_f.weight"] = {{D}};
+  s["lm_head.weight"] = {{VOCAB, D}};
+  s["encoder.embed_tokens.weight"] = {{TEXT_VOCAB, TEXT_DIM}};
+  s["feature_extractor.encodec.quantizer.vq.layers.0._codebook.embed"] = {{4096, SPEECH_DIM}};
+  const int CD = 768, CFF = 2304;
+  s["backbone.embed.weight"] = {{CD, 512, 7}};
+  s["backbone.embed.bias"] = {{CD}};
+  s["backbone.norm.scale.weight"] = {{4, CD}};
+  s["backbone.norm.shift.weight"] = {{4, CD}};
+  for (int i : {0, 1, 3, 4}) {
+    std::string p = "backbone.pos_net." + std::to_string(i) + ".";
+    for (const char* n : {"norm1", "norm2"}) {
+      s[p + n + ".weight"] = {{CD}};
+      s[p + n + ".bias"] = {{CD}};
+    }
+    for (const char* n : {"conv1", "conv2"}) {
+      s[p + n + ".weight"] = {{CD, CD, 3}};
+      s[p + n + ".bias"] = {{CD}};
+    }
+  }
+  s["backbone.pos_net.2.norm.weight"] = {{CD}};
+  s["backbone.pos_net.2.norm.bias"] = {{CD}};
+  for (const char* n : {"q", "k", "v", "proj_out"}) {
+    s[std::string("backbone.pos_net.2.") + n + ".weight"] = {{CD, CD, 1}};
+    s[std::string("backbone.pos_net.2.") + n + ".bias"] = {{CD}};
+  }
+  s["backbone.pos_net.5.weight"] = {{CD}};
+  s["backbone.pos_net.5.bias"] = {{CD}};
+  for (int i = 0; i < 12; ++i) {
+    std::string p = "backbone.convnext." + std::to_string(i) + ".";
+    s[p + "dwconv.weight"] = {{CD, 1, 7}};
+    s[p + "dwconv.bias"] = {{CD}};
+    s[p + "norm.scale.weight"] = {{4, CD}};
+    s[p + "norm.shift.weight"] = {{4, CD}};
+    s[p + "pwconv1.weight"] = {{CFF, CD}};
+    s[p + "pwconv1.bias"] = {{CFF}};
+    s[p + "pwconv2.weight"] = {{CD, CFF}};
+    s[p + "pwconv2.bias"] = {{CD}};
+    s[p + "gamma"] = {{CD}};
+  }
+  s["backbone.final_layer_norm.weight"] = {{CD}};
+  s["backbone.final_layer_norm.bias"] = {{CD}};
+  s["head.out.weight"] = {{1282, CD}};
+  s["head.out.bias"] = {{1282}};
+  return s;
+}
+
+const std::map<std::string, WeightSpec>& specs() {
+  static const std::map<std::string, WeightSpec> s = make_specs();
+  return s;
+}
+
+int64_t numel_of(const WeightSpec& w) {
+  int64_t n = 1;
+  for (auto d : w.shape) n *= d;
+  return n;
+}
+
+}  // namespace
+
+struct GraphKey {
+  int B, stride;
+  const void *slots, *text, *rowstep, *tok, *margin;
+  void* stream;
+  bool operator<(const GraphKey& o) const {
+    return std::tie(B, stride, slots, text, rowstep, tok, margin, stream) <
+           std::tie(o.B, o.stride, o.slots, o.text, o.rowstep, o.tok, o.margin, o.stream);
+  }
+};
+
+struct lvx_ctx {
+  lvx_config cfg{};
+  std::map<std::string, std::vector<float>> host;  // staged fp32 weights (released at finalize)
+  std::vector<void*> allocs;
+  bool finalized = false;
+  ArWeights arw;
+  ArState st;
+  CodecWeights cw;
+  CodecScratch cs;
+  float* window_override = nullptr;
+  std::map<GraphKey, hipGraphExec_t> graphs;
+  std::vector<hipGraph_t> graph_defs;
+  bool use_graphs = true;
+  std::mutex mu;
+
+  template <typename T>
+  int dalloc(T** p, size_t n) {
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, n * sizeof(T) + 256);
+    if (e != hipSuccess) return fail(LVX_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+    allocs.push_back(q);
+    *p = reinterpret_cast<T*>(q);
+    return 0;
+  }
+  int upload_f32(const std::vector<float>& v, const float** out) {
+    float* d;
+    if (int r = dalloc(&d, v.size())) return r;
+    HIP_TRY(hipMemcpy(d, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+    *out = d;
+    return 0;
+  }
+  // matrices in the weight dtype
+  int upload_w(const std::vector<float>& v, const void** out) {
+    if (cfg.weight_dtype == LVX_DTYPE_F32) return upload_f32(v, reinterpret_cast<const float**>(out));
+    std::vector<bf16_t> h(v.size());
+    for (size_t i = 0; i < v.size(); ++i) h[i] = f32_to_bf16(v[i]);
+    bf16_t* d;
+    if (int r = dalloc(&d, h.size())) return r;
+    HIP_TRY(hipMemcpy(d, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+    *out = d;
+    return 0;
+  }
+  const std::vector<float>& H(const std::string& k) { return host.at(k); }
+};
+
+// conv weight [N][C][T] -> tap-major [N][T*C]
+static std::vector<float> repack_conv(const std::vector<float>& w, int N, int C, int T) {
+  std::vector<float> o((size_t)N * C * T);
+  for (int n = 0; n < N; ++n)
+    for (int c = 0; c < C; ++c)
+      for (int t = 0; t < T; ++t) o[(size_t)n * T * C + (size_t)t * C + c] = w[((size_t)n * C + c) * T + t];
+  return o;
+}
+
+extern "C" {
+
+int lvx_version(void) { return 1; }
+
+const char* lvx_last_error(void) { return g_err.c_str(); }
+
+int lvx_create(const lvx_config* cfg, lvx_ctx** out) {
+  if (!cfg || !out) return fail(LVX_E_ARG, "null argument");
+  if (cfg->weight_dtype != LVX_DTYPE_F32 && cfg->weight_dtype != LVX_DTYPE_BF16)
+    return fail(LVX_E_ARG, "weight_dtype must be LVX_DTYPE_F32 or LVX_DTYPE_BF16");
+  if (cfg->kv_dtype != LVX_DTYPE_F32 && cfg->kv_dtype != LVX_DTYPE_BF16)
+    return fail(LVX_E_ARG, "kv_dtype must be LVX_DTYPE_F32 or LVX_DTYPE_BF16");
+  if (cfg->max_streams < 1 || cfg->max_streams > 1024) return fail(LVX_E_ARG, "max_streams out of range [1,1024]");
+  if (cfg->max_positions < 1 || cfg->max_positions > BLOCK_SIZE)
+    return fail(LVX_E_ARG, "max_positions out of range [1,8192] (GPTConfig.block_size)");
+  if (cfg->max_codec_frames < 1) return fail(LVX_E_ARG, "max_codec_frames must be >= 1");
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev == 0) return fail(LVX_E_HIP, "no HIP device available");
+  if (cfg->device < 0 || cfg->device >= ndev) return fail(LVX_E_ARG, "device ordinal out of range");
+  auto* c = new lvx_ctx();
+  c->cfg = *cfg;
+  *out = c;
+  return LVX_OK;
+}
+
+void lvx_destroy(lvx_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->cfg.device);
+  for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (auto g : c->graph_defs) (void)hipGraphDestroy(g);
+  for (void* p : c->allocs) (void)hipFree(p);
+  delete c;
+}
+
+int lvx_set_weight(lvx_ctx* c, const char* name, const float* data, int64_t numel) {
+  if (!c || !name || !data) return fail(LVX_E_ARG, "null argument");
+  std::string k(name);
+  if (c->finalized) return fail(LVX_E_STATE, "weights are frozen after lvx_finalize");
+  if (k == "head.istft.window") {
+    if (numel != 1280) return fail(LVX_E_ARG, "head.istft.window must have 1280 elements");
+    c->host[k] = std::vector<float>(data, data + numel);
+    return LVX_OK;
+  }
+  auto it = specs().find(k);
+  if (it == specs().end()) return fail(LVX_E_NAME, "unknown weight name: " + k);
+  if (numel != numel_of(it->second))
+    return fail(LVX_E_ARG, "weight " + k + ": expected " + std::to_string(numel_of(it->second)) + " elements, got " +
+                               std::to_string(numel));
+  c->host[k] = std::vector<float>(data, data + numel);
+  return LVX_OK;
+}
+
+int lvx_missing_weights(lvx_ctx* c, const char** first) {
+  if (!c) return fail(LVX_E_ARG, "null ctx");
+  if (c->finalized) return 0;
+  int n = 0;
+  static thread_local std::string name;
+  for (auto& kv : specs())
+    if (!c->host.count(kv.first)) {
+      if (n == 0) name = kv.first;
+      ++n;
+    }
+  if (first) *first = n ? name.c_str() : nullptr;
+  return n;
+}
+
+int lvx_finalize(lvx_ctx* c) {
+  if (!c) return fail(LVX_E_ARG, "null ctx");
+  if (c->finalized) return LVX_OK;
+  const char* miss = nullptr;
+  if (lvx_missing_weights(c, &miss) > 0) return fail(LVX_E_STATE, std::string("missing weight: ") + miss);
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  int r;
+#define UP_F(key, dst) \
+  if ((r = c->upload_f32(c->H(key), &(dst)))) return r;
+#define UP_W(vec, dst) \
+  if ((r = c->upload_w((vec), &(dst)))) return r;
+  // ---- AR ----
+  ArWeights& w = c->arw;
+  UP_F("transformer.wpe.weight", w.wpe);
+  UP_F("encoder.embed_tokens.weight", w.text_table);
+  UP_F("feature_extractor.encodec.quantizer.vq.layers.0._codebook.embed", w.codebook);
+  for (int i = 0; i < N_LAYER; ++i) {
+    std::string p = "transformer.h." + std::to_string(i) + ".";
+    UP_F(p + "ln_1.weight", w.ln1[i]);
+    UP_F(p + "ln_2.weight", w.ln2[i]);
+    UP_W(c->H(p + "attn.c_attn.weight"), w.w_attn[i]);
+    UP_W(c->H(p + "attn.c_proj.weight"), w.w_aproj[i]);
+    UP_W(c->H(p + "mlp.c_fc.weight"), w.w_fc[i]);
+    UP_W(c->H(p + "mlp.c_proj.weight"), w.w_mproj[i]);
+  }
+  UP_F("transformer.ln_f.weight", w.lnf);
+  UP_W(c->H("lm_head.weight"), w.w_lm);
+  // ---- codec ----
+  CodecWeights& cw = c->cw;
+  cw.codebook = w.codebook;
+  UP_W(repack_conv(c->H("backbone.embed.weight"), 768, 512, 7), cw.embed_w);
+  UP_F("backbone.embed.bias", cw.embed_b);
+  UP_F("backbone.norm.scale.weight", cw.ada_scale);
+  UP_F("backbone.norm.shift.weight", cw.ada_shift);
+  int ri = 0;
+  for (int i : {0, 1, 3, 4}) {
+    std::string p = "backbone.pos_net." + std::to_string(i) + ".";
+    UP_F(p + "norm1.weight", cw.rn_n1w[ri]);
+    UP_F(p + "norm1.bias", cw.rn_n1b[ri]);
+    UP_F(p + "norm2.weight", cw.rn_n2w[ri]);
+    UP_F(p + "norm2.bias", cw.rn_n2b[ri]);
+    UP_W(repack_conv(c->H(p + "conv1.weight"), 768, 768, 3), cw.rn_c1w[ri]);
+    UP_F(p + "conv1.bias", cw.rn_c1b[ri]);
+    UP_W(repack_conv(c->H(p + "conv2.weight"), 768, 768, 3), cw.rn_c2w[ri]);
+    UP_F(p + "conv2.bias", cw.rn_c2b[ri]);
+    ++ri;
+  }
+  {
+    const std::string p = "backbone.pos_net.2.";
+    UP_F(p + "norm.weight", cw.at_nw);
+    UP_F(p + "norm.bias", cw.at_nb);
+    std::vector<float> qkv, qkvb;
+    for (const char* n : {"q", "k", "v"}) {
+      auto& m = c->H(p + n + ".weight");
+      qkv.insert(qkv.end(), m.begin(), m.end());
+      auto& b = c->H(p + n + ".bias");
+      qkvb.insert(qkvb.end(), b.begin(), b.end());
+    }
+    UP_W(qkv, cw.at_qkv_w);
+    if ((r = c->upload_f32(qkvb, &cw.at_qkv_b))) return r;
+    UP_W(c->H(p + "proj_out.weight"), cw.at_proj_w);
+    UP_F(p + "proj_out.bias", cw.at_proj_b);
+  }
+  UP_F("backbone.pos_net.5.weight", cw.pn_w);
+  UP_F("backbone.pos_net.5.bias", cw.pn_b);
+  for (int i = 0; i < 12; ++i) {
+    std::string p = "backbone.convnext." + std::to_string(i) + ".";
+    UP_F(p + "dwconv.weight", cw.dw_w[i]);
+    UP_F(p + "dwconv.bias", cw.dw_b[i]);
+    UP_F(p + "norm.scale.weight", cw.cn_scale[i]);
+    UP_F(p + "norm.shift.weight", cw.cn_shift[i]);
+    UP_W(c->H(p + "pwconv1.weight"), cw.pw1_w[i]);
+    UP_F(p + "pwconv1.bias", cw.pw1_b[i]);
+    UP_W(c->H(p + "pwconv2.weight"), cw.pw2_w[i]);
+    UP_F(p + "pwconv2.bias", cw.pw2_b[i]);
+    UP_F(p + "gamma", cw.gamma[i]);
+  }
+  UP_F("backbone.final_layer_norm.weight", cw.fln_w);
+  UP_F("backbone.final_layer_norm.bias", cw.fln_b);
+  UP_W(c->H("head.out.weight"), cw.head_w);
+  UP_F("head.out.bias", cw.head_b);
+  {
+    std::vector<float> win(1280);
+    if (c->host.count("head.istft.window")) win = c->H("head.istft.window");
+    else
+      for (int n = 0; n < 1280; ++n) win[n] = (float)(0.5 - 0.5 * std::cos(2.0 * M_PI * n / 1280.0));
+    if ((r = c->upload_f32(win, &cw.window))) return r;
+    std::vector<float> tw(2 * 1280);
+    for (int m = 0; m < 1280; ++m) {
+      tw[2 * m] = (float)std::cos(2.0 * M_PI * m / 1280.0);
+      tw[2 * m + 1] = (float)std::sin(2.0 * M_PI * m / 1280.0);
+    }
+    if ((r = c->upload_f32(tw, &cw.twiddle))) return r;
+  }
+#undef UP_F
+#undef UP_W
+  // ---- AR state ----
+  ArState& st = c->st;
+  const int S = c->cfg.max_streams, P = c->cfg.max_positions;
+  st.max_pos = P;
+  st.max_streams = S;
+  if ((r = c->dalloc(&st.slots, S)) || (r = c->dalloc(&st.pos, S)) || (r = c->dalloc(&st.prev, S)) ||
+      (r = c->dalloc(&st.err, 4)) || (r = c->dalloc(&st.x, (size_t)S * D)) || (r = c->dalloc(&st.q, (size_t)S * D)) ||
+      (r = c->dalloc(&st.part_o, (size_t)S * N_HEAD * NSPLIT * HD)) ||
+      (r = c->dalloc(&st.part_ml, (size_t)S * N_HEAD * NSPLIT * 2)) || (r = c->dalloc(&st.h, (size_t)S * DFF)) ||
+      (r = c->dalloc(&st.logits, (size_t)S * VOCAB)))
+    return r;
+  HIP_TRY(hipMemset(st.pos, 0, S * 4));
+  HIP_TRY(hipMemset(st.prev, 0, S * 4));
+  HIP_TRY(hipMemset(st.err, 0, 16));
+  const size_t kvn = (size_t)N_LAYER * S * N_HEAD * P * HD;
+  const size_t kvb = c->cfg.kv_dtype == LVX_DTYPE_BF16 ? 2 : 4;
+  {
+    char* k;
+    char* v;
+    if ((r = c->dalloc(&k, kvn * kvb)) || (r = c->dalloc(&v, kvn * kvb))) return r;
+    st.kc = k;
+    st.vc = v;
+  }
+  // ---- codec scratch ----
+  CodecScratch& cs = c->cs;
+  const int M = c->cfg.max_codec_frames;
+  cs.max_frames = M;
+  if ((r = c->dalloc(&cs.x, (size_t)M * 768)) || (r = c->dalloc(&cs.t1, (size_t)M * 2304)) ||
+      (r = c->dalloc(&cs.t2, (size_t)(M + 4 * 64) * 2304 + (size_t)768 * 4 * M)) ||
+      (r = c->dalloc(&cs.feats, (size_t)M * 512)) ||
+      (r = c->dalloc(&cs.att, (size_t)M * (std::min(M, kMaxCodecL) + 4))) ||
+      (r = c->dalloc(&cs.stats, (size_t)M * 32 * 2)) || (r = c->dalloc(&cs.spec, (size_t)M * 1282)) ||
+      (r = c->dalloc(&cs.frames, (size_t)M * 1280)))
+    return r;
+  HIP_TRY(hipDeviceSynchronize());
+  c->host.clear();
+  c->finalized = true;
+  return LVX_OK;
+}
+
+#define NEED_FINAL(c)                                                              \
+  do {                                                                             \
+    if (!(c)) return fail(LVX_E_ARG, "null ctx");                                  \
+    if (!(c)->finalized) return fail(LVX_E_STATE, "call lvx_finalize first");      \
+  } while (0)
+
+int lvx_text_embed(lvx_ctx* c, const int64_t* ids, int n, float* out, void* stream) {
+  NEED_FINAL(c);
+  if (n < 0 || (n > 0 && (!ids || !out))) return fail(LVX_E_ARG, "bad ids/out");
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  launch_text_embed(c->arw.text_table, ids, n, out, (hipStream_t)stream);
+  HIP_TRY(hipGetLastError());
+  return LVX_OK;
+}
+
+int lvx_codes_to_features(lvx_ctx* c, const int64_t* codes, int B, int L, float* feats, void* stream) {
+  NEED_FINAL(c);
+  if (B < 0 || L < 0 || ((B * L) > 0 && (!codes || !feats))) return fail(LVX_E_ARG, "bad codes/feats");
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  launch_codes_to_features(c->arw.codebook, codes, B, L, feats, (hipStream_t)stream);
+  HIP_TRY(hipGetLastError());
+  return LVX_OK;
+}
+
+int lvx_stream_reset(lvx_ctx* c, int slot, void* stream) {
+  NEED_FINAL(c);
+  if (slot < 0 || slot >= c->cfg.max_streams) return fail(LVX_E_ARG, "slot out of range");
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  HIP_TRY(hipMemsetAsync(c->st.pos + slot, 0, 4, (hipStream_t)stream));
+  return LVX_OK;
+}
+
+int lvx_stream_set(lvx_ctx* c, int slot, int pos, int prev_token, void* stream) {
+  NEED_FINAL(c);
+  if (slot < 0 || slot >= c->cfg.max_streams) return fail(LVX_E_ARG, "slot out of range");
+  if (pos < 0 || pos > c->cfg.max_positions) return fail(LVX_E_CAPACITY, "position out of range");
+  if (prev_token < 0 || prev_token >= VOCAB) return fail(LVX_E_ARG, "prev_token out of range");
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  launch_set_slot(c->st.pos, c->st.prev, slot, pos, prev_token, (hipStream_t)stream);
+  HIP_TRY(hipGetLastError());
+  return LVX_OK;
+}
+
+int lvx_stream_position(lvx_ctx* c, int slot, int* pos_out, void* stream) {
+  NEED_FINAL(c);
+  if (slot < 0 || slot >= c->cfg.max_streams || !pos_out) return fail(LVX_E_ARG, "bad slot/pos_out");
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  int32_t v[2];
+  HIP_TRY(hipMemcpyAsync(&v[0], c->st.pos + slot, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIP_TRY(hipMemcpyAsync(&v[1], c->st.err, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  *pos_out = v[0];
+  if (v[1]) {
+    (void)hipMemsetAsync(c->st.err, 0, 4, (hipStream_t)stream);
+    return fail(LVX_E_CAPACITY, "a stream exceeded its KV capacity (max_positions)");
+  }
+  return LVX_OK;
+}
+
+int lvx_set_graphs(lvx_ctx* c, int enable) {
+  if (!c) return fail(LVX_E_ARG, "null ctx");
+  c->use_graphs = enable != 0;
+  return LVX_OK;
+}
+
+int lvx_ar_forward_row(lvx_ctx* c, int slot, int pos, const float* emb_row, float* logits, void* stream) {
+  NEED_FINAL(c);
+  if (slot < 0 || slot >= c->cfg.max_streams) return fail(LVX_E_ARG, "slot out of range");
+  if (pos < 0 || pos >= BLOCK_SIZE)
+    return fail(LVX_E_CAPACITY, "Cannot forward sequence of length " + std::to_string(pos + 1) +
+                                    ", block size is only " + std::to_string(BLOCK_SIZE));
+  if (pos >= c->cfg.max_positions)
+    return fail(LVX_E_CAPACITY, "position " + std::to_string(pos) + " exceeds the KV capacity " +
+                                    std::to_string(c->cfg.max_positions));
+  if (!emb_row || !logits) return fail(LVX_E_ARG, "null emb_row/logits");
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  ar_launch_step(c->arw, c->st, c->cfg.weight_dtype, c->cfg.kv_dtype, 1, 1, emb_row, slot, pos, logits,
+                 (hipStream_t)stream);
+  HIP_TRY(hipGetLastError());
+  return LVX_OK;
+}
+
+int lvx_ar_step(lvx_ctx* c, int B, const int32_t* slots, const int32_t* text_plan, int plan_stride,
+                int32_t* rowstep, int32_t* tok_plan, float* margin_plan, void* stream) {
+  NEED_FINAL(c);
+  if (B < 1 || B > c->cfg.max_streams) return fail(LVX_E_ARG, "B out of range [1, max_streams]");
+  if (plan_stride < 1) return fail(LVX_E_ARG, "plan_stride must be >= 1");
+  if (!slots || !text_plan || !rowstep || !tok_plan) return fail(LVX_E_ARG, "null slots/text_plan/rowstep/tok_plan");
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  ArState st = c->st;
+  st.slots = const_cast<int32_t*>(slots);
+  st.text_plan = text_plan;
+  st.plan_stride = plan_stride;
+  st.rowstep = rowstep;
+  st.tok_plan = tok_plan;
+  st.margin_plan = margin_plan;
+  hipStream_t s = (hipStream_t)stream;
+  if (!c->use_graphs || s == nullptr) {
+    ar_launch_step(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, 0, nullptr, 0, 0, nullptr, s);
+    HIP_TRY(hipGetLastError());
+    return LVX_OK;
+  }
+  std::lock_guard<std::mutex> lk(c->mu);
+  GraphKey key{B, plan_stride, slots, text_plan, rowstep, tok_plan, margin_plan, stream};
+  auto it = c->graphs.find(key);
+  if (it == c->graphs.end()) {
+    hipGraph_t g;
+    HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    ar_launch_step(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, 0, nullptr, 0, 0, nullptr, s);
+    hipError_t le = hipGetLastError();
+    HIP_TRY(hipStreamEndCapture(s, &g));
+    if (le != hipSuccess) return fail(LVX_E_HIP, std::string("capture: ") + hipGetErrorString(le));
+    hipGraphExec_t ex;
+    HIP_TRY(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    c->graph_defs.push_back(g);
+    it = c->graphs.emplace(key, ex).first;
+  }
+  HIP_TRY(hipGraphLaunch(it->second, s));
+  return LVX_OK;
+}
+
+int lvx_ar_steps(lvx_ctx* c, int n_steps, int B, const int32_t* slots, const int32_t* text_plan, int plan_stride,
+                 int32_t* rowstep, int32_t* tok_plan, float* margin_plan, void* stream) {
+  for (int i = 0; i < n_steps; ++i)
+    if (int r = lvx_ar_step(c, B, slots, text_plan, plan_stride, rowstep, tok_plan, margin_plan, stream)) return r;
+  return LVX_OK;
+}
+
+int lvx_check_errors(lvx_ctx* c, void* stream) {
+  NEED_FINAL(c);
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  int32_t v = 0;
+  HIP_TRY(hipMemcpyAsync(&v, c->st.err, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  if (v) {
+    (void)hipMemsetAsync(c->st.err, 0, 4, (hipStream_t)stream);
+    if (v & 1) return fail(LVX_E_CAPACITY, "a stream exceeded its KV capacity (max_positions)");
+    return fail(LVX_E_CAPACITY, "a batch row ran past the end of its text plan (plan_stride)");
+  }
+  return LVX_OK;
+}
+
+static int codec_check(lvx_ctx* c, int B, int L, int bw) {
+  if (B < 1 || L < 1) return fail(LVX_E_ARG, "B and L must be >= 1");
+  if ((long long)B * L > c->cfg.max_codec_frames)
+    return fail(LVX_E_CAPACITY, "B*L = " + std::to_string((long long)B * L) + " exceeds max_codec_frames " +
+                                    std::to_string(c->cfg.max_codec_frames));
+  if (L > kMaxCodecL) return fail(LVX_E_CAPACITY, "L exceeds the codec's max frames per stream (4096)");
+  if (bw < 0 || bw > 3) return fail(LVX_E_ARG, "bandwidth_id out of range [0,3]");
+  return 0;
+}
+
+int lvx_codec_decode_features(lvx_ctx* c, const float* feats, int B, int L, int bw, float* pcm, void* stream) {
+  NEED_FINAL(c);
+  if (int r = codec_check(c, B, L, bw)) return r;
+  if (!feats || !pcm) return fail(LVX_E_ARG, "null feats/pcm");
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  codec_launch_decode(c->cw, c->cs, c->cfg.weight_dtype, feats, nullptr, B, L, bw, pcm, (hipStream_t)stream);
+  HIP_TRY(hipGetLastError());
+  return LVX_OK;
+}
+
+int lvx_codec_decode_codes(lvx_ctx* c, const int32_t* codes, int B, int L, int bw, float* pcm, void* stream) {
+  NEED_FINAL(c);
+  if (int r = codec_check(c, B, L, bw)) return r;
+  if (!codes || !pcm) return fail(LVX_E_ARG, "null codes/pcm");
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  codec_launch_decode(c->cw, c->cs, c->cfg.weight_dtype, nullptr, codes, B, L, bw, pcm, (hipStream_t)stream);
+  HIP_TRY(hipGetLastError());
+  return LVX_OK;
+}
+
+}  // extern "C"

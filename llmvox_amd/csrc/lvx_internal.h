@@ -1,0 +1,109 @@
+// Internal (C++) interfaces between the C-ABI front end and the kernel files.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "lvx_common.h"
+#include "llmvox.h"
+
+namespace lvx {
+
+constexpr int N_LAYER = 4, N_HEAD = 8, D = 768, HD = 96, DFF = 3072, VOCAB = 4096;
+constexpr int TEXT_DIM = 256, SPEECH_DIM = 512, TEXT_VOCAB = 386, BLOCK_SIZE = 8192;
+constexpr int NSPLIT = 16;  // max KV splits per (stream, head) in decode attention
+
+// Device-resident AR weights. Matrices are [out][in] row-major (torch Linear layout),
+// in the context's weight dtype; vectors and gathered tables are fp32.
+struct ArWeights {
+  const float* wpe = nullptr;         // [8192][768]
+  const float* text_table = nullptr;  // [386][256]
+  const float* codebook = nullptr;    // [4096][512] (shared with the codec)
+  const float* ln1[N_LAYER] = {};
+  const float* ln2[N_LAYER] = {};
+  const float* lnf = nullptr;
+  const void* w_attn[N_LAYER] = {};   // [2304][768]
+  const void* w_aproj[N_LAYER] = {};  // [768][768]
+  const void* w_fc[N_LAYER] = {};     // [3072][768]
+  const void* w_mproj[N_LAYER] = {};  // [768][3072]
+  const void* w_lm = nullptr;         // [4096][768]
+};
+
+// Device-resident decode state + scratch.
+struct ArState {
+  int32_t* slots = nullptr;      // [B] slot of batch row b (-1: idle row)
+  const int32_t* text_plan = nullptr;  // [B][plan_stride] text id of row b at its step j
+  int32_t* rowstep = nullptr;    // [B] next step j of row b (advanced by the step)
+  int32_t* tok_plan = nullptr;   // [B][plan_stride] greedy token of row b at step j
+  float* margin_plan = nullptr;  // [B][plan_stride] top1-top2 logit margin (optional)
+  int plan_stride = 1;
+  int32_t* pos = nullptr;       // [max_streams] per-slot next position
+  int32_t* prev = nullptr;      // [max_streams] per-slot previous token
+  int32_t* err = nullptr;       // [1] capacity overflow flag
+  float* x = nullptr;           // [B][768] residual stream
+  float* q = nullptr;           // [B][768]
+  float* part_o = nullptr;      // [B][8][NSPLIT][96]
+  float* part_ml = nullptr;     // [B][8][NSPLIT][2]
+  float* h = nullptr;           // [B][3072]
+  float* logits = nullptr;      // [B][4096]
+  void* kc = nullptr;           // [4][max_streams][8][max_pos][96]
+  void* vc = nullptr;
+  int max_pos = 0, max_streams = 0;
+};
+
+// Launches the whole decode step (embed -> 4 blocks -> lm_head [-> argmax]).
+// mode 0: fused step (inputs from st.slots/st.text_ids, argmax + state advance)
+// mode 1: drop-in row forward (emb_row given, single stream, logits to `logits_out`)
+void ar_launch_step(const ArWeights& w, const ArState& st, int wdtype, int kvdtype, int B, int mode,
+                    const float* emb_row, int slot, int pos, float* logits_out, hipStream_t s);
+
+void launch_set_slot(int32_t* pos, int32_t* prev, int slot, int p, int tok, hipStream_t s);
+void launch_text_embed(const float* table, const int64_t* ids, int n, float* out, hipStream_t s);
+void launch_codes_to_features(const float* codebook, const int64_t* codes, int B, int L, float* feats,
+                              hipStream_t s);
+
+// ---------------- codec ----------------
+struct CodecWeights {
+  const float* codebook = nullptr;      // [4096][512]
+  const void* embed_w = nullptr;        // [768][7*512] (tap-major repack of [768][512][7])
+  const float* embed_b = nullptr;
+  const float* ada_scale = nullptr;     // backbone.norm.scale.weight [4][768]
+  const float* ada_shift = nullptr;
+  // pos_net resnet blocks 0,1,3,4 -> index 0..3
+  const float* rn_n1w[4] = {}; const float* rn_n1b[4] = {};
+  const float* rn_n2w[4] = {}; const float* rn_n2b[4] = {};
+  const void* rn_c1w[4] = {};  const float* rn_c1b[4] = {};  // [768][3*768]
+  const void* rn_c2w[4] = {};  const float* rn_c2b[4] = {};
+  const float* at_nw = nullptr; const float* at_nb = nullptr;
+  const void* at_qkv_w = nullptr; const float* at_qkv_b = nullptr;  // [2304][768], [2304]
+  const void* at_proj_w = nullptr; const float* at_proj_b = nullptr;
+  const float* pn_w = nullptr; const float* pn_b = nullptr;  // pos_net.5 GroupNorm
+  const float* dw_w[12] = {};   // [768][7]
+  const float* dw_b[12] = {};
+  const float* cn_scale[12] = {}; const float* cn_shift[12] = {};  // [4][768]
+  const void* pw1_w[12] = {}; const float* pw1_b[12] = {};  // [2304][768]
+  const void* pw2_w[12] = {}; const float* pw2_b[12] = {};  // [768][2304]
+  const float* gamma[12] = {};
+  const float* fln_w = nullptr; const float* fln_b = nullptr;
+  const void* head_w = nullptr; const float* head_b = nullptr;  // [1282][768]
+  const float* window = nullptr;  // [1280] periodic Hann
+  const float* twiddle = nullptr; // FFT tables (see istft)
+};
+
+struct CodecScratch {
+  float* x = nullptr;      // [M][768]
+  float* t1 = nullptr;     // [M][2304] general temp
+  float* t2 = nullptr;     // [M][2304]
+  float* feats = nullptr;  // [M][512]
+  float* att = nullptr;    // [sum_b L_b^2] scores
+  float* stats = nullptr;  // [B][32][2]
+  float* spec = nullptr;   // [M][1282]
+  float* frames = nullptr; // [M][1280]
+  int max_frames = 0;
+};
+
+// feats_in: [B][512][L] (reference layout) when codes == nullptr; else codes [B][L]
+void codec_launch_decode(const CodecWeights& w, const CodecScratch& sc, int wdtype, const float* feats_in,
+                         const int32_t* codes, int B, int L, int bw, float* pcm, hipStream_t s);
+
+}  // namespace lvx

@@ -1,0 +1,149 @@
+"""Thin Python owner of one ``lvx_ctx`` (one device): weights, KV slots, entry points.
+
+Every compute method is asynchronous on the device's current torch stream and takes /
+returns torch device tensors (torch is only the allocator and the stream provider here).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from .weights import CODEBOOK_KEY, TEXT_EMBED_KEY
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class Engine:
+    def __init__(self, device_index: int = 0, weight_dtype: str = "fp32", kv_dtype: str = "fp32",
+                 max_streams: int = 8, max_positions: int = 8192, max_codec_frames: int = 1280):
+        self.lib = _lib.load()
+        if not torch.cuda.is_available():
+            raise RuntimeError("llmvox_amd needs a ROCm GPU (MI355X); there is no CPU path")
+        self.device = torch.device(f"cuda:{device_index}")
+        self.device_index = device_index
+        cfg = _lib.LvxConfig(device_index, _lib.DTYPES[weight_dtype], _lib.DTYPES[kv_dtype], max_streams,
+                             max_positions, max_codec_frames)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.lvx_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self.h = h
+        self.weight_dtype = weight_dtype
+        self.kv_dtype = kv_dtype
+        self.max_streams = max_streams
+        self.max_positions = max_positions
+        self.max_codec_frames = max_codec_frames
+        self.finalized = False
+
+    # ---- weights ----------------------------------------------------------------
+    def set_weight(self, name: str, arr):
+        a = np.ascontiguousarray(np.asarray(arr, dtype=np.float32))
+        _lib.check(self.lib.lvx_set_weight(self.h, name.encode(), a.ctypes.data_as(ctypes.c_void_p), a.size))
+
+    def load_weights(self, gpt: Dict[str, np.ndarray], codec: Dict[str, np.ndarray], text_table: np.ndarray):
+        for k, v in gpt.items():
+            if k.endswith("attn.bias"):  # causal-mask buffer of the no-flash path, not a weight
+                continue
+            self.set_weight(k, v)
+        for k, v in codec.items():
+            if k == "head.istft.window":
+                continue
+            self.set_weight(k, v)
+        self.set_weight(TEXT_EMBED_KEY, text_table)
+        # exactly torch's periodic Hann window (decoder/spectral_ops.py:30-31)
+        self.set_weight("head.istft.window", torch.hann_window(1280).numpy())
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.lvx_finalize(self.h))
+        self.finalized = True
+
+    # ---- helpers ----------------------------------------------------------------
+    def stream_handle(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # ---- drop-in members -------------------------------------------------------------
+    def text_embed(self, ids: torch.Tensor) -> torch.Tensor:
+        ids = ids.to(self.device, torch.int64).contiguous()
+        out = torch.empty(*ids.shape, 256, device=self.device, dtype=torch.float32)
+        _lib.check(self.lib.lvx_text_embed(self.h, _ptr(ids), ids.numel(), _ptr(out), self.stream_handle()))
+        return out
+
+    def codes_to_features(self, codes: torch.Tensor) -> torch.Tensor:
+        """codes int [B, L] -> [B, 512, L]."""
+        codes = codes.to(self.device, torch.int64).contiguous()
+        B, L = codes.shape
+        out = torch.empty(B, 512, L, device=self.device, dtype=torch.float32)
+        _lib.check(self.lib.lvx_codes_to_features(self.h, _ptr(codes), B, L, _ptr(out), self.stream_handle()))
+        return out
+
+    def forward_row(self, slot: int, pos: int, row: torch.Tensor, logits: torch.Tensor):
+        _lib.check(self.lib.lvx_ar_forward_row(self.h, slot, pos, _ptr(row), _ptr(logits), self.stream_handle()))
+
+    def reset_slot(self, slot: int):
+        _lib.check(self.lib.lvx_stream_reset(self.h, slot, self.stream_handle()))
+
+    def set_slot(self, slot: int, pos: int, prev_token: int = 0):
+        _lib.check(self.lib.lvx_stream_set(self.h, slot, pos, prev_token, self.stream_handle()))
+
+    def slot_position(self, slot: int) -> int:
+        v = ctypes.c_int()
+        _lib.check(self.lib.lvx_stream_position(self.h, slot, ctypes.byref(v), self.stream_handle()))
+        return v.value
+
+    def ar_steps(self, n_steps: int, slots: torch.Tensor, text_plan: torch.Tensor, rowstep: torch.Tensor,
+                 tok_plan: torch.Tensor, margin_plan: Optional[torch.Tensor] = None):
+        B, stride = text_plan.shape
+        _lib.check(self.lib.lvx_ar_steps(self.h, n_steps, B, _ptr(slots), _ptr(text_plan), stride, _ptr(rowstep),
+                                         _ptr(tok_plan), _ptr(margin_plan), self.stream_handle()))
+
+    def check_errors(self):
+        _lib.check(self.lib.lvx_check_errors(self.h, self.stream_handle()))
+
+    def set_graphs(self, enable: bool):
+        _lib.check(self.lib.lvx_set_graphs(self.h, int(enable)))
+
+    def decode_features(self, feats: torch.Tensor, bandwidth_id: int = 0) -> torch.Tensor:
+        feats = feats.to(self.device, torch.float32).contiguous()
+        B, C, L = feats.shape
+        if C != 512:
+            raise ValueError(f"features must be [B, 512, L], got {tuple(feats.shape)}")
+        pcm = torch.empty(B, 320 * L, device=self.device, dtype=torch.float32)
+        _lib.check(self.lib.lvx_codec_decode_features(self.h, _ptr(feats), B, L, int(bandwidth_id), _ptr(pcm),
+                                                      self.stream_handle()))
+        return pcm
+
+    def decode_codes(self, codes: torch.Tensor, bandwidth_id: int = 0, out: Optional[torch.Tensor] = None):
+        codes = codes.to(self.device, torch.int32).contiguous()
+        B, L = codes.shape
+        pcm = out if out is not None else torch.empty(B, 320 * L, device=self.device, dtype=torch.float32)
+        _lib.check(self.lib.lvx_codec_decode_codes(self.h, _ptr(codes), B, L, int(bandwidth_id), _ptr(pcm),
+                                                   self.stream_handle()))
+        return pcm
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.lvx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def build_engine(device_index=0, weight_dtype="fp32", kv_dtype="fp32", seed=1234, max_streams=8,
+                 max_positions=8192, max_codec_frames=1280, weights=None) -> Engine:
+    """Engine loaded with ``weights`` = (gpt, codec, text_table) or the seeded synthetic set."""
+    from .weights import synthetic_all
+    e = Engine(device_index, weight_dtype, kv_dtype, max_streams, max_positions, max_codec_frames)
+    gw, cw, tt = weights if weights is not None else synthetic_all(seed)
+    e.load_weights(gw, cw, tt)
+    return e
+
+
+__all__ = ["Engine", "build_engine", "CODEBOOK_KEY"]
