@@ -1,0 +1,329 @@
+#!/usr/bin/env python3
+"""LLMVoX streaming-TTS hot path on MI355X — the driver's benchmark.
+
+Workload (BASELINE.json configs[1]): "30M LLMVoX bf16, 1xMI355X, 1 stream, 256-token chunk,
+greedy". One bench STEP = one 256-token chunk of one utterance stream: 256 greedy AR decode
+steps of the speech-token GPT (fused HIP step, replayed as a HIP graph) + the WavTokenizer
+decode of those 256 codes into 81,920 PCM samples at 24 kHz + the PCM copy to the host.
+Steps continue the same stream (positions 0..K*256-1). Synthetic input: the config's 64-char
+sentence (66 ByT5 ids, then PAD), seeded synthetic weights at the reference init scales
+(no checkpoints offline).
+
+Multi-GPU (--gpus N under torch.distributed.run): one process per GPU, each running its own
+stream(s) (independent utterance streams: weak scaling); rank 0 scatters the text-id plans
+and gathers the PCM over RCCL (the path's only exchange, BASELINE north_star).
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+SENTENCE = "The quick brown fox jumps over the lazy dog near the river bank."
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
+
+
+def sentence_ids(text):
+    from llmvox_amd.tokenizer import ByteTokenizer
+    tok = ByteTokenizer()
+    ids = []
+    for w in text.split(" "):
+        t = tok(w.strip())["input_ids"]
+        if w.endswith("."):
+            t = t + [385]
+        ids += t
+    return ids
+
+
+def random_sentence(rng):
+    letters = "abcdefghijklmnopqrstuvwxyz "
+    s = "".join(rng.choice(list(letters), size=63))
+    s = " ".join(w for w in s.split(" ") if w) or "a"
+    return (s[:63]).strip() + "."
+
+
+def plan_for(ids, start, n, pad=384):
+    out = np.full(n, pad, dtype=np.int32)
+    seg = ids[start:start + n]
+    out[:len(seg)] = seg
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+def kernel_bytes(which, B, t, wbytes, kvbytes):
+    """Algorithmic HBM bytes of one launch (weights streamed once + KV + activations)."""
+    D, F, V = 768, 3072, 4096
+    act = 4 * B
+    if which == 0:
+        return 3 * D * D * wbytes + act * (D + D) + 2 * D * kvbytes * B
+    if which == 1:
+        return 2 * t * D * kvbytes * B + act * (D + 8 * 16 * 98)
+    if which == 2:
+        return D * D * wbytes + act * (8 * 16 * 98 + 2 * D)
+    if which == 3:
+        return F * D * wbytes + act * (D + F)
+    if which == 4:
+        return D * F * wbytes + act * (F + 2 * D)
+    if which == 5:
+        return V * D * wbytes + act * (D + V)
+    raise ValueError(which)
+
+
+KNAMES = {0: "ar_gemv c_attn", 1: "ar_attn (split-KV decode)", 2: "ar_gemv c_proj(+merge)",
+          3: "ar_gemv c_fc(+gelu)", 4: "ar_gemv mlp.c_proj", 5: "ar_gemv lm_head"}
+KCALLS = {0: 4, 1: 4, 2: 4, 3: 4, 4: 4, 5: 1}
+
+
+def probe_kernels(eng, slots, t, wbytes, kvbytes, iters=200):
+    res = {}
+    s = torch.cuda.current_stream(eng.device)
+    for k in KNAMES:
+        eng.probe_kernel(k, slots, 10)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        eng.probe_kernel(k, slots, iters)
+        e1.record(s)
+        e1.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / iters
+        by = kernel_bytes(k, slots.numel(), t, wbytes, kvbytes)
+        res[k] = {"name": KNAMES[k], "avg_us": us, "bytes": by, "gbs": by / (us * 1e-6) / 1e9,
+                  "share_us_per_step": us * KCALLS[k]}
+    return res
+
+
+# ---------------------------------------------------------------------------------------
+def cpu_baseline(n_chunks, chunk, max_seconds=60.0):
+    """The reference CPU eager path (oracle restatement: fp32, B=1, O(t) history/KV cats),
+    on this host's cores, on the same chunked workload (bounded)."""
+    from llmvox_amd import weights as LW
+    from oracle import reference_cpu as R
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    gw, cw, tt = LW.synthetic_all(1234)
+    W, Wc = R.to_torch(gw), R.to_torch(cw)
+    table = torch.from_numpy(tt)
+    cb = Wc[R.CODEBOOK_KEY]
+    ids = sentence_ids(SENTENCE)
+    t0 = time.perf_counter()
+    hist, kv, prev, done = None, None, None, 0
+    with torch.inference_mode():
+        for c in range(n_chunks):
+            toks = []
+            for i in range(c * chunk, (c + 1) * chunk):
+                tid = ids[i] if i < len(ids) else 384
+                te = table[tid].view(1, 1, -1)
+                se = torch.zeros(1, 1, 512) if i == 0 else cb[prev].view(1, 1, -1)
+                x = R.build_input(te, se)
+                hist = x if hist is None else torch.cat([hist, x], dim=1)
+                logits, kv = R.gpt_forward(W, hist, kv)
+                prev = R.greedy_token(logits)
+                toks.append(prev)
+            pcm = R.decode_codes(Wc, torch.tensor([toks]))
+            _ = pcm.numpy().astype("float32").tobytes()
+            done += chunk
+            if time.perf_counter() - t0 > max_seconds:
+                break
+    dt = time.perf_counter() - t0
+    cpu = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": done / dt, "unit": "speech tokens/s", "cores": threads, "kind": "port",
+            "sample": f"{done} tokens = {done // chunk} x ({chunk} fp32 AR steps + codec decode of {chunk} "
+                      f"frames), 1 stream, oracle/reference_cpu.py, {dt:.1f} s on {cpu}"}
+
+
+# ---------------------------------------------------------------------------------------
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--streams", type=int, default=1, help="streams per GPU (configs[2]: 32)")
+    ap.add_argument("--chunk", type=int, default=256)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-probe", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+
+    from llmvox_amd.engine import build_engine
+    S, chunk, K, Wm = args.streams, args.chunk, args.steps, args.warmup
+    if (K + 0) * chunk > 8192:
+        raise SystemExit("steps * chunk must stay within block_size 8192 positions")
+    eng = build_engine(local, args.dtype, args.dtype, max_streams=max(S, 1), max_positions=8192,
+                       max_codec_frames=S * chunk)
+    dev = eng.device
+    torch.cuda.set_device(dev)
+
+    # ---- text plans: stream 0 of rank 0 speaks the config sentence; others seeded sentences
+    n_pos = max(K, Wm) * chunk
+    plans = np.zeros((world * S, n_pos), dtype=np.int32)
+    rng = np.random.default_rng(1234)
+    for g in range(world * S):
+        ids = sentence_ids(SENTENCE if g == 0 else random_sentence(rng))
+        plans[g] = plan_for(ids, 0, n_pos)
+    full = torch.from_numpy(plans).to(dev)
+    if dist is not None:  # rank 0 scatters the text-id shards over RCCL
+        mine = torch.empty(S, n_pos, dtype=torch.int32, device=dev)
+        dist.scatter(mine, list(full.split(S)) if rank == 0 else None, src=0)
+    else:
+        mine = full[:S].contiguous()
+
+    slots = torch.arange(S, dtype=torch.int32, device=dev)
+    text_plan = torch.empty(S, chunk, dtype=torch.int32, device=dev)
+    rowstep = torch.zeros(S, dtype=torch.int32, device=dev)
+    tok_plan = torch.zeros(S, chunk, dtype=torch.int32, device=dev)
+    pcm = torch.empty(S, 320 * chunk, dtype=torch.float32, device=dev)
+    pcm_host = torch.empty(S, 320 * chunk, dtype=torch.float32, pin_memory=True)
+    gathered = [torch.empty_like(pcm) for _ in range(world)] if (dist is not None and rank == 0) else None
+
+    def run_chunk(c):
+        text_plan.copy_(mine[:, c * chunk:(c + 1) * chunk])
+        rowstep.zero_()
+        eng.ar_steps(chunk, slots, text_plan, rowstep, tok_plan)
+        eng.decode_codes(tok_plan, 0, out=pcm)
+        if dist is not None:
+            dist.gather(pcm, gathered, dst=0)
+        pcm_host.copy_(pcm, non_blocking=True)
+
+    def reset_all():
+        for s in range(S):
+            eng.reset_slot(s)
+
+    # ---- warmup (also captures the graph), then reset to position 0
+    reset_all()
+    for c in range(Wm):
+        run_chunk(c)
+    torch.cuda.synchronize()
+    eng.check_errors()
+    reset_all()
+    torch.cuda.synchronize()
+
+    # ---- timed region: K chunks
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for c in range(K):
+        run_chunk(c)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    eng.check_errors()
+    if dist is not None:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+
+    total_tokens = world * S * K * chunk
+    value = total_tokens / dt
+    toks_rank0 = tok_plan[0].cpu().numpy()
+
+    # ---- p50 first-chunk latency: fresh segment -> first 10-token dump (3,200 samples) on host
+    lat = []
+    first = torch.empty(1, 320 * 10, dtype=torch.float32, pin_memory=True)
+    one_slot = slots[:1]
+    tp1 = torch.empty(1, 10, dtype=torch.int32, device=dev)
+    rs1 = torch.zeros(1, dtype=torch.int32, device=dev)
+    tk1 = torch.zeros(1, 10, dtype=torch.int32, device=dev)
+    for r in range(12):
+        torch.cuda.synchronize()
+        ta = time.perf_counter()
+        eng.reset_slot(0)
+        tp1.copy_(mine[:1, :10])
+        rs1.zero_()
+        eng.ar_steps(10, one_slot, tp1, rs1, tk1)
+        p = eng.decode_codes(tk1, 0)
+        first.copy_(p)
+        torch.cuda.synchronize()
+        if r >= 2:
+            lat.append((time.perf_counter() - ta) * 1e3)
+    p50 = statistics.median(lat)
+
+    # ---- roofline: dominant kernel class, timed live with HIP events on the compute stream
+    rl, kern = None, None
+    if not args.no_probe:
+        reset_all()
+        for s in range(S):
+            eng.set_slot(s, K * chunk - 1, 0)
+        wb = 2 if args.dtype == "bf16" else 4
+        kern = probe_kernels(eng, slots, K * chunk, wb, wb)
+        dom = max(kern.values(), key=lambda r: r["share_us_per_step"])
+        rl = {"bound": "hbm", "kernel": dom["name"], "achieved": round(dom["gbs"], 1), "peak": HBM_PEAK_GBS,
+              "unit": "GB/s", "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4), "traffic": None,
+              "bytes_per_launch": dom["bytes"], "avg_us": round(dom["avg_us"], 3)}
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            try:
+                tr = json.load(open(pmc))
+                key = f"{args.dtype}:{dom['name']}"
+                if key in tr:
+                    rl["traffic"] = tr[key]
+            except Exception:
+                pass
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(K, chunk)
+
+    if rank == 0:
+        out = {
+            "metric": "speech tokens/sec (+ 24kHz audio samples/sec = 320 x tokens/s; p50 first-chunk latency)",
+            "value": round(value, 1),
+            "unit": "speech tokens/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": Wm,
+            "ms_per_step": round(dt / K * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (config 64-char sentence -> ByT5 ids, seeded synthetic weights at reference init scales)",
+            "config": {"workload": f"configs[{1 if S == 1 else 2}]: 30M LLMVoX {args.dtype}, {S} stream(s)/GPU, "
+                                   f"{chunk}-token chunk, greedy AR + WavTokenizer decode + PCM to host",
+                       "streams_per_gpu": S, "chunk_tokens": chunk, "positions": K * chunk,
+                       "parallelism": f"streams sharded over {world} GPU(s), RCCL scatter text / gather PCM"},
+            "audio_samples_per_s": round(320 * value, 1),
+            "realtime_factor_per_stream": round(value / (world * S) / 75.0, 1),
+            "p50_first_chunk_latency_ms": round(p50, 3),
+            "roofline": rl,
+            "cpu_baseline": cpu,
+            "kernels": {v["name"]: {"avg_us": round(v["avg_us"], 2), "GB/s": round(v["gbs"], 1)}
+                        for v in kern.values()} if kern else None,
+            "tokens_head": toks_rank0[:8].tolist(),
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

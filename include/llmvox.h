@@ -109,6 +109,11 @@ int lvx_ar_steps(lvx_ctx* ctx, int n_steps, int B, const int32_t* slots_dev, con
 int lvx_check_errors(lvx_ctx* ctx, void* stream);
 /* Set a slot's position and previous token (rewind after a speculative run-ahead, or jump). */
 int lvx_stream_set(lvx_ctx* ctx, int slot, int pos, int prev_token, void* stream);
+/* Measurement hook (bench.py): launch one kernel class of the decode step `iters` times for the
+ * batch rows `slots` at their current positions (0 c_attn, 1 attention, 2 c_proj+merge,
+ * 3 c_fc, 4 mlp c_proj, 5 lm_head). Writes only scratch and the K/V row at the current
+ * position (which the next real step overwrites). */
+int lvx_probe_kernel(lvx_ctx* ctx, int which, int B, const int32_t* slots_dev, int iters, void* stream);
 /* Host-side view of a slot's position (synchronises the stream). */
 int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
 /* Enable/disable HIP-graph replay of lvx_ar_step for a given B (default on). */

@@ -20,77 +20,21 @@
 namespace lvx {
 
 // ---------------------------------------------------------------------------------
-// embed: a2-a4 (+ wpe add of src/model.py:206-212, only the last row is ever used)
-// ---------------------------------------------------------------------------------
-template <int MODE>
-__global__ __launch_bounds__(256) void ar_embed_kernel(ArState st, const float* __restrict__ text_table,
-                                                       const float* __restrict__ codebook,
-                                                       const float* __restrict__ wpe,
-                                                       const float* __restrict__ emb_row, int slot_arg,
-                                                       int pos_arg) {
-  __shared__ float red[4];
-  const int b = blockIdx.x, tid = threadIdx.x;
-  if (MODE == 1) {
-    if (tid == 0) {
-      st.slots[0] = slot_arg;
-      st.pos[slot_arg] = pos_arg;
-    }
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      int i = tid + 256 * j;
-      st.x[i] = emb_row[i] + wpe[(size_t)pos_arg * D + i];
-    }
-    return;
-  }
-  const int s = st.slots[b];
-  if (s < 0) {  // idle row: zero input, nothing else of the row is stored
-#pragma unroll
-    for (int j = 0; j < 3; ++j) st.x[(size_t)b * D + tid + 256 * j] = 0.f;
-    return;
-  }
-  int p = st.pos[s];
-  if (p >= st.max_pos) {
-    if (tid == 0) atomicOr(st.err, 1);
-    p = st.max_pos - 1;
-  }
-  int step = st.rowstep[b];
-  if (step >= st.plan_stride) {  // ran past the end of the plan: flag, never read out of bounds
-    if (tid == 0) atomicOr(st.err, 2);
-    step = st.plan_stride - 1;
-  }
-  const int tok = min(max(st.text_plan[(size_t)b * st.plan_stride + step], 0), TEXT_VOCAB - 1);
-  const int prev = min(max(st.prev[s], 0), VOCAB - 1);
-  float v[3];
-  float ss = 0.f;
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    int i = tid + 256 * j;
-    float e;
-    if (i < TEXT_DIM) e = text_table[(size_t)tok * TEXT_DIM + i];
-    else e = (p == 0) ? 0.f : codebook[(size_t)prev * SPEECH_DIM + (i - TEXT_DIM)];
-    v[j] = e;
-    ss += e * e;
-  }
-  ss = block_sum<256>(ss, red);
-  const float den = fmaxf(sqrtf(ss), 1e-8f);  // F.normalize: x / max(||x||_2, eps)
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    int i = tid + 256 * j;
-    st.x[(size_t)b * D + i] = v[j] / den + wpe[(size_t)p * D + i];
-  }
-}
-
-// ---------------------------------------------------------------------------------
 // GEMV family: out[b][n] = sum_k W[n][k] * in[b][k]   (W row-major [N][K], TW in {f32,bf16})
-//   IN  0: in = LayerNorm(x[b]) * ln_w   (eps 1e-5, no bias; src/model.py:37-38)
-//   IN  1: in = h[b] (fp32)
+//   IN  0: in = LayerNorm(x[b]) * ln_w            (eps 1e-5, no bias; src/model.py:37-38)
+//   IN  1: in = h[b] (fp32, K = 3072)
 //   IN  2: in = merge of the split-KV attention partials (flash-decoding combine)
+//   IN  3: layer-0 c_attn: builds x[b] first (a2-a4: text row, codebook row of the previous
+//          token or 0 at position 0, L2-normalise eps 1e-8, + wpe[pos]; or, for the drop-in
+//          row forward, the caller's row + wpe[pos]), block 0 stores it, then LayerNorm.
 //   OUT 0: c_attn: q -> st.q, k/v -> KV cache at the slot's position
 //   OUT 1: residual: x[b][n] += out
 //   OUT 2: h[b][n] = gelu_tanh(out)
 //   OUT 3: logits: dst[b][n] = out
-// 4 waves per block, RPW rows per wave; lanes split K in 4-element chunks (coalesced 1 KB /
-// 512 B per wave-instruction), per-row partials reduced across the wave with DPP shuffles.
+// A block is 4 waves; KW waves share the K range of the same RPW rows (KW in {1,4}). Each
+// lane owns 4-element K chunks. All weight loads of the wave are issued before the input
+// prologue (they do not depend on it), so the HBM/MALL latency overlaps the LN / merge /
+// embed work, and the weights stay in registers across batch groups of BG rows.
 // ---------------------------------------------------------------------------------
 struct GemvArgs {
   ArState st;
@@ -101,44 +45,124 @@ struct GemvArgs {
   const float* ln_w;
   float* dst;
   int kv_bf16;
+  // IN 3 inputs
+  const float* text_table;
+  const float* codebook;
+  const float* wpe;
+  const float* emb_row;  // drop-in row mode when non-null
+  int slot_arg, pos_arg;
 };
 
-template <int K, int BG, int IN>
-__device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, int g0, int bg, float* red) {
+template <typename TW> struct WReg;
+template <> struct WReg<float> {
+  typedef float4 T;
+  __device__ __forceinline__ static T load(const float* p) { return *reinterpret_cast<const float4*>(p); }
+  __device__ __forceinline__ static float4 f(T v) { return v; }
+  __device__ __forceinline__ static T zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+};
+template <> struct WReg<bf16_t> {
+  typedef uint2 T;
+  __device__ __forceinline__ static T load(const bf16_t* p) { return *reinterpret_cast<const uint2*>(p); }
+  __device__ __forceinline__ static float4 f(T u) {
+    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                       __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+  }
+  __device__ __forceinline__ static T zero() { return make_uint2(0u, 0u); }
+};
+
+// LayerNorm of one 768-row held as 3 float4 per lane (one wave), written to xs
+__device__ __forceinline__ void wave_ln_to_lds(float4 (&v)[3], const float* __restrict__ lnw, float* xs_row, int lane) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+  const float mean = wave_sum(s) * (1.0f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const float dx = v[j].x - mean, dy = v[j].y - mean, dz = v[j].z - mean, dw = v[j].w - mean;
+    q += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+  }
+  const float var = wave_sum(q) * (1.0f / D);
+  const float rstd = 1.0f / sqrtf(var + 1e-5f);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int k = j * 256 + lane * 4;
+    const float4 g = *reinterpret_cast<const float4*>(lnw + k);
+    *reinterpret_cast<float4*>(xs_row + k) =
+        make_float4((v[j].x - mean) * rstd * g.x, (v[j].y - mean) * rstd * g.y, (v[j].z - mean) * rstd * g.z,
+                    (v[j].w - mean) * rstd * g.w);
+  }
+}
+
+template <int K, int IN>
+__device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, int g0, int bg) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  if (IN == 0) {
-    // one wave per row: two-pass mean/var in fp32
-    for (int bb = wave; bb < bg; bb += 4) {
-      const float* xr = a.st.x + (size_t)(g0 + bb) * D;
+  if (IN == 0 || IN == 3) {
+    for (int bb = wave; bb < bg; bb += 4) {  // one wave per row
+      const int b = g0 + bb;
       float4 v[3];
-      float s = 0.f;
+      if (IN == 0) {
+        const float* xr = a.st.x + (size_t)b * D;
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        v[j] = *reinterpret_cast<const float4*>(xr + j * 256 + lane * 4);
-        s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
-      }
-      const float mean = wave_sum(s) * (1.0f / D);
-      float q = 0.f;
+        for (int j = 0; j < 3; ++j) v[j] = *reinterpret_cast<const float4*>(xr + j * 256 + lane * 4);
+      } else if (a.emb_row) {
+        const float* wr = a.wpe + (size_t)a.pos_arg * D;
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        float dx = v[j].x - mean, dy = v[j].y - mean, dz = v[j].z - mean, dw = v[j].w - mean;
-        q += (dx * dx + dy * dy) + (dz * dz + dw * dw);
-      }
-      const float var = wave_sum(q) * (1.0f / D);
-      const float rstd = 1.0f / sqrtf(var + 1e-5f);
+        for (int j = 0; j < 3; ++j) {
+          const int k = j * 256 + lane * 4;
+          const float4 e = *reinterpret_cast<const float4*>(a.emb_row + k);
+          const float4 p = *reinterpret_cast<const float4*>(wr + k);
+          v[j] = make_float4(e.x + p.x, e.y + p.y, e.z + p.z, e.w + p.w);
+        }
+        if (blockIdx.x == 0)
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const int k = j * 256 + lane * 4;
-        const float4 g = *reinterpret_cast<const float4*>(a.ln_w + k);
-        float4 o = make_float4((v[j].x - mean) * rstd * g.x, (v[j].y - mean) * rstd * g.y,
-                               (v[j].z - mean) * rstd * g.z, (v[j].w - mean) * rstd * g.w);
-        *reinterpret_cast<float4*>(xs + bb * K + k) = o;
+          for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + j * 256 + lane * 4) = v[j];
+      } else {
+        const int s = a.st.slots[b];
+        if (s < 0) {
+#pragma unroll
+          for (int j = 0; j < 3; ++j) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+          int p = a.st.pos[s];
+          if (p >= a.st.max_pos) {
+            if (lane == 0 && blockIdx.x == 0) atomicOr(a.st.err, 1);
+            p = a.st.max_pos - 1;
+          }
+          int step = a.st.rowstep[b];
+          if (step >= a.st.plan_stride) {
+            if (lane == 0 && blockIdx.x == 0) atomicOr(a.st.err, 2);
+            step = a.st.plan_stride - 1;
+          }
+          const int tok = min(max(a.st.text_plan[(size_t)b * a.st.plan_stride + step], 0), TEXT_VOCAB - 1);
+          const int prev = min(max(a.st.prev[s], 0), VOCAB - 1);
+          float ss = 0.f;
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            const int k = j * 256 + lane * 4;  // j == 0: text part (k < 256), else speech part
+            if (j == 0) v[j] = *reinterpret_cast<const float4*>(a.text_table + (size_t)tok * TEXT_DIM + k);
+            else if (p == 0) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            else v[j] = *reinterpret_cast<const float4*>(a.codebook + (size_t)prev * SPEECH_DIM + (k - TEXT_DIM));
+            ss += (v[j].x * v[j].x + v[j].y * v[j].y) + (v[j].z * v[j].z + v[j].w * v[j].w);
+          }
+          ss = wave_sum(ss);
+          const float den = fmaxf(sqrtf(ss), 1e-8f);  // F.normalize: x / max(||x||_2, eps)
+          const float* wr = a.wpe + (size_t)p * D;
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            const int k = j * 256 + lane * 4;
+            const float4 pe = *reinterpret_cast<const float4*>(wr + k);
+            v[j] = make_float4(v[j].x / den + pe.x, v[j].y / den + pe.y, v[j].z / den + pe.z, v[j].w / den + pe.w);
+          }
+        }
+        if (blockIdx.x == 0)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = v[j];
       }
+      wave_ln_to_lds(v, a.ln_w, xs + bb * K, lane);
     }
   } else if (IN == 1) {
-    for (int e = tid * 4; e < bg * K; e += 256 * 4) {
+    for (int e = tid * 4; e < bg * K; e += 256 * 4)
       *reinterpret_cast<float4*>(xs + e) = *reinterpret_cast<const float4*>(a.st.h + (size_t)g0 * K + e);
-    }
   } else {
     // merge NSPLIT partials per (b, head): y = sum_s e^{m_s-M} o_s / sum_s e^{m_s-M} l_s
     for (int e = tid; e < bg * D; e += 256) {
@@ -163,53 +187,86 @@ __device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, i
       xs[bb * K + c] = num / den;
     }
   }
-  (void)red;
 }
 
-template <typename TW, int K, int BG, int IN, int OUT, int RPW>
+template <typename TW, int K, int KW, int RPW, int BG, int IN, int OUT>
 __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
+  constexpr int KC = K / KW;     // K columns per wave
+  constexpr int NI = KC / 256;   // 4-element chunks per lane per row
+  constexpr int WROWS = 4 / KW;  // row groups per block
   __shared__ __attribute__((aligned(16))) float xs[BG * K];
-  __shared__ float red[8];
+  __shared__ float part[4][RPW][BG];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int row0 = (blockIdx.x * 4 + wave) * RPW;
+  const int rg = wave / KW, kp = wave % KW;
+  const int row0 = (blockIdx.x * WROWS + rg) * RPW;
   const TW* __restrict__ W = reinterpret_cast<const TW*>(a.W);
+  typename WReg<TW>::T wr[RPW][NI];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int n = row0 + r;
+#pragma unroll
+    for (int it = 0; it < NI; ++it)
+      wr[r][it] = (n < a.N) ? WReg<TW>::load(W + (size_t)n * K + kp * KC + it * 256 + lane * 4) : WReg<TW>::zero();
+  }
   for (int g0 = 0; g0 < a.B; g0 += BG) {
     const int bg = min(BG, a.B - g0);
-    __syncthreads();
-    gemv_stage_input<K, BG, IN>(a, xs, g0, bg, red);
+    if (g0) __syncthreads();
+    gemv_stage_input<K, IN>(a, xs, g0, bg);
     __syncthreads();
     float acc[RPW][BG];
 #pragma unroll
     for (int r = 0; r < RPW; ++r)
 #pragma unroll
       for (int bb = 0; bb < BG; ++bb) acc[r][bb] = 0.f;
-#pragma unroll 3
-    for (int it = 0; it < K / 256; ++it) {
-      const int k = it * 256 + lane * 4;
-      float4 w[RPW];
 #pragma unroll
-      for (int r = 0; r < RPW; ++r) {
-        const int n = row0 + r;
-        w[r] = (n < a.N) ? Ld<TW>::load4(W + (size_t)n * K + k) : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+    for (int it = 0; it < NI; ++it) {
+      const int k = kp * KC + it * 256 + lane * 4;
 #pragma unroll
       for (int bb = 0; bb < BG; ++bb) {
         if (bb < bg) {
           const float4 xv = *reinterpret_cast<const float4*>(xs + bb * K + k);
 #pragma unroll
-          for (int r = 0; r < RPW; ++r)
-            acc[r][bb] += (w[r].x * xv.x + w[r].y * xv.y) + (w[r].z * xv.z + w[r].w * xv.w);
+          for (int r = 0; r < RPW; ++r) {
+            const float4 w = WReg<TW>::f(wr[r][it]);
+            acc[r][bb] += (w.x * xv.x + w.y * xv.y) + (w.z * xv.z + w.w * xv.w);
+          }
         }
       }
     }
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+#pragma unroll
+      for (int bb = 0; bb < BG; ++bb) {
+        if (bb >= bg) continue;
+        const float v = wave_sum(acc[r][bb]);
+        if (KW > 1) {
+          if (lane == 0) part[wave][r][bb] = v;
+        } else {
+          acc[r][bb] = v;
+        }
+      }
+    if (KW > 1) {
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < RPW; ++r)
+#pragma unroll
+        for (int bb = 0; bb < BG; ++bb) {
+          if (bb >= bg) continue;
+          float v = 0.f;
+#pragma unroll
+          for (int q = 0; q < KW; ++q) v += part[rg * KW + q][r][bb];
+          acc[r][bb] = v;
+        }
+    }
+    // epilogue: one lane per (row, batch row); with KW > 1 only the row group's first wave
+    if (KW > 1 && kp != 0) continue;
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
       const int n = row0 + r;
 #pragma unroll
       for (int bb = 0; bb < BG; ++bb) {
-        if (bb >= bg) continue;
-        const float v = wave_sum(acc[r][bb]);
-        if (n >= a.N || lane != ((r * BG + bb) & 63)) continue;
+        if (bb >= bg || n >= a.N || lane != ((r * BG + bb) & 63)) continue;
+        const float v = acc[r][bb];
         const int b = g0 + bb;
         if (OUT == 0) {
           if (n < D) {
@@ -217,9 +274,15 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
           } else {
             const int c = (n - D) % D, which = (n - D) / D;
             const int head = c / HD, d = c - head * HD;
-            const int s = a.st.slots[b];
-            if (s < 0) continue;
-            const int p = min(a.st.pos[s], a.st.max_pos - 1);
+            int s, p;
+            if (IN == 3 && a.emb_row) {
+              s = a.slot_arg;
+              p = a.pos_arg;
+            } else {
+              s = a.st.slots[b];
+              if (s < 0) continue;
+              p = min(a.st.pos[s], a.st.max_pos - 1);
+            }
             const size_t idx =
                 ((((size_t)a.layer * a.st.max_streams + s) * N_HEAD + head) * a.st.max_pos + p) * HD + d;
             if (a.kv_bf16) reinterpret_cast<bf16_t*>(which ? a.st.vc : a.st.kc)[idx] = f32_to_bf16(v);
@@ -237,69 +300,118 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
   }
 }
 
+// drop-in row mode: publish (slot, pos) for the later kernels of the step
+__global__ void ar_row_state_kernel(ArState st, int slot, int pos) {
+  st.slots[0] = slot;
+  st.pos[slot] = pos;
+}
+
 // ---------------------------------------------------------------------------------
-// split-KV decode attention (src/model.py:79-95 with T_q = 1, is_causal False):
-// grid (NSPLIT/4, 8 heads, B), one wave per split. Lane = key for the scores (each lane
-// reads its key's 96-element row), online softmax per wave, P.V with lane = output dim.
+// split-KV decode attention (src/model.py:79-95 with T_q = 1, is_causal False, scale 1/sqrt(96)):
+// grid (NSPLIT, 8 heads, B); a block owns a contiguous key range of its (stream, head) and
+// walks it in 64-key tiles staged through LDS with coalesced 16-B loads. Scores: 4 lanes per
+// key (24 dims each); online softmax across tiles; P.V with one thread per (dim, key half).
 // Partials (m, l, o) are merged in the c_proj prologue.
 // ---------------------------------------------------------------------------------
+constexpr int ATK = 64;        // keys per tile
+constexpr int KS_LD = HD + 1;  // padded K row: conflict-free 4-lanes-per-key reads
+
+template <typename TKV>
+__device__ __forceinline__ void load_piece8(const TKV* p, float* v);
+template <>
+__device__ __forceinline__ void load_piece8<float>(const float* p, float* v) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+template <>
+__device__ __forceinline__ void load_piece8<bf16_t>(const bf16_t* p, float* v) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+  v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+  v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xffff0000u);
+  v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+
 template <typename TKV>
 __global__ __launch_bounds__(256) void ar_attn_kernel(ArState st, int layer) {
   __shared__ __attribute__((aligned(16))) float qs[HD];
-  const int head = blockIdx.y, b = blockIdx.z;
+  __shared__ float Ks[ATK * KS_LD];
+  __shared__ __attribute__((aligned(16))) float Vs[ATK * HD];
+  __shared__ float ps[ATK];
+  __shared__ float red[8];
+  __shared__ float ohalf[HD];
+  const int sp = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int s = st.slots[b];
   if (s < 0) return;
   const int t = min(st.pos[s], st.max_pos - 1) + 1;
-  if (tid < HD) qs[tid] = st.q[(size_t)b * D + head * HD + tid] * 0.10206207261596575f;  // 1/sqrt(96)
-  __syncthreads();
-  const int ns = min(NSPLIT, (t + 63) / 64);
-  const int sp = blockIdx.x * 4 + wave;
+  const int ns = min(NSPLIT, (t + ATK - 1) / ATK);
   if (sp >= ns) return;
   const int chunk = (t + ns - 1) / ns;
   const int k0 = sp * chunk, k1 = min(t, k0 + chunk);
+  if (tid < HD) qs[tid] = st.q[(size_t)b * D + head * HD + tid] * 0.10206207261596575f;  // 96 ** -0.5
   const size_t base = (((size_t)layer * st.max_streams + s) * N_HEAD + head) * st.max_pos;
-  const TKV* __restrict__ K = reinterpret_cast<const TKV*>(st.kc) + base * HD;
-  const TKV* __restrict__ V = reinterpret_cast<const TKV*>(st.vc) + base * HD;
-  float m = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f;
-  for (int kb = k0; kb < k1; kb += 64) {
-    const int key = kb + lane;
-    const bool valid = key < k1;
-    float sc = -INFINITY;
-    if (valid) {
-      const TKV* kr = K + (size_t)key * HD;
-      float a0 = 0.f, a1 = 0.f;
+  const TKV* __restrict__ Kg = reinterpret_cast<const TKV*>(st.kc) + base * HD;
+  const TKV* __restrict__ Vg = reinterpret_cast<const TKV*>(st.vc) + base * HD;
+  const int key = tid >> 2, part = tid & 3;
+  const int od = tid % HD, oh = tid / HD;  // P.V: thread (dim, key half), tid < 192
+  float m = -INFINITY, l = 0.f, o = 0.f;
+  for (int kb = k0; kb < k1; kb += ATK) {
+    const int nk = min(ATK, k1 - kb);
+    __syncthreads();
+    // stage K and V tiles: nk * 96 elements each, 8-element pieces
+    for (int pc = tid; pc < nk * (HD / 8); pc += 256) {
+      const int kk = pc / (HD / 8), d0 = (pc % (HD / 8)) * 8;
+      float v[8];
+      load_piece8<TKV>(Kg + (size_t)(kb + kk) * HD + d0, v);
 #pragma unroll
-      for (int d = 0; d < HD; d += 8) {
-        const float4 k4a = Ld<TKV>::load4(kr + d);
-        const float4 k4b = Ld<TKV>::load4(kr + d + 4);
-        const float4 qa = *reinterpret_cast<const float4*>(qs + d);
-        const float4 qb = *reinterpret_cast<const float4*>(qs + d + 4);
-        a0 += (qa.x * k4a.x + qa.y * k4a.y) + (qa.z * k4a.z + qa.w * k4a.w);
-        a1 += (qb.x * k4b.x + qb.y * k4b.y) + (qb.z * k4b.z + qb.w * k4b.w);
+      for (int i = 0; i < 8; ++i) Ks[kk * KS_LD + d0 + i] = v[i];
+      load_piece8<TKV>(Vg + (size_t)(kb + kk) * HD + d0, v);
+      *reinterpret_cast<float4*>(Vs + kk * HD + d0) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(Vs + kk * HD + d0 + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    }
+    __syncthreads();
+    float sc = -INFINITY;
+    {
+      float acc = 0.f;
+      if (key < nk) {
+        const float* kr = Ks + key * KS_LD + part * 24;
+        const float* qr = qs + part * 24;
+#pragma unroll
+        for (int d = 0; d < 24; ++d) acc += qr[d] * kr[d];
       }
-      sc = a0 + a1;
+      acc += __shfl_xor(acc, 1, 64);
+      acc += __shfl_xor(acc, 2, 64);
+      if (key < nk) sc = acc;
     }
-    const float mt = wave_max(sc);
+    const float wm = wave_max(sc);
+    if (lane == 0) red[wave] = wm;
+    __syncthreads();
+    const float mt = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
     const float mn = fmaxf(m, mt);
-    const float p = valid ? expf(sc - mn) : 0.f;
     const float alpha = (m == -INFINITY) ? 0.f : expf(m - mn);
-    l = l * alpha + wave_sum(p);
-    o0 *= alpha;
-    o1 *= alpha;
-    const int nk = min(64, k1 - kb);
-    for (int j = 0; j < nk; ++j) {
-      const float pj = __shfl(p, j, 64);
-      const TKV* vr = V + (size_t)(kb + j) * HD;
-      o0 += pj * Ld<TKV>::load1(vr + lane);
-      if (lane < HD - 64) o1 += pj * Ld<TKV>::load1(vr + 64 + lane);
+    const float p = (key < nk) ? expf(sc - mn) : 0.f;
+    if (part == 0 && key < ATK) ps[key] = p;
+    const float wsum = wave_sum(part == 0 ? p : 0.f);
+    __syncthreads();  // ps ready; red[0..3] reads done
+    if (lane == 0) red[4 + wave] = wsum;
+    if (tid < 2 * HD) {
+      float acc = 0.f;
+      const int j0 = oh * (ATK / 2), j1 = min(nk, j0 + ATK / 2);
+      for (int j = j0; j < j1; ++j) acc += ps[j] * Vs[j * HD + od];
+      o = o * alpha + acc;
     }
+    __syncthreads();
+    l = l * alpha + ((red[4] + red[5]) + (red[6] + red[7]));
     m = mn;
   }
-  float* po = st.part_o + ((size_t)(b * N_HEAD + head) * NSPLIT + sp) * HD;
-  po[lane] = o0;
-  if (lane < HD - 64) po[64 + lane] = o1;
-  if (lane == 0) {
+  if (tid >= HD && tid < 2 * HD) ohalf[od] = o;
+  __syncthreads();
+  if (tid < HD) {
+    float* po = st.part_o + ((size_t)(b * N_HEAD + head) * NSPLIT + sp) * HD;
+    po[tid] = o + ohalf[tid];
+  }
+  if (tid == 0) {
     float* ml = st.part_ml + ((size_t)(b * N_HEAD + head) * NSPLIT + sp) * 2;
     ml[0] = m;
     ml[1] = l;
@@ -308,42 +420,52 @@ __global__ __launch_bounds__(256) void ar_attn_kernel(ArState st, int layer) {
 
 // ---------------------------------------------------------------------------------
 // greedy select (streaming_server.py:342-347): argmax with first-index ties, top1-top2
-// margin, then the slot's prev token / position advance.
+// margin, then the slot's prev token / position / plan step advance.
 // ---------------------------------------------------------------------------------
+struct Best {
+  float v, v2;
+  int i;
+};
+__device__ __forceinline__ Best best_merge(Best a, Best c) {
+  const bool cb = (c.v > a.v) || (c.v == a.v && c.i < a.i);
+  Best r;
+  if (cb) { r.v = c.v; r.i = c.i; r.v2 = fmaxf(c.v2, a.v); }
+  else { r.v = a.v; r.i = a.i; r.v2 = fmaxf(a.v2, c.v); }
+  return r;
+}
+
 __global__ __launch_bounds__(256) void ar_argmax_kernel(ArState st) {
-  __shared__ float sv[256], sv2[256];
-  __shared__ int si[256];
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const float* lg = st.logits + (size_t)b * VOCAB;
-  float bv = -INFINITY, bv2 = -INFINITY;
-  int bi = 0x7fffffff;
-  for (int i = tid; i < VOCAB; i += 256) {
-    const float v = lg[i];
-    if (v > bv) { bv2 = bv; bv = v; bi = i; }
-    else if (v > bv2) bv2 = v;
+  __shared__ float sv[4], sv2[4];
+  __shared__ int si[4];
+  const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int s = st.slots[b];
+  if (s < 0) return;
+  const float4* lg = reinterpret_cast<const float4*>(st.logits + (size_t)b * VOCAB);
+  Best bt{-INFINITY, -INFINITY, 0x7fffffff};
+#pragma unroll
+  for (int j = 0; j < VOCAB / 1024; ++j) {
+    const float4 v = lg[j * 256 + tid];
+    const int i0 = (j * 256 + tid) * 4;
+    bt = best_merge(bt, Best{v.x, -INFINITY, i0});
+    bt = best_merge(bt, Best{v.y, -INFINITY, i0 + 1});
+    bt = best_merge(bt, Best{v.z, -INFINITY, i0 + 2});
+    bt = best_merge(bt, Best{v.w, -INFINITY, i0 + 3});
   }
-  sv[tid] = bv; sv2[tid] = bv2; si[tid] = bi;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Best c{__shfl_xor(bt.v, o, 64), __shfl_xor(bt.v2, o, 64), __shfl_xor(bt.i, o, 64)};
+    bt = best_merge(bt, c);
+  }
+  if (lane == 0) { sv[wave] = bt.v; sv2[wave] = bt.v2; si[wave] = bt.i; }
   __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
-    if (tid < off) {
-      float av = sv[tid], av2 = sv2[tid]; int ai = si[tid];
-      float cv = sv[tid + off], cv2 = sv2[tid + off]; int ci = si[tid + off];
-      const bool c_better = (cv > av) || (cv == av && ci < ai);
-      float nv, nv2; int ni;
-      if (c_better) { nv = cv; ni = ci; nv2 = fmaxf(cv2, av); }
-      else { nv = av; ni = ai; nv2 = fmaxf(av2, cv); }
-      sv[tid] = nv; sv2[tid] = nv2; si[tid] = ni;
-    }
-    __syncthreads();
-  }
   if (tid == 0) {
-    const int s = st.slots[b];
-    if (s < 0) return;
+    Best r{sv[0], sv2[0], si[0]};
+    for (int w = 1; w < 4; ++w) r = best_merge(r, Best{sv[w], sv2[w], si[w]});
     const int j = st.rowstep[b];
-    if (j >= st.plan_stride) return;  // flagged by the embed kernel
-    st.tok_plan[(size_t)b * st.plan_stride + j] = si[0];
-    if (st.margin_plan) st.margin_plan[(size_t)b * st.plan_stride + j] = sv[0] - sv2[0];
-    st.prev[s] = si[0];
+    if (j >= st.plan_stride) return;  // flagged by the embed prologue
+    st.tok_plan[(size_t)b * st.plan_stride + j] = r.i;
+    if (st.margin_plan) st.margin_plan[(size_t)b * st.plan_stride + j] = r.v - r.v2;
+    st.prev[s] = r.i;
     st.pos[s] = st.pos[s] + 1;
     st.rowstep[b] = j + 1;
   }
@@ -352,56 +474,97 @@ __global__ __launch_bounds__(256) void ar_argmax_kernel(ArState st) {
 // ---------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------
-template <typename TW, int K, int IN, int OUT, int RPW>
-static void launch_gemv_bg(const GemvArgs& a, hipStream_t s) {
-  const int rows_per_block = 4 * RPW;
+template <typename TW, int K, int KW, int RPW, int IN, int OUT>
+static void launch_gemv(const GemvArgs& a, hipStream_t s) {
+  const int rows_per_block = (4 / KW) * RPW;
   dim3 grid((a.N + rows_per_block - 1) / rows_per_block);
   constexpr int BGMAX = (K == 768) ? 16 : 4;
-  if (a.B <= 1) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, 1, IN, OUT, RPW>), grid, dim3(256), 0, s, a);
-  else if (a.B <= 2) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, 2, IN, OUT, RPW>), grid, dim3(256), 0, s, a);
-  else if (a.B <= 4 || BGMAX == 4) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, 4, IN, OUT, RPW>), grid, dim3(256), 0, s, a);
-  else if (a.B <= 8) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, (BGMAX >= 8 ? 8 : 4), IN, OUT, RPW>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((ar_gemv_kernel<TW, K, BGMAX, IN, OUT, RPW>), grid, dim3(256), 0, s, a);
+  if (a.B <= 1) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 1, IN, OUT>), grid, dim3(256), 0, s, a);
+  else if (a.B <= 2) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 2, IN, OUT>), grid, dim3(256), 0, s, a);
+  else if (a.B <= 4 || BGMAX == 4) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 4, IN, OUT>), grid, dim3(256), 0, s, a);
+  else if (a.B <= 8) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, (BGMAX >= 8 ? 8 : 4), IN, OUT>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, BGMAX, IN, OUT>), grid, dim3(256), 0, s, a);
 }
 
 template <typename TW>
-static void ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B, float* logits_dst,
-                      hipStream_t s) {
+static void ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B, const float* emb_row, int slot,
+                      int pos, float* logits_dst, hipStream_t s) {
   GemvArgs a{};
   a.st = st;
   a.B = B;
   a.kv_bf16 = kvdtype == LVX_DTYPE_BF16;
+  a.text_table = w.text_table;
+  a.codebook = w.codebook;
+  a.wpe = w.wpe;
+  a.emb_row = emb_row;
+  a.slot_arg = slot;
+  a.pos_arg = pos;
   for (int l = 0; l < N_LAYER; ++l) {
     a.layer = l;
-    // LN1 + c_attn (+ KV append)
+    // (layer 0: embed) + LN1 + c_attn + KV append
     a.W = w.w_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
-    launch_gemv_bg<TW, 768, 0, 0, 2>(a, s);
+    if (l == 0) launch_gemv<TW, 768, 1, 2, 3, 0>(a, s);
+    else launch_gemv<TW, 768, 1, 2, 0, 0>(a, s);
+    if (l == 0 && emb_row) hipLaunchKernelGGL(ar_row_state_kernel, dim3(1), dim3(1), 0, s, st, slot, pos);
     if (kvdtype == LVX_DTYPE_BF16)
-      hipLaunchKernelGGL((ar_attn_kernel<bf16_t>), dim3(NSPLIT / 4, N_HEAD, B), dim3(256), 0, s, st, l);
+      hipLaunchKernelGGL((ar_attn_kernel<bf16_t>), dim3(NSPLIT, N_HEAD, B), dim3(256), 0, s, st, l);
     else
-      hipLaunchKernelGGL((ar_attn_kernel<float>), dim3(NSPLIT / 4, N_HEAD, B), dim3(256), 0, s, st, l);
+      hipLaunchKernelGGL((ar_attn_kernel<float>), dim3(NSPLIT, N_HEAD, B), dim3(256), 0, s, st, l);
     a.W = w.w_aproj[l]; a.N = D;
-    launch_gemv_bg<TW, 768, 2, 1, 1>(a, s);
+    launch_gemv<TW, 768, 1, 1, 2, 1>(a, s);
     a.W = w.w_fc[l]; a.N = DFF; a.ln_w = w.ln2[l];
-    launch_gemv_bg<TW, 768, 0, 2, 2>(a, s);
+    launch_gemv<TW, 768, 1, 2, 0, 2>(a, s);
     a.W = w.w_mproj[l]; a.N = D;
-    launch_gemv_bg<TW, 3072, 1, 1, 1>(a, s);
+    launch_gemv<TW, 3072, 4, 2, 1, 1>(a, s);
   }
   a.W = w.w_lm; a.N = VOCAB; a.ln_w = w.lnf; a.dst = logits_dst;
-  launch_gemv_bg<TW, 768, 0, 3, 2>(a, s);
+  launch_gemv<TW, 768, 1, 2, 0, 3>(a, s);
+}
+
+// Launch one kernel class of the decode step `iters` times (bench.py times it with HIP events):
+// 0 c_attn(+embed, layer 0)  1 attention  2 c_proj(+merge)  3 c_fc  4 mlp c_proj  5 lm_head  6 argmax
+template <typename TW>
+static int ar_probe_impl(const ArWeights& w, const ArState& st, int kvdtype, int B, int which, int iters,
+                         hipStream_t s) {
+  GemvArgs a{};
+  a.st = st;
+  a.B = B;
+  a.kv_bf16 = kvdtype == LVX_DTYPE_BF16;
+  a.text_table = w.text_table;
+  a.codebook = w.codebook;
+  a.wpe = w.wpe;
+  a.layer = 1;
+  for (int i = 0; i < iters; ++i) {
+    switch (which) {
+      case 0: a.W = w.w_attn[1]; a.N = 3 * D; a.ln_w = w.ln1[1]; launch_gemv<TW, 768, 1, 2, 0, 0>(a, s); break;
+      case 1:
+        if (kvdtype == LVX_DTYPE_BF16)
+          hipLaunchKernelGGL((ar_attn_kernel<bf16_t>), dim3(NSPLIT, N_HEAD, B), dim3(256), 0, s, st, 1);
+        else
+          hipLaunchKernelGGL((ar_attn_kernel<float>), dim3(NSPLIT, N_HEAD, B), dim3(256), 0, s, st, 1);
+        break;
+      case 2: a.W = w.w_aproj[1]; a.N = D; launch_gemv<TW, 768, 1, 1, 2, 1>(a, s); break;
+      case 3: a.W = w.w_fc[1]; a.N = DFF; a.ln_w = w.ln2[1]; launch_gemv<TW, 768, 1, 2, 0, 2>(a, s); break;
+      case 4: a.W = w.w_mproj[1]; a.N = D; launch_gemv<TW, 3072, 4, 2, 1, 1>(a, s); break;
+      case 5: a.W = w.w_lm; a.N = VOCAB; a.ln_w = w.lnf; a.dst = st.logits; launch_gemv<TW, 768, 1, 2, 0, 3>(a, s); break;
+      default: return -1;
+    }
+  }
+  return 0;
+}
+
+int ar_probe(const ArWeights& w, const ArState& st, int wdtype, int kvdtype, int B, int which, int iters,
+             hipStream_t s) {
+  return wdtype == LVX_DTYPE_BF16 ? ar_probe_impl<bf16_t>(w, st, kvdtype, B, which, iters, s)
+                                  : ar_probe_impl<float>(w, st, kvdtype, B, which, iters, s);
 }
 
 void ar_launch_step(const ArWeights& w, const ArState& st, int wdtype, int kvdtype, int B, int mode,
                     const float* emb_row, int slot, int pos, float* logits_out, hipStream_t s) {
-  if (mode == 0)
-    hipLaunchKernelGGL((ar_embed_kernel<0>), dim3(B), dim3(256), 0, s, st, w.text_table, w.codebook, w.wpe,
-                       nullptr, 0, 0);
-  else
-    hipLaunchKernelGGL((ar_embed_kernel<1>), dim3(1), dim3(256), 0, s, st, w.text_table, w.codebook, w.wpe,
-                       emb_row, slot, pos);
   float* dst = mode == 0 ? st.logits : logits_out;
-  if (wdtype == LVX_DTYPE_BF16) ar_layers<bf16_t>(w, st, kvdtype, B, dst, s);
-  else ar_layers<float>(w, st, kvdtype, B, dst, s);
+  const float* er = mode == 0 ? nullptr : emb_row;
+  if (wdtype == LVX_DTYPE_BF16) ar_layers<bf16_t>(w, st, kvdtype, B, er, slot, pos, dst, s);
+  else ar_layers<float>(w, st, kvdtype, B, er, slot, pos, dst, s);
   if (mode == 0) hipLaunchKernelGGL(ar_argmax_kernel, dim3(B), dim3(256), 0, s, st);
 }
 

@@ -523,6 +523,18 @@ int lvx_check_errors(lvx_ctx* c, void* stream) {
   return LVX_OK;
 }
 
+int lvx_probe_kernel(lvx_ctx* c, int which, int B, const int32_t* slots, int iters, void* stream) {
+  NEED_FINAL(c);
+  if (B < 1 || B > c->cfg.max_streams || !slots || iters < 1) return fail(LVX_E_ARG, "bad probe arguments");
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  ArState st = c->st;
+  st.slots = const_cast<int32_t*>(slots);
+  if (ar_probe(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, which, iters, (hipStream_t)stream))
+    return fail(LVX_E_ARG, "unknown probe kernel id");
+  HIP_TRY(hipGetLastError());
+  return LVX_OK;
+}
+
 static int codec_check(lvx_ctx* c, int B, int L, int bw) {
   if (B < 1 || L < 1) return fail(LVX_E_ARG, "B and L must be >= 1");
   if ((long long)B * L > c->cfg.max_codec_frames)

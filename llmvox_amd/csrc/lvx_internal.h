@@ -57,6 +57,8 @@ struct ArState {
 void ar_launch_step(const ArWeights& w, const ArState& st, int wdtype, int kvdtype, int B, int mode,
                     const float* emb_row, int slot, int pos, float* logits_out, hipStream_t s);
 
+int ar_probe(const ArWeights& w, const ArState& st, int wdtype, int kvdtype, int B, int which, int iters,
+             hipStream_t s);
 void launch_set_slot(int32_t* pos, int32_t* prev, int slot, int p, int tok, hipStream_t s);
 void launch_text_embed(const float* table, const int64_t* ids, int n, float* out, hipStream_t s);
 void launch_codes_to_features(const float* codebook, const int64_t* codes, int B, int L, float* feats,

@@ -100,6 +100,9 @@ class Engine:
         _lib.check(self.lib.lvx_ar_steps(self.h, n_steps, B, _ptr(slots), _ptr(text_plan), stride, _ptr(rowstep),
                                          _ptr(tok_plan), _ptr(margin_plan), self.stream_handle()))
 
+    def probe_kernel(self, which: int, slots: torch.Tensor, iters: int):
+        _lib.check(self.lib.lvx_probe_kernel(self.h, which, slots.numel(), _ptr(slots), iters, self.stream_handle()))
+
     def check_errors(self):
         _lib.check(self.lib.lvx_check_errors(self.h, self.stream_handle()))
 
