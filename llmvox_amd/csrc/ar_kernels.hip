@@ -50,7 +50,6 @@ struct GemvArgs {
   const float* codebook;
   const float* wpe;
   const float* emb_row;  // drop-in row mode when non-null
-  int slot_arg, pos_arg;
 };
 
 template <typename TW> struct WReg;
@@ -95,7 +94,7 @@ __device__ __forceinline__ void wave_ln_to_lds(float4 (&v)[3], const float* __re
 }
 
 template <int K, int IN>
-__device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, int g0, int bg) {
+__device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, float* aux, int g0, int bg) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   if (IN == 0 || IN == 3) {
     for (int bb = wave; bb < bg; bb += 4) {  // one wave per row
@@ -105,36 +104,31 @@ __device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, i
         const float* xr = a.st.x + (size_t)b * D;
 #pragma unroll
         for (int j = 0; j < 3; ++j) v[j] = *reinterpret_cast<const float4*>(xr + j * 256 + lane * 4);
-      } else if (a.emb_row) {
-        const float* wr = a.wpe + (size_t)a.pos_arg * D;
+      } else if (a.emb_row) {  // drop-in row forward: caller's normalised row + wpe[pos]
+        const int p = a.st.rowinfo[0].y;
+        const float* wr = a.wpe + (size_t)p * D;
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           const int k = j * 256 + lane * 4;
           const float4 e = *reinterpret_cast<const float4*>(a.emb_row + k);
-          const float4 p = *reinterpret_cast<const float4*>(wr + k);
-          v[j] = make_float4(e.x + p.x, e.y + p.y, e.z + p.z, e.w + p.w);
+          const float4 pe = *reinterpret_cast<const float4*>(wr + k);
+          v[j] = make_float4(e.x + pe.x, e.y + pe.y, e.z + pe.z, e.w + pe.w);
         }
         if (blockIdx.x == 0)
 #pragma unroll
           for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + j * 256 + lane * 4) = v[j];
       } else {
-        const int s = a.st.slots[b];
-        if (s < 0) {
+        const int4 ri = a.st.rowinfo[b];  // {slot, pos, text id, prev token}, validated by the producer
+        if (ri.x < 0) {
 #pragma unroll
           for (int j = 0; j < 3; ++j) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
         } else {
-          int p = a.st.pos[s];
-          if (p >= a.st.max_pos) {
-            if (lane == 0 && blockIdx.x == 0) atomicOr(a.st.err, 1);
-            p = a.st.max_pos - 1;
-          }
-          int step = a.st.rowstep[b];
-          if (step >= a.st.plan_stride) {
+          const int p = ri.y, prev = ri.w;
+          int tok = ri.z;
+          if (tok < 0) {
             if (lane == 0 && blockIdx.x == 0) atomicOr(a.st.err, 2);
-            step = a.st.plan_stride - 1;
+            tok = 384;
           }
-          const int tok = min(max(a.st.text_plan[(size_t)b * a.st.plan_stride + step], 0), TEXT_VOCAB - 1);
-          const int prev = min(max(a.st.prev[s], 0), VOCAB - 1);
           float ss = 0.f;
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
@@ -164,27 +158,48 @@ __device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, i
     for (int e = tid * 4; e < bg * K; e += 256 * 4)
       *reinterpret_cast<float4*>(xs + e) = *reinterpret_cast<const float4*>(a.st.h + (size_t)g0 * K + e);
   } else {
-    // merge NSPLIT partials per (b, head): y = sum_s e^{m_s-M} o_s / sum_s e^{m_s-M} l_s
+    // merge the split-KV partials: y = sum_s c_s o_s, c_s = e^{m_s - M} / sum_s' e^{m_s' - M} l_s'.
+    // Phase A: one thread per (row, head) turns the (m, l) pairs into coefficients (zero for unused
+    // splits); phase B: every element sums all NSPLIT partials unconditionally (part_o is zeroed at
+    // allocation, so unused splits hold finite values), one round trip of independent loads.
+    for (int q = tid; q < bg * N_HEAD; q += 256) {
+      const int bb = q / N_HEAD, head = q - bb * N_HEAD, b = g0 + bb;
+      const int4 ri = a.st.rowinfo[b];
+      float* cf = aux + q * NSPLIT;
+      const int t = ri.y + 1;
+      const int ns = ri.x < 0 ? 0 : min(NSPLIT, (t + 63) / 64);
+      const float* ml = a.st.part_ml + ((size_t)(b * N_HEAD + head) * NSPLIT) * 2;
+      float m[NSPLIT], l[NSPLIT];
+#pragma unroll
+      for (int i = 0; i < NSPLIT; ++i) { m[i] = ml[2 * i]; l[i] = ml[2 * i + 1]; }
+      float M = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < NSPLIT; ++i) if (i < ns) M = fmaxf(M, m[i]);
+      float den = 0.f;
+#pragma unroll
+      for (int i = 0; i < NSPLIT; ++i) {
+        const float f = (i < ns && m[i] != -INFINITY) ? expf(m[i] - M) : 0.f;
+        m[i] = f;
+        den += f * l[i];
+      }
+      const float inv = ns ? 1.0f / den : 0.f;
+#pragma unroll
+      for (int i = 0; i < NSPLIT; ++i) cf[i] = m[i] * inv;
+    }
+    __syncthreads();
     for (int e = tid; e < bg * D; e += 256) {
       const int bb = e / D, c = e - bb * D;
       const int b = g0 + bb;
       const int head = c / HD, d = c - head * HD;
-      const int s = a.st.slots[b];
-      if (s < 0) { xs[bb * K + c] = 0.f; continue; }
-      const int t = min(a.st.pos[s], a.st.max_pos - 1) + 1;
-      const int ns = min(NSPLIT, (t + 63) / 64);
-      const float* ml = a.st.part_ml + ((size_t)(b * N_HEAD + head) * NSPLIT) * 2;
+      const float* cf = aux + (bb * N_HEAD + head) * NSPLIT;
       const float* po = a.st.part_o + ((size_t)(b * N_HEAD + head) * NSPLIT) * HD + d;
-      float M = -INFINITY;
-      for (int i = 0; i < ns; ++i) M = fmaxf(M, ml[2 * i]);
-      float num = 0.f, den = 0.f;
-      for (int i = 0; i < ns; ++i) {
-        const float m = ml[2 * i];
-        const float f = (m == -INFINITY) ? 0.f : expf(m - M);
-        num += f * po[(size_t)i * HD];
-        den += f * ml[2 * i + 1];
-      }
-      xs[bb * K + c] = num / den;
+      float pv[NSPLIT];
+#pragma unroll
+      for (int i = 0; i < NSPLIT; ++i) pv[i] = po[(size_t)i * HD];
+      float y = 0.f;
+#pragma unroll
+      for (int i = 0; i < NSPLIT; ++i) y += cf[i] * pv[i];
+      xs[bb * K + c] = y;
     }
   }
 }
@@ -196,6 +211,7 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
   constexpr int WROWS = 4 / KW;  // row groups per block
   __shared__ __attribute__((aligned(16))) float xs[BG * K];
   __shared__ float part[4][RPW][BG];
+  __shared__ float aux[IN == 2 ? BG * N_HEAD * NSPLIT : 1];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int rg = wave / KW, kp = wave % KW;
   const int row0 = (blockIdx.x * WROWS + rg) * RPW;
@@ -211,7 +227,7 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
   for (int g0 = 0; g0 < a.B; g0 += BG) {
     const int bg = min(BG, a.B - g0);
     if (g0) __syncthreads();
-    gemv_stage_input<K, IN>(a, xs, g0, bg);
+    gemv_stage_input<K, IN>(a, xs, aux, g0, bg);
     __syncthreads();
     float acc[RPW][BG];
 #pragma unroll
@@ -274,15 +290,9 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
           } else {
             const int c = (n - D) % D, which = (n - D) / D;
             const int head = c / HD, d = c - head * HD;
-            int s, p;
-            if (IN == 3 && a.emb_row) {
-              s = a.slot_arg;
-              p = a.pos_arg;
-            } else {
-              s = a.st.slots[b];
-              if (s < 0) continue;
-              p = min(a.st.pos[s], a.st.max_pos - 1);
-            }
+            const int4 ri = a.st.rowinfo[b];
+            const int s = ri.x, p = ri.y;
+            if (s < 0) continue;
             const size_t idx =
                 ((((size_t)a.layer * a.st.max_streams + s) * N_HEAD + head) * a.st.max_pos + p) * HD + d;
             if (a.kv_bf16) reinterpret_cast<bf16_t*>(which ? a.st.vc : a.st.kc)[idx] = f32_to_bf16(v);
@@ -300,9 +310,33 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
   }
 }
 
-// drop-in row mode: publish (slot, pos) for the later kernels of the step
+// Per-row control record of the step in flight: {slot, pos, text id, prev token}. Built once per
+// lvx_ar_steps call (then advanced by the argmax kernel of every step), so the kernels of a step read
+// one 16-byte record instead of chasing slots -> pos / prev / rowstep -> text_plan.
+// text id -1 marks "past the end of the plan": reported by the step that would consume it.
+__device__ __forceinline__ int4 make_rowinfo(const ArState& st, int b, int s, int p, int j, int prev) {
+  if (s < 0) return make_int4(-1, 0, 0, 0);
+  if (p >= st.max_pos) {
+    atomicOr(st.err, 1);
+    p = st.max_pos - 1;
+  }
+  int tok = 384;  // no plan bound (measurement probes): PAD
+  if (st.text_plan)
+    tok = (j < st.plan_stride) ? min(max(st.text_plan[(size_t)b * st.plan_stride + j], 0), TEXT_VOCAB - 1) : -1;
+  return make_int4(s, p, tok, min(max(prev, 0), VOCAB - 1));
+}
+
+__global__ void ar_rowinfo_init_kernel(ArState st, int B) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int s = st.slots[b];
+  const int j = st.rowstep ? st.rowstep[b] : 0;
+  st.rowinfo[b] = s < 0 ? make_int4(-1, 0, 0, 0) : make_rowinfo(st, b, s, st.pos[s], j, st.prev[s]);
+}
+
+// drop-in row mode: publish (slot, pos) for the kernels of the step
 __global__ void ar_row_state_kernel(ArState st, int slot, int pos) {
-  st.slots[0] = slot;
+  st.rowinfo[0] = make_int4(slot, pos, 0, 0);
   st.pos[slot] = pos;
 }
 
@@ -332,8 +366,31 @@ __device__ __forceinline__ void load_piece8<bf16_t>(const bf16_t* p, float* v) {
   v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xffff0000u);
 }
 
+template <typename TKV> struct KvPiece;
+template <> struct KvPiece<float> {
+  float4 a, b;
+  __device__ __forceinline__ void load(const float* p) {
+    a = *reinterpret_cast<const float4*>(p);
+    b = *reinterpret_cast<const float4*>(p + 4);
+  }
+  __device__ __forceinline__ void get(float* v) const {
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+};
+template <> struct KvPiece<bf16_t> {
+  uint4 u;
+  __device__ __forceinline__ void load(const bf16_t* p) { u = *reinterpret_cast<const uint4*>(p); }
+  __device__ __forceinline__ void get(float* v) const {
+    v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+    v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+    v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xffff0000u);
+    v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xffff0000u);
+  }
+};
+
 template <typename TKV>
 __global__ __launch_bounds__(256) void ar_attn_kernel(ArState st, int layer) {
+  constexpr int PPT = ATK * (HD / 8) / 256;  // 8-element pieces per thread per tile (3)
   __shared__ __attribute__((aligned(16))) float qs[HD];
   __shared__ float Ks[ATK * KS_LD];
   __shared__ __attribute__((aligned(16))) float Vs[ATK * HD];
@@ -342,35 +399,53 @@ __global__ __launch_bounds__(256) void ar_attn_kernel(ArState st, int layer) {
   __shared__ float ohalf[HD];
   const int sp = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int s = st.slots[b];
+  const int4 ri = st.rowinfo[b];
+  const int s = ri.x;
   if (s < 0) return;
-  const int t = min(st.pos[s], st.max_pos - 1) + 1;
+  const int t = ri.y + 1;
   const int ns = min(NSPLIT, (t + ATK - 1) / ATK);
   if (sp >= ns) return;
   const int chunk = (t + ns - 1) / ns;
   const int k0 = sp * chunk, k1 = min(t, k0 + chunk);
-  if (tid < HD) qs[tid] = st.q[(size_t)b * D + head * HD + tid] * 0.10206207261596575f;  // 96 ** -0.5
   const size_t base = (((size_t)layer * st.max_streams + s) * N_HEAD + head) * st.max_pos;
   const TKV* __restrict__ Kg = reinterpret_cast<const TKV*>(st.kc) + base * HD;
   const TKV* __restrict__ Vg = reinterpret_cast<const TKV*>(st.vc) + base * HD;
+  // register-staged tile pipeline: tile i+1 is loaded while tile i is computed
+  KvPiece<TKV> kp[PPT], vp[PPT];
+  auto issue = [&](int kb) {
+    const int nk = min(ATK, k1 - kb);
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int pc = tid + 256 * i, kk = pc / (HD / 8), d0 = (pc % (HD / 8)) * 8;
+      if (kk < nk) {
+        kp[i].load(Kg + (size_t)(kb + kk) * HD + d0);
+        vp[i].load(Vg + (size_t)(kb + kk) * HD + d0);
+      }
+    }
+  };
+  issue(k0);
+  if (tid < HD) qs[tid] = st.q[(size_t)b * D + head * HD + tid] * 0.10206207261596575f;  // 96 ** -0.5
   const int key = tid >> 2, part = tid & 3;
   const int od = tid % HD, oh = tid / HD;  // P.V: thread (dim, key half), tid < 192
   float m = -INFINITY, l = 0.f, o = 0.f;
   for (int kb = k0; kb < k1; kb += ATK) {
     const int nk = min(ATK, k1 - kb);
-    __syncthreads();
-    // stage K and V tiles: nk * 96 elements each, 8-element pieces
-    for (int pc = tid; pc < nk * (HD / 8); pc += 256) {
-      const int kk = pc / (HD / 8), d0 = (pc % (HD / 8)) * 8;
-      float v[8];
-      load_piece8<TKV>(Kg + (size_t)(kb + kk) * HD + d0, v);
+    __syncthreads();  // previous tile's LDS reads are done
 #pragma unroll
-      for (int i = 0; i < 8; ++i) Ks[kk * KS_LD + d0 + i] = v[i];
-      load_piece8<TKV>(Vg + (size_t)(kb + kk) * HD + d0, v);
-      *reinterpret_cast<float4*>(Vs + kk * HD + d0) = make_float4(v[0], v[1], v[2], v[3]);
-      *reinterpret_cast<float4*>(Vs + kk * HD + d0 + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    for (int i = 0; i < PPT; ++i) {
+      const int pc = tid + 256 * i, kk = pc / (HD / 8), d0 = (pc % (HD / 8)) * 8;
+      if (kk < nk) {
+        float v[8];
+        kp[i].get(v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) Ks[kk * KS_LD + d0 + e] = v[e];
+        vp[i].get(v);
+        *reinterpret_cast<float4*>(Vs + kk * HD + d0) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(Vs + kk * HD + d0 + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
     }
     __syncthreads();
+    if (kb + ATK < k1) issue(kb + ATK);
     float sc = -INFINITY;
     {
       float acc = 0.f;
@@ -391,17 +466,16 @@ __global__ __launch_bounds__(256) void ar_attn_kernel(ArState st, int layer) {
     const float mn = fmaxf(m, mt);
     const float alpha = (m == -INFINITY) ? 0.f : expf(m - mn);
     const float p = (key < nk) ? expf(sc - mn) : 0.f;
-    if (part == 0 && key < ATK) ps[key] = p;
+    if (part == 0) ps[key] = p;
     const float wsum = wave_sum(part == 0 ? p : 0.f);
-    __syncthreads();  // ps ready; red[0..3] reads done
     if (lane == 0) red[4 + wave] = wsum;
+    __syncthreads();  // ps and the tile sums are visible
     if (tid < 2 * HD) {
       float acc = 0.f;
       const int j0 = oh * (ATK / 2), j1 = min(nk, j0 + ATK / 2);
       for (int j = j0; j < j1; ++j) acc += ps[j] * Vs[j * HD + od];
       o = o * alpha + acc;
     }
-    __syncthreads();
     l = l * alpha + ((red[4] + red[5]) + (red[6] + red[7]));
     m = mn;
   }
@@ -438,7 +512,8 @@ __global__ __launch_bounds__(256) void ar_argmax_kernel(ArState st) {
   __shared__ float sv[4], sv2[4];
   __shared__ int si[4];
   const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int s = st.slots[b];
+  const int4 ri = st.rowinfo[b];
+  const int s = ri.x;
   if (s < 0) return;
   const float4* lg = reinterpret_cast<const float4*>(st.logits + (size_t)b * VOCAB);
   Best bt{-INFINITY, -INFINITY, 0x7fffffff};
@@ -462,12 +537,14 @@ __global__ __launch_bounds__(256) void ar_argmax_kernel(ArState st) {
     Best r{sv[0], sv2[0], si[0]};
     for (int w = 1; w < 4; ++w) r = best_merge(r, Best{sv[w], sv2[w], si[w]});
     const int j = st.rowstep[b];
-    if (j >= st.plan_stride) return;  // flagged by the embed prologue
-    st.tok_plan[(size_t)b * st.plan_stride + j] = r.i;
-    if (st.margin_plan) st.margin_plan[(size_t)b * st.plan_stride + j] = r.v - r.v2;
+    if (j < st.plan_stride) {
+      st.tok_plan[(size_t)b * st.plan_stride + j] = r.i;
+      if (st.margin_plan) st.margin_plan[(size_t)b * st.plan_stride + j] = r.v - r.v2;
+    }
     st.prev[s] = r.i;
-    st.pos[s] = st.pos[s] + 1;
+    st.pos[s] = ri.y + 1;
     st.rowstep[b] = j + 1;
+    st.rowinfo[b] = make_rowinfo(st, b, s, ri.y + 1, j + 1, r.i);
   }
 }
 
@@ -497,15 +574,13 @@ static void ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B,
   a.codebook = w.codebook;
   a.wpe = w.wpe;
   a.emb_row = emb_row;
-  a.slot_arg = slot;
-  a.pos_arg = pos;
+  if (emb_row) hipLaunchKernelGGL(ar_row_state_kernel, dim3(1), dim3(1), 0, s, st, slot, pos);
   for (int l = 0; l < N_LAYER; ++l) {
     a.layer = l;
     // (layer 0: embed) + LN1 + c_attn + KV append
     a.W = w.w_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
     if (l == 0) launch_gemv<TW, 768, 1, 2, 3, 0>(a, s);
     else launch_gemv<TW, 768, 1, 2, 0, 0>(a, s);
-    if (l == 0 && emb_row) hipLaunchKernelGGL(ar_row_state_kernel, dim3(1), dim3(1), 0, s, st, slot, pos);
     if (kvdtype == LVX_DTYPE_BF16)
       hipLaunchKernelGGL((ar_attn_kernel<bf16_t>), dim3(NSPLIT, N_HEAD, B), dim3(256), 0, s, st, l);
     else
@@ -534,6 +609,7 @@ static int ar_probe_impl(const ArWeights& w, const ArState& st, int kvdtype, int
   a.codebook = w.codebook;
   a.wpe = w.wpe;
   a.layer = 1;
+  hipLaunchKernelGGL(ar_rowinfo_init_kernel, dim3((B + 63) / 64), dim3(64), 0, s, st, B);
   for (int i = 0; i < iters; ++i) {
     switch (which) {
       case 0: a.W = w.w_attn[1]; a.N = 3 * D; a.ln_w = w.ln1[1]; launch_gemv<TW, 768, 1, 2, 0, 0>(a, s); break;
@@ -592,6 +668,10 @@ __global__ void codes_to_features_kernel(const float* __restrict__ cb, const int
 __global__ void set_slot_kernel(int32_t* pos, int32_t* prev, int slot, int p, int tok) {
   pos[slot] = p;
   prev[slot] = tok;
+}
+
+void ar_launch_rowinfo_init(const ArState& st, int B, hipStream_t s) {
+  hipLaunchKernelGGL(ar_rowinfo_init_kernel, dim3((B + 63) / 64), dim3(64), 0, s, st, B);
 }
 
 void launch_set_slot(int32_t* pos, int32_t* prev, int slot, int p, int tok, hipStream_t s) {

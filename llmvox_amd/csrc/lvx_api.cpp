@@ -350,8 +350,10 @@ int lvx_finalize(lvx_ctx* c) {
       (r = c->dalloc(&st.err, 4)) || (r = c->dalloc(&st.x, (size_t)S * D)) || (r = c->dalloc(&st.q, (size_t)S * D)) ||
       (r = c->dalloc(&st.part_o, (size_t)S * N_HEAD * NSPLIT * HD)) ||
       (r = c->dalloc(&st.part_ml, (size_t)S * N_HEAD * NSPLIT * 2)) || (r = c->dalloc(&st.h, (size_t)S * DFF)) ||
-      (r = c->dalloc(&st.logits, (size_t)S * VOCAB)))
+      (r = c->dalloc(&st.logits, (size_t)S * VOCAB)) || (r = c->dalloc(&st.rowinfo, S)))
     return r;
+  HIP_TRY(hipMemset(st.part_o, 0, (size_t)S * N_HEAD * NSPLIT * HD * 4));
+  HIP_TRY(hipMemset(st.part_ml, 0, (size_t)S * N_HEAD * NSPLIT * 2 * 4));
   HIP_TRY(hipMemset(st.pos, 0, S * 4));
   HIP_TRY(hipMemset(st.prev, 0, S * 4));
   HIP_TRY(hipMemset(st.err, 0, 16));
@@ -463,12 +465,14 @@ int lvx_ar_forward_row(lvx_ctx* c, int slot, int pos, const float* emb_row, floa
   return LVX_OK;
 }
 
-int lvx_ar_step(lvx_ctx* c, int B, const int32_t* slots, const int32_t* text_plan, int plan_stride,
-                int32_t* rowstep, int32_t* tok_plan, float* margin_plan, void* stream) {
+static int ar_step_impl(lvx_ctx* c, int n_steps, int B, const int32_t* slots, const int32_t* text_plan,
+                        int plan_stride, int32_t* rowstep, int32_t* tok_plan, float* margin_plan, void* stream) {
   NEED_FINAL(c);
   if (B < 1 || B > c->cfg.max_streams) return fail(LVX_E_ARG, "B out of range [1, max_streams]");
   if (plan_stride < 1) return fail(LVX_E_ARG, "plan_stride must be >= 1");
+  if (n_steps < 0) return fail(LVX_E_ARG, "n_steps must be >= 0");
   if (!slots || !text_plan || !rowstep || !tok_plan) return fail(LVX_E_ARG, "null slots/text_plan/rowstep/tok_plan");
+  if (n_steps == 0) return LVX_OK;
   HIP_TRY(hipSetDevice(c->cfg.device));
   ArState st = c->st;
   st.slots = const_cast<int32_t*>(slots);
@@ -478,8 +482,10 @@ int lvx_ar_step(lvx_ctx* c, int B, const int32_t* slots, const int32_t* text_pla
   st.tok_plan = tok_plan;
   st.margin_plan = margin_plan;
   hipStream_t s = (hipStream_t)stream;
+  ar_launch_rowinfo_init(st, B, s);  // per-row control records, then advanced by every step
   if (!c->use_graphs || s == nullptr) {
-    ar_launch_step(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, 0, nullptr, 0, 0, nullptr, s);
+    for (int i = 0; i < n_steps; ++i)
+      ar_launch_step(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, 0, nullptr, 0, 0, nullptr, s);
     HIP_TRY(hipGetLastError());
     return LVX_OK;
   }
@@ -498,15 +504,18 @@ int lvx_ar_step(lvx_ctx* c, int B, const int32_t* slots, const int32_t* text_pla
     c->graph_defs.push_back(g);
     it = c->graphs.emplace(key, ex).first;
   }
-  HIP_TRY(hipGraphLaunch(it->second, s));
+  for (int i = 0; i < n_steps; ++i) HIP_TRY(hipGraphLaunch(it->second, s));
   return LVX_OK;
+}
+
+int lvx_ar_step(lvx_ctx* c, int B, const int32_t* slots, const int32_t* text_plan, int plan_stride,
+                int32_t* rowstep, int32_t* tok_plan, float* margin_plan, void* stream) {
+  return ar_step_impl(c, 1, B, slots, text_plan, plan_stride, rowstep, tok_plan, margin_plan, stream);
 }
 
 int lvx_ar_steps(lvx_ctx* c, int n_steps, int B, const int32_t* slots, const int32_t* text_plan, int plan_stride,
                  int32_t* rowstep, int32_t* tok_plan, float* margin_plan, void* stream) {
-  for (int i = 0; i < n_steps; ++i)
-    if (int r = lvx_ar_step(c, B, slots, text_plan, plan_stride, rowstep, tok_plan, margin_plan, stream)) return r;
-  return LVX_OK;
+  return ar_step_impl(c, n_steps, B, slots, text_plan, plan_stride, rowstep, tok_plan, margin_plan, stream);
 }
 
 int lvx_check_errors(lvx_ctx* c, void* stream) {
@@ -527,7 +536,7 @@ int lvx_probe_kernel(lvx_ctx* c, int which, int B, const int32_t* slots, int ite
   NEED_FINAL(c);
   if (B < 1 || B > c->cfg.max_streams || !slots || iters < 1) return fail(LVX_E_ARG, "bad probe arguments");
   HIP_TRY(hipSetDevice(c->cfg.device));
-  ArState st = c->st;
+  ArState st = c->st;  // no plan bound: text_plan / rowstep / tok_plan stay null
   st.slots = const_cast<int32_t*>(slots);
   if (ar_probe(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, which, iters, (hipStream_t)stream))
     return fail(LVX_E_ARG, "unknown probe kernel id");

@@ -37,6 +37,7 @@ struct ArState {
   int32_t* tok_plan = nullptr;   // [B][plan_stride] greedy token of row b at step j
   float* margin_plan = nullptr;  // [B][plan_stride] top1-top2 logit margin (optional)
   int plan_stride = 1;
+  int4* rowinfo = nullptr;       // [B] {slot, pos, text id, prev token} of the step in flight
   int32_t* pos = nullptr;       // [max_streams] per-slot next position
   int32_t* prev = nullptr;      // [max_streams] per-slot previous token
   int32_t* err = nullptr;       // [1] capacity overflow flag
@@ -59,6 +60,7 @@ void ar_launch_step(const ArWeights& w, const ArState& st, int wdtype, int kvdty
 
 int ar_probe(const ArWeights& w, const ArState& st, int wdtype, int kvdtype, int B, int which, int iters,
              hipStream_t s);
+void ar_launch_rowinfo_init(const ArState& st, int B, hipStream_t s);
 void launch_set_slot(int32_t* pos, int32_t* prev, int slot, int p, int tok, hipStream_t s);
 void launch_text_embed(const float* table, const int64_t* ids, int n, float* out, hipStream_t s);
 void launch_codes_to_features(const float* codebook, const int64_t* codes, int B, int L, float* feats,
