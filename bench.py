@@ -187,12 +187,9 @@ def main():
     for g in range(world * S):
         ids = sentence_ids(SENTENCE if g == 0 else random_sentence(rng))
         plans[g] = plan_for(ids, 0, n_pos)
-    full = torch.from_numpy(plans).to(dev)
-    if dist is not None:  # rank 0 scatters the text-id shards over RCCL
-        mine = torch.empty(S, n_pos, dtype=torch.int32, device=dev)
-        dist.scatter(mine, list(full.split(S)) if rank == 0 else None, src=0)
-    else:
-        mine = full[:S].contiguous()
+    from llmvox_amd.parallel import gather_pcm, scatter_plans
+    # rank 0 scatters the text-id shards over RCCL (the path's inbound exchange)
+    mine = scatter_plans(torch.from_numpy(plans), S, n_pos, dev, dist, rank)
 
     slots = torch.arange(S, dtype=torch.int32, device=dev)
     text_plan = torch.empty(S, chunk, dtype=torch.int32, device=dev)
@@ -200,7 +197,6 @@ def main():
     tok_plan = torch.zeros(S, chunk, dtype=torch.int32, device=dev)
     pcm = torch.empty(S, 320 * chunk, dtype=torch.float32, device=dev)
     pcm_host = torch.empty(S, 320 * chunk, dtype=torch.float32, pin_memory=True)
-    gathered = [torch.empty_like(pcm) for _ in range(world)] if (dist is not None and rank == 0) else None
 
     def run_chunk(c):
         text_plan.copy_(mine[:, c * chunk:(c + 1) * chunk])
@@ -208,7 +204,7 @@ def main():
         eng.ar_steps(chunk, slots, text_plan, rowstep, tok_plan)
         eng.decode_codes(tok_plan, 0, out=pcm)
         if dist is not None:
-            dist.gather(pcm, gathered, dst=0)
+            gather_pcm(pcm, dist, rank, world)  # PCM back to rank 0 (outbound exchange)
         pcm_host.copy_(pcm, non_blocking=True)
 
     def reset_all():

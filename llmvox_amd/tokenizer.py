@@ -5,7 +5,8 @@ and adds "[PAD]" (id 384) then "EOS" (id 385); streaming_server.py:306 calls
 ``tokenizer(word)["input_ids"]``.  ByT5 ids: 0 <pad>, 1 </s>, 2 <unk>, 3 + byte value for
 UTF-8 bytes, 259 + n for <extra_id_n> (n < 125), and "</s>" appended at the end.
 Special tokens are matched in the text (longest match first); "<pad>", "</s>" and "<unk>"
-also swallow the whitespace around them (their AddedToken has lstrip/rstrip=True).
+also swallow the whitespace around them (their AddedToken has lstrip/rstrip=True). The
+trailing </s> is not added again when the ids already end with </s>.
 """
 from __future__ import annotations
 
@@ -47,7 +48,8 @@ class ByteTokenizer:
             pos = m.end()
         if pos < len(text):
             ids.extend(b + 3 for b in text[pos:].encode("utf-8"))
-        ids.append(1)
+        if not ids or ids[-1] != 1:  # ByT5 appends </s> only when the ids do not already end with it
+            ids.append(1)
         return ids
 
     def __call__(self, text: str) -> Dict[str, List[int]]:

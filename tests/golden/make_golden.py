@@ -288,6 +288,13 @@ def main(ref_root="/root/reference"):
         json.dump(tr, f, indent=1)
     print("scheduler traces:", {k: len(v["items"]) for k, v in tr.items()})
 
+    # --- text cleaning (streaming_server.py:106-149)
+    import streaming_server as SS
+    texts = ["  **Hi**  - there #1 & you@x ... 1,000 a/b c\\d 5.", "Step 2. then 3.14 and 2.", "a...b", "x--y",
+             "#tag @me & you", "1,234,567 items", "path/to//file", "it's *fine*", "end.<|eot_id|>"]
+    with open(os.path.join(HERE, "clean_text_golden.json"), "w") as f:
+        json.dump({t: SS.clean_text(t) for t in texts}, f, indent=0)
+
     # --- tokenizer cases
     cases = ["The", "quick", "bank.", "EOS", "a[PAD]b", "é", "</s>x", "<pad>", " hi ", "<extra_id_0>",
              "x<extra_id_5>y", "<unk>", "a EOS b", "EOSEOS", "", "日本", "it's", "3.14", "tide<|eot_id|>",

@@ -1,0 +1,39 @@
+"""Stream sharding: rank 0 scatters text plans and gathers PCM (gloo, world size 2, CPU)."""
+import os
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from llmvox_amd.parallel import gather_pcm, scatter_plans, shard_of
+    S, n_pos = 3, 16
+    full = torch.arange(world * S * n_pos, dtype=torch.int32).view(world * S, n_pos) if rank == 0 else None
+    mine = scatter_plans(full, S, n_pos, "cpu", dist, rank)
+    pcm = mine.float() * 2  # stand-in for this rank's decode
+    got = gather_pcm(pcm, dist, rank, world)
+    if rank == 0:
+        q.put((torch.cat(got).tolist(), [shard_of(g, S) for g in range(world * S)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_scatter_gather_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 1000
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(120)
+        assert p.exitcode == 0
+    gathered, shards = q.get(timeout=10)
+    expect = (torch.arange(2 * 3 * 16, dtype=torch.float32).view(6, 16) * 2).tolist()
+    assert gathered == expect
+    assert shards == [0, 0, 0, 1, 1, 1]

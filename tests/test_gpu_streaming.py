@@ -1,0 +1,126 @@
+"""The scheduler layers on the HIP path: the drop-in ModelHandler under the reference-shaped
+audio_generator_sync, and the fused batched scheduler, against the reference's own stream."""
+import os
+from queue import Queue
+
+import numpy as np
+import pytest
+import torch
+
+from llmvox_amd import streaming as S
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+WORDS = "The quick brown fox jumps over the lazy dog near the river bank.".split(" ")
+
+
+class _Stop(Exception):
+    pass
+
+
+@pytest.fixture(scope="module")
+def handler():
+    from llmvox_amd.handler import ModelHandler
+    from llmvox_amd.config import default_config
+    return ModelHandler(default_config(weight_dtype="fp32", kv_dtype="fp32", max_streams=8, max_positions=2048),
+                        device_id=0)
+
+
+def _run_dropin(h, words, n_calls, index=0, dump=10, config=None):
+    real = h.model
+    calls = {"n": 0}
+
+    def counted(*a, **k):
+        if calls["n"] >= n_calls:
+            raise _Stop()
+        calls["n"] += 1
+        return real(*a, **k)
+
+    h.model = counted
+    tq, aq = Queue(), Queue()
+    for w in words:
+        tq.put(w)
+    try:
+        S.audio_generator_sync(index, dump, h, tq, aq, config=config)
+    except _Stop:
+        pass
+    finally:
+        h.model = real
+    return [aq.get() for _ in range(aq.qsize())]
+
+
+def test_dropin_handler_reproduces_reference_stream(handler):
+    g = np.load(os.path.join(GOLDEN, "stream_golden.npz"))
+    items = _run_dropin(handler, WORDS, int(g["model_calls"]))
+    chunks = [np.frombuffer(b, dtype=np.float32) for b in items]
+    assert [len(c) for c in chunks] == g["sizes"].tolist()
+    for i in range(3):
+        assert np.abs(chunks[i] - g[f"chunk{i}"]).max() < 2e-4
+
+
+def test_fused_scheduler_reproduces_reference_stream(handler):
+    g = np.load(os.path.join(GOLDEN, "stream_golden.npz"))
+    a = np.load(os.path.join(GOLDEN, "ar_golden.npz"))
+    sch = S.FusedScheduler(handler.engine, max_chunk=64)
+    st = sch.open_stream(index=0, dump_size=10)
+    for w in WORDS:
+        st.feed(w)
+    while len([e for e in st.events if isinstance(e, bytes)]) < 3:
+        assert sch.run_chunk() > 0
+    assert st.tokens[:130] == a["ids"][:130].tolist()
+    chunks = [np.frombuffer(e, dtype=np.float32) for e in st.events if isinstance(e, bytes)]
+    for i in range(3):
+        assert len(chunks[i]) == len(g[f"chunk{i}"])
+        assert np.abs(chunks[i] - g[f"chunk{i}"]).max() < 2e-4
+    sch.close_stream(st)
+
+
+def test_fused_rollback_matches_dropin_on_forced_eoa(handler):
+    """Declare the token the model emits at step 23 to be the end-of-audio id: both paths must
+    reset there (signal, flush of the remainder incl. that token, new segment) identically."""
+    a = np.load(os.path.join(GOLDEN, "ar_golden.npz"))
+    eoa = int(a["ids"][23])
+    cfg = {"eoa_token_id": eoa}
+    ref = _run_dropin(handler, WORDS, 120, config=cfg)
+    sch = S.FusedScheduler(handler.engine, max_chunk=32)
+    st = sch.open_stream(index=0, dump_size=10, eoa_id=eoa)
+    for w in WORDS:
+        st.feed(w)
+    while sum(1 for e in st.tokens) < 120:
+        if sch.run_chunk() == 0:
+            break
+    got = st.events[:len(ref)]
+    assert [type(x) for x in got] == [type(x) for x in ref]
+    for x, y in zip(got, ref):
+        if isinstance(x, bytes):
+            xa, ya = np.frombuffer(x, dtype=np.float32), np.frombuffer(y, dtype=np.float32)
+            assert xa.shape == ya.shape and np.abs(xa - ya).max() < 2e-4
+        else:
+            assert x == y
+    sch.close_stream(st)
+
+
+def test_fused_multistream_batch_equals_single(handler):
+    """Four streams batched in one scheduler == each stream alone (streams are independent)."""
+    texts = [WORDS, "a quick test.".split(" "), "hello there world.".split(" "), "one two.".split(" ")]
+    sch = S.FusedScheduler(handler.engine, max_chunk=48)
+    sts = []
+    for i, t in enumerate(texts):
+        st = sch.open_stream(index=i % 2, dump_size=10 if i % 2 == 0 else 160)
+        for w in t:
+            st.feed(w)
+        sts.append(st)
+    for _ in range(6):
+        sch.run_chunk()
+    batched = [list(st.tokens) for st in sts]
+    for st in sts:
+        sch.close_stream(st)
+    for i, t in enumerate(texts):
+        one = S.FusedScheduler(handler.engine, max_chunk=48)
+        st = one.open_stream(index=i % 2, dump_size=10 if i % 2 == 0 else 160)
+        for w in t:
+            st.feed(w)
+        while len(st.tokens) < len(batched[i]):
+            one.run_chunk()
+        assert st.tokens[:len(batched[i])] == batched[i]
+        one.close_stream(st)

@@ -1,0 +1,71 @@
+"""The CPU oracle against the golden vectors produced by the reference itself
+(tests/golden/make_golden.py). This pins the oracle before it is trusted as the checker."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from llmvox_amd import weights as LW
+from oracle import reference_cpu as R
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def W():
+    gw, cw, tt = LW.synthetic_all(1234)
+    return R.to_torch(gw), R.to_torch(cw), torch.from_numpy(tt)
+
+
+def test_ar_ids_and_logits_bitexact(W):
+    g = np.load(os.path.join(GOLDEN, "ar_golden.npz"))
+    Wg, Wc, tt = W
+    n = 96  # keep the CPU suite fast; the full 256 are checked on the GPU
+    ids, margins, logits = R.ar_decode(Wg, tt, Wc[R.CODEBOOK_KEY], g["text_ids"].tolist(), n, record_logits=True)
+    assert ids == g["ids"][:n].tolist()
+    np.testing.assert_allclose(margins, g["margins"][:n], rtol=0, atol=0)
+    for k, step in enumerate(g["logit_steps"]):
+        if step < n:
+            np.testing.assert_array_equal(logits[step].numpy(), g["logits"][k])
+
+
+def test_teacher_forced_equals_kv_decode(W):
+    """Second, independent oracle: the training-form causal full-sequence pass."""
+    g = np.load(os.path.join(GOLDEN, "ar_golden.npz"))
+    Wg, Wc, tt = W
+    n = 80
+    lg = R.teacher_forced_logits(Wg, tt, Wc[R.CODEBOOK_KEY], g["text_ids"].tolist(), g["ids"][:n].tolist())
+    assert lg.argmax(-1).tolist() == g["ids"][:n].tolist()
+    for k, step in enumerate(g["logit_steps"]):
+        if step < n:
+            assert np.abs(lg[step].numpy() - g["logits"][k]).max() < 1e-5
+
+
+@pytest.mark.parametrize("L", [1, 2, 10, 30])
+def test_codec_pcm_bitexact(W, L):
+    c = np.load(os.path.join(GOLDEN, "codec_golden.npz"))
+    _, Wc, _ = W
+    pcm = R.decode_codes(Wc, torch.from_numpy(c[f"codes_{L}"]).long()).numpy()
+    np.testing.assert_array_equal(pcm, c[f"pcm_{L}"])
+
+
+def test_codec_intermediates(W):
+    c = np.load(os.path.join(GOLDEN, "codec_golden.npz"))
+    _, Wc, _ = W
+    feats = R.codes_to_features(Wc, torch.from_numpy(c["codes_10"]).long())
+    np.testing.assert_array_equal(feats.numpy(), c["features_10"])
+    np.testing.assert_array_equal(R.backbone(Wc, feats).numpy(), c["backbone_10"])
+
+
+def test_codes_to_features_rejects_batched_2d(W):
+    """The reference reads a 2-D input as (K, L): [B>1, L] indexes past the single codebook."""
+    _, Wc, _ = W
+    with pytest.raises(IndexError):
+        R.codes_to_features(Wc, torch.zeros(2, 5, dtype=torch.long))
+
+
+def test_istft_envelope_and_length(W):
+    spec = torch.randn(1, 641, 7, dtype=torch.complex64)
+    y = R.istft_same(spec)
+    assert y.shape == (1, 7 * 320)
