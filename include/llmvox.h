@@ -116,6 +116,8 @@ int lvx_stream_set(lvx_ctx* ctx, int slot, int pos, int prev_token, void* stream
 int lvx_probe_kernel(lvx_ctx* ctx, int which, int B, const int32_t* slots_dev, int iters, void* stream);
 /* Host-side view of a slot's position (synchronises the stream). */
 int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
+/* Development switches for in-process A/B timing ("gemv_reg": register-path GEMV for B <= 4). */
+int lvx_set_option(lvx_ctx* ctx, const char* name, int value);
 /* Enable/disable HIP-graph replay of lvx_ar_step for a given B (default on). */
 int lvx_set_graphs(lvx_ctx* ctx, int enable);
 

@@ -310,6 +310,273 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Register-path GEMV for B <= 4 rows (the B = 1 latency path). No LDS and no barrier unless K is
+// split across waves: every wave loads its inputs FIRST (x rows / h chunks / control records),
+// then its weight rows, and computes LayerNorm / the embedding in registers while the weight
+// stream is in flight (vmcnt counts in issue order, so inputs issued first are usable first).
+// The lane layout of the inputs (k = i*256 + lane*4) is the lane layout of the weight chunks.
+// ---------------------------------------------------------------------------------
+template <int OUT>
+__device__ __forceinline__ void gemv_store(const GemvArgs& a, int n, int b, float v) {
+  if (OUT == 0) {
+    if (n < D) {
+      a.st.q[(size_t)b * D + n] = v;
+    } else {
+      const int c = (n - D) % D, which = (n - D) / D;
+      const int head = c / HD, d = c - head * HD;
+      const int4 ri = a.st.rowinfo[b];
+      if (ri.x < 0) return;
+      const size_t idx = ((((size_t)a.layer * a.st.max_streams + ri.x) * N_HEAD + head) * a.st.max_pos + ri.y) * HD + d;
+      if (a.kv_bf16) reinterpret_cast<bf16_t*>(which ? a.st.vc : a.st.kc)[idx] = f32_to_bf16(v);
+      else reinterpret_cast<float*>(which ? a.st.vc : a.st.kc)[idx] = v;
+    }
+  } else if (OUT == 1) {
+    a.st.x[(size_t)b * D + n] += v;
+  } else if (OUT == 2) {
+    a.st.h[(size_t)b * DFF + n] = gelu_tanh(v);
+  } else {
+    a.dst[(size_t)b * a.N + n] = v;
+  }
+}
+
+__device__ __forceinline__ void wave_ln_regs(float4 (&v)[3], const float4 (&g)[3]) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+  const float mean = wave_sum(s) * (1.0f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    v[j].x -= mean; v[j].y -= mean; v[j].z -= mean; v[j].w -= mean;
+    q += (v[j].x * v[j].x + v[j].y * v[j].y) + (v[j].z * v[j].z + v[j].w * v[j].w);
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / D) + 1e-5f);
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+    v[j] = make_float4(v[j].x * rstd * g[j].x, v[j].y * rstd * g[j].y, v[j].z * rstd * g[j].z, v[j].w * rstd * g[j].w);
+}
+
+template <typename TW, int K, int KW, int RPW, int BB, int IN, int OUT>
+__global__ __launch_bounds__(256) void ar_gemv_reg_kernel(GemvArgs a) {
+  static_assert(IN != 2, "the split-KV merge needs the LDS path");
+  static_assert(IN == 1 || KW == 1, "LayerNorm inputs need the whole row in one wave");
+  constexpr int KC = K / KW, NI = KC / 256, WROWS = 4 / KW;
+  __shared__ float part[KW > 1 ? 4 * RPW * BB : 1];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int rg = wave / KW, kp = wave % KW;
+  const int row0 = (blockIdx.x * WROWS + rg) * RPW;
+  const int B = a.B;
+  // 1. inputs first
+  float4 xin[BB][NI];
+  int4 ri[BB];
+  float4 g[3];
+  if (IN == 0 || IN == 3) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) g[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
+  }
+#pragma unroll
+  for (int b = 0; b < BB; ++b) {
+    if (b >= B) continue;
+    if (IN == 0) {
+#pragma unroll
+      for (int i = 0; i < NI; ++i) xin[b][i] = *reinterpret_cast<const float4*>(a.st.x + (size_t)b * D + i * 256 + lane * 4);
+    } else if (IN == 1) {
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+        xin[b][i] = *reinterpret_cast<const float4*>(a.st.h + (size_t)b * K + kp * KC + i * 256 + lane * 4);
+    } else {
+      ri[b] = a.st.rowinfo[b];
+    }
+  }
+  // 2. the weight stream
+  const TW* __restrict__ W = reinterpret_cast<const TW*>(a.W);
+  typename WReg<TW>::T wr[RPW][NI];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int n = row0 + r;
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+      wr[r][i] = (n < a.N) ? WReg<TW>::load(W + (size_t)n * K + kp * KC + i * 256 + lane * 4) : WReg<TW>::zero();
+  }
+  // 3. prologue math in registers
+  if (IN == 3) {
+#pragma unroll
+    for (int b = 0; b < BB; ++b) {
+      if (b >= B) continue;
+      float4 (&v)[NI] = xin[b];
+      if (a.emb_row) {  // drop-in row forward: caller's normalised row + wpe[pos]
+        const float* wr_ = a.wpe + (size_t)ri[b].y * D;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const float4 e = *reinterpret_cast<const float4*>(a.emb_row + j * 256 + lane * 4);
+          const float4 pe = *reinterpret_cast<const float4*>(wr_ + j * 256 + lane * 4);
+          v[j] = make_float4(e.x + pe.x, e.y + pe.y, e.z + pe.z, e.w + pe.w);
+        }
+      } else if (ri[b].x < 0) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        const int p = ri[b].y, prev = ri[b].w;
+        int tok = ri[b].z;
+        if (tok < 0) {
+          if (lane == 0 && blockIdx.x == 0 && wave == 0) atomicOr(a.st.err, 2);
+          tok = 384;
+        }
+        const float* wr_ = a.wpe + (size_t)p * D;
+        float4 pe[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) pe[j] = *reinterpret_cast<const float4*>(wr_ + j * 256 + lane * 4);
+        float ss = 0.f;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const int k = j * 256 + lane * 4;
+          if (j == 0) v[j] = *reinterpret_cast<const float4*>(a.text_table + (size_t)tok * TEXT_DIM + k);
+          else if (p == 0) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+          else v[j] = *reinterpret_cast<const float4*>(a.codebook + (size_t)prev * SPEECH_DIM + (k - TEXT_DIM));
+          ss += (v[j].x * v[j].x + v[j].y * v[j].y) + (v[j].z * v[j].z + v[j].w * v[j].w);
+        }
+        const float den = fmaxf(sqrtf(wave_sum(ss)), 1e-8f);  // F.normalize: x / max(||x||_2, eps)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          v[j] = make_float4(v[j].x / den + pe[j].x, v[j].y / den + pe[j].y, v[j].z / den + pe[j].z, v[j].w / den + pe[j].w);
+      }
+      if (blockIdx.x == 0 && wave == 0)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = v[j];
+    }
+  }
+  if (IN == 0 || IN == 3) {
+#pragma unroll
+    for (int b = 0; b < BB; ++b)
+      if (b < B) wave_ln_regs(reinterpret_cast<float4 (&)[3]>(xin[b]), g);
+  }
+  // 4. FMA
+  float acc[RPW][BB];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r)
+#pragma unroll
+    for (int b = 0; b < BB; ++b) acc[r][b] = 0.f;
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const float4 w = WReg<TW>::f(wr[r][i]);
+#pragma unroll
+      for (int b = 0; b < BB; ++b) {
+        if (b >= B) continue;
+        const float4 xv = xin[b][i];
+        acc[r][b] += (w.x * xv.x + w.y * xv.y) + (w.z * xv.z + w.w * xv.w);
+      }
+    }
+  // 5. reduce (+ combine the K-split waves through LDS)
+#pragma unroll
+  for (int r = 0; r < RPW; ++r)
+#pragma unroll
+    for (int b = 0; b < BB; ++b) {
+      if (b >= B) continue;
+      acc[r][b] = wave_sum(acc[r][b]);
+      if (KW > 1 && lane == 0) part[(wave * RPW + r) * BB + b] = acc[r][b];
+    }
+  if (KW > 1) {
+    __syncthreads();
+    if (kp != 0) return;
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+#pragma unroll
+      for (int b = 0; b < BB; ++b) {
+        if (b >= B) continue;
+        float v = 0.f;
+#pragma unroll
+        for (int q = 0; q < KW; ++q) v += part[((rg * KW + q) * RPW + r) * BB + b];
+        acc[r][b] = v;
+      }
+  }
+  // 6. epilogue
+#pragma unroll
+  for (int r = 0; r < RPW; ++r)
+#pragma unroll
+    for (int b = 0; b < BB; ++b) {
+      const int n = row0 + r;
+      if (b >= B || n >= a.N || lane != ((r * BB + b) & 63)) continue;
+      gemv_store<OUT>(a, n, b, acc[r][b]);
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// c_proj for B = 1 with the split-KV merge in the prologue, one global round trip: every thread
+// issues its partial loads (3 output elements x 16 splits) and one (m, l) pair of the 8 x 16
+// (head, split) table BEFORE the weight rows; the per-head max / denominator are reduced over
+// the 16 lanes of each head with shuffles, the coefficients go through LDS once.
+// ---------------------------------------------------------------------------------
+template <typename TW, int RPW>
+__global__ __launch_bounds__(256) void ar_cproj_b1_kernel(GemvArgs a) {
+  __shared__ float cf[N_HEAD * NSPLIT];
+  __shared__ __attribute__((aligned(16))) float xs[D];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int4 ri = a.st.rowinfo[0];
+  // (m, l) of (head = tid / 16, split = tid % 16) and the 48 partials of this thread's 3 elements
+  float2 ml = make_float2(-INFINITY, 0.f);
+  if (tid < N_HEAD * NSPLIT) ml = reinterpret_cast<const float2*>(a.st.part_ml)[tid];
+  float pv[3][NSPLIT];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int e = tid + 256 * j, head = e / HD, d = e - head * HD;
+    const float* po = a.st.part_o + ((size_t)head * NSPLIT) * HD + d;
+#pragma unroll
+    for (int i = 0; i < NSPLIT; ++i) pv[j][i] = po[(size_t)i * HD];
+  }
+  const int row0 = (blockIdx.x * 4 + wave) * RPW;
+  const TW* __restrict__ W = reinterpret_cast<const TW*>(a.W);
+  typename WReg<TW>::T wr[RPW][3];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r)
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      wr[r][i] = (row0 + r < a.N) ? WReg<TW>::load(W + (size_t)(row0 + r) * D + i * 256 + lane * 4) : WReg<TW>::zero();
+  if (tid < N_HEAD * NSPLIT) {
+    const int t = ri.y + 1;
+    const int ns = ri.x < 0 ? 0 : min(NSPLIT, (t + 63) / 64);
+    const int sp = tid & (NSPLIT - 1);
+    const bool on = sp < ns && ml.x != -INFINITY;
+    float M = on ? ml.x : -INFINITY;
+#pragma unroll
+    for (int o = 1; o < NSPLIT; o <<= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
+    const float f = on ? expf(ml.x - M) : 0.f;
+    float den = f * ml.y;
+#pragma unroll
+    for (int o = 1; o < NSPLIT; o <<= 1) den += __shfl_xor(den, o, 64);
+    cf[tid] = (ns > 0) ? f / den : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int e = tid + 256 * j, head = e / HD;
+    float y = 0.f;
+#pragma unroll
+    for (int i = 0; i < NSPLIT; ++i) y += cf[head * NSPLIT + i] * pv[j][i];
+    xs[e] = y;
+  }
+  __syncthreads();
+  float acc[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) acc[r] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float4 xv = *reinterpret_cast<const float4*>(xs + i * 256 + lane * 4);
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const float4 w = WReg<TW>::f(wr[r][i]);
+      acc[r] += (w.x * xv.x + w.y * xv.y) + (w.z * xv.z + w.w * xv.w);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const float v = wave_sum(acc[r]);
+    if (lane == r && row0 + r < a.N) a.st.x[row0 + r] += v;
+  }
+}
+
 // Per-row control record of the step in flight: {slot, pos, text id, prev token}. Built once per
 // lvx_ar_steps call (then advanced by the argmax kernel of every step), so the kernels of a step read
 // one 16-byte record instead of chasing slots -> pos / prev / rowstep -> text_plan.
@@ -492,6 +759,107 @@ __global__ __launch_bounds__(256) void ar_attn_kernel(ArState st, int layer) {
   }
 }
 
+// Variant 2 (option "attn_v2"): no LDS in the key loop. A block walks its key range in 64-key
+// tiles; lane quad (tid/4) owns one key per tile and lane tid%4 owns 24 of its 96 dims: the K and
+// V pieces (48 B bf16 each) load straight to registers, the score needs two quad shuffles, and
+// every wave keeps its own online-softmax state (m, l, o[24] per lane) so the loop has no
+// barrier. The 4 wave states are merged once at the end through LDS.
+template <typename TKV>
+__global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer) {
+  __shared__ float wm_s[4], wl_s[4];
+  __shared__ float wo_s[4][HD];
+  const int sp = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int4 ri = st.rowinfo[b];
+  const int s = ri.x;
+  if (s < 0) return;
+  const int t = ri.y + 1;
+  const int ns = min(NSPLIT, (t + ATK - 1) / ATK);
+  if (sp >= ns) return;
+  const int chunk = (t + ns - 1) / ns;
+  const int k0 = sp * chunk, k1 = min(t, k0 + chunk);
+  const size_t base = (((size_t)layer * st.max_streams + s) * N_HEAD + head) * st.max_pos;
+  const TKV* __restrict__ Kg = reinterpret_cast<const TKV*>(st.kc) + base * HD;
+  const TKV* __restrict__ Vg = reinterpret_cast<const TKV*>(st.vc) + base * HD;
+  const int part = tid & 3, kq = tid >> 2;  // key slot within the 64-key tile
+  float q[24];
+  {
+    const float* qg = st.q + (size_t)b * D + head * HD + part * 24;
+#pragma unroll
+    for (int i = 0; i < 24; i += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(qg + i);
+      q[i] = v.x * 0.10206207261596575f; q[i + 1] = v.y * 0.10206207261596575f;
+      q[i + 2] = v.z * 0.10206207261596575f; q[i + 3] = v.w * 0.10206207261596575f;
+    }
+  }
+  float m = -INFINITY, l = 0.f, o[24];
+#pragma unroll
+  for (int i = 0; i < 24; ++i) o[i] = 0.f;
+  for (int kb = k0; kb < k1; kb += ATK) {
+    const int key = kb + kq;
+    const bool valid = key < k1;
+    float kf[24], vf[24];
+    if (valid) {
+      KvPiece<TKV> kp[3], vp[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        kp[i].load(Kg + (size_t)key * HD + part * 24 + i * 8);
+        vp[i].load(Vg + (size_t)key * HD + part * 24 + i * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) { kp[i].get(kf + 8 * i); vp[i].get(vf + 8 * i); }
+    }
+    float sc = 0.f;
+    if (valid) {
+#pragma unroll
+      for (int i = 0; i < 24; ++i) sc += q[i] * kf[i];
+    }
+    sc += __shfl_xor(sc, 1, 64);
+    sc += __shfl_xor(sc, 2, 64);
+    if (!valid) sc = -INFINITY;
+    const float mn = fmaxf(m, wave_max(sc));
+    if (mn == -INFINITY) continue;  // this wave has no key in this tile yet (wave-uniform)
+    const float alpha = (m == -INFINITY) ? 0.f : expf(m - mn);
+    const float p = valid ? expf(sc - mn) : 0.f;
+    l = l * alpha + wave_sum(part == 0 ? p : 0.f);
+#pragma unroll
+    for (int i = 0; i < 24; ++i) o[i] = o[i] * alpha + (valid ? p * vf[i] : 0.f);
+    m = mn;
+  }
+  // sum o over the 16 key slots of the wave (lanes with equal part)
+#pragma unroll
+  for (int i = 0; i < 24; ++i) {
+    float v = o[i];
+    v += __shfl_xor(v, 4, 64);
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    o[i] = v;
+  }
+  if (lane < 4) {
+#pragma unroll
+    for (int i = 0; i < 24; ++i) wo_s[wave][lane * 24 + i] = o[i];
+  }
+  if (lane == 0) { wm_s[wave] = m; wl_s[wave] = l; }
+  __syncthreads();
+  if (tid < HD) {
+    const float M = fmaxf(fmaxf(wm_s[0], wm_s[1]), fmaxf(wm_s[2], wm_s[3]));
+    float ov = 0.f, lv = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float f = (wm_s[w] == -INFINITY) ? 0.f : expf(wm_s[w] - M);
+      ov += f * wo_s[w][tid];
+      lv += f * wl_s[w];
+    }
+    st.part_o[((size_t)(b * N_HEAD + head) * NSPLIT + sp) * HD + tid] = ov;
+    if (tid == 0) {
+      float* ml = st.part_ml + ((size_t)(b * N_HEAD + head) * NSPLIT + sp) * 2;
+      ml[0] = M;
+      ml[1] = lv;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------
 // greedy select (streaming_server.py:342-347): argmax with first-index ties, top1-top2
 // margin, then the slot's prev token / position / plan step advance.
@@ -551,16 +919,38 @@ __global__ __launch_bounds__(256) void ar_argmax_kernel(ArState st) {
 // ---------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------
+int g_opt_gemv_reg = 0;  // runtime A/B switches (lvx_set_option); measured: LDS path faster at B=1
+int g_opt_attn_v2 = 1;
+int g_opt_cproj_b1 = 1;
+
 template <typename TW, int K, int KW, int RPW, int IN, int OUT>
 static void launch_gemv(const GemvArgs& a, hipStream_t s) {
   const int rows_per_block = (4 / KW) * RPW;
   dim3 grid((a.N + rows_per_block - 1) / rows_per_block);
   constexpr int BGMAX = (K == 768) ? 16 : 4;
+  if constexpr (IN == 2 && OUT == 1 && K == 768 && KW == 1) {
+    if (g_opt_cproj_b1 && a.B == 1) { hipLaunchKernelGGL((ar_cproj_b1_kernel<TW, RPW>), grid, dim3(256), 0, s, a); return; }
+  }
+  if constexpr (IN != 2) {
+    if (g_opt_gemv_reg && a.B <= 1) { hipLaunchKernelGGL((ar_gemv_reg_kernel<TW, K, KW, RPW, 1, IN, OUT>), grid, dim3(256), 0, s, a); return; }
+    if (g_opt_gemv_reg && a.B <= 4) { hipLaunchKernelGGL((ar_gemv_reg_kernel<TW, K, KW, RPW, 4, IN, OUT>), grid, dim3(256), 0, s, a); return; }
+  }
   if (a.B <= 1) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 1, IN, OUT>), grid, dim3(256), 0, s, a);
   else if (a.B <= 2) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 2, IN, OUT>), grid, dim3(256), 0, s, a);
   else if (a.B <= 4 || BGMAX == 4) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 4, IN, OUT>), grid, dim3(256), 0, s, a);
   else if (a.B <= 8) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, (BGMAX >= 8 ? 8 : 4), IN, OUT>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, BGMAX, IN, OUT>), grid, dim3(256), 0, s, a);
+}
+
+static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_t s) {
+  dim3 grid(NSPLIT, N_HEAD, B);
+  if (g_opt_attn_v2) {
+    if (kvdtype == LVX_DTYPE_BF16) hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t>), grid, dim3(256), 0, s, st, l);
+    else hipLaunchKernelGGL((ar_attn_v2_kernel<float>), grid, dim3(256), 0, s, st, l);
+  } else {
+    if (kvdtype == LVX_DTYPE_BF16) hipLaunchKernelGGL((ar_attn_kernel<bf16_t>), grid, dim3(256), 0, s, st, l);
+    else hipLaunchKernelGGL((ar_attn_kernel<float>), grid, dim3(256), 0, s, st, l);
+  }
 }
 
 template <typename TW>
@@ -581,10 +971,7 @@ static void ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B,
     a.W = w.w_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
     if (l == 0) launch_gemv<TW, 768, 1, 2, 3, 0>(a, s);
     else launch_gemv<TW, 768, 1, 2, 0, 0>(a, s);
-    if (kvdtype == LVX_DTYPE_BF16)
-      hipLaunchKernelGGL((ar_attn_kernel<bf16_t>), dim3(NSPLIT, N_HEAD, B), dim3(256), 0, s, st, l);
-    else
-      hipLaunchKernelGGL((ar_attn_kernel<float>), dim3(NSPLIT, N_HEAD, B), dim3(256), 0, s, st, l);
+    launch_attn(st, kvdtype, B, l, s);
     a.W = w.w_aproj[l]; a.N = D;
     launch_gemv<TW, 768, 1, 1, 2, 1>(a, s);
     a.W = w.w_fc[l]; a.N = DFF; a.ln_w = w.ln2[l];
@@ -613,12 +1000,7 @@ static int ar_probe_impl(const ArWeights& w, const ArState& st, int kvdtype, int
   for (int i = 0; i < iters; ++i) {
     switch (which) {
       case 0: a.W = w.w_attn[1]; a.N = 3 * D; a.ln_w = w.ln1[1]; launch_gemv<TW, 768, 1, 2, 0, 0>(a, s); break;
-      case 1:
-        if (kvdtype == LVX_DTYPE_BF16)
-          hipLaunchKernelGGL((ar_attn_kernel<bf16_t>), dim3(NSPLIT, N_HEAD, B), dim3(256), 0, s, st, 1);
-        else
-          hipLaunchKernelGGL((ar_attn_kernel<float>), dim3(NSPLIT, N_HEAD, B), dim3(256), 0, s, st, 1);
-        break;
+      case 1: launch_attn(st, kvdtype, B, 1, s); break;
       case 2: a.W = w.w_aproj[1]; a.N = D; launch_gemv<TW, 768, 1, 1, 2, 1>(a, s); break;
       case 3: a.W = w.w_fc[1]; a.N = DFF; a.ln_w = w.ln2[1]; launch_gemv<TW, 768, 1, 2, 0, 2>(a, s); break;
       case 4: a.W = w.w_mproj[1]; a.N = D; launch_gemv<TW, 3072, 4, 2, 1, 1>(a, s); break;

@@ -21,6 +21,7 @@
 using namespace lvx;
 
 static constexpr int kMaxCodecL = 4096;
+static constexpr int kGraphSteps = 16;  // decode steps per captured graph
 
 namespace {
 
@@ -115,12 +116,12 @@ int64_t numel_of(const WeightSpec& w) {
 }  // namespace
 
 struct GraphKey {
-  int B, stride;
+  int B, stride, nsteps;
   const void *slots, *text, *rowstep, *tok, *margin;
   void* stream;
   bool operator<(const GraphKey& o) const {
-    return std::tie(B, stride, slots, text, rowstep, tok, margin, stream) <
-           std::tie(o.B, o.stride, o.slots, o.text, o.rowstep, o.tok, o.margin, o.stream);
+    return std::tie(B, stride, nsteps, slots, text, rowstep, tok, margin, stream) <
+           std::tie(o.B, o.stride, o.nsteps, o.slots, o.text, o.rowstep, o.tok, o.margin, o.stream);
   }
 };
 
@@ -442,6 +443,19 @@ int lvx_stream_position(lvx_ctx* c, int slot, int* pos_out, void* stream) {
   return LVX_OK;
 }
 
+int lvx_set_option(lvx_ctx* c, const char* name, int value) {
+  if (!c || !name) return fail(LVX_E_ARG, "null argument");
+  std::string n(name);
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (n == "gemv_reg") g_opt_gemv_reg = value;
+  else if (n == "attn_v2") g_opt_attn_v2 = value;
+  else if (n == "cproj_b1") g_opt_cproj_b1 = value;
+  else return fail(LVX_E_NAME, "unknown option " + n);
+  for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);  // captured kernels change
+  c->graphs.clear();
+  return LVX_OK;
+}
+
 int lvx_set_graphs(lvx_ctx* c, int enable) {
   if (!c) return fail(LVX_E_ARG, "null ctx");
   c->use_graphs = enable != 0;
@@ -490,21 +504,37 @@ static int ar_step_impl(lvx_ctx* c, int n_steps, int B, const int32_t* slots, co
     return LVX_OK;
   }
   std::lock_guard<std::mutex> lk(c->mu);
-  GraphKey key{B, plan_stride, slots, text_plan, rowstep, tok_plan, margin_plan, stream};
-  auto it = c->graphs.find(key);
-  if (it == c->graphs.end()) {
-    hipGraph_t g;
-    HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    ar_launch_step(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, 0, nullptr, 0, 0, nullptr, s);
-    hipError_t le = hipGetLastError();
-    HIP_TRY(hipStreamEndCapture(s, &g));
-    if (le != hipSuccess) return fail(LVX_E_HIP, std::string("capture: ") + hipGetErrorString(le));
-    hipGraphExec_t ex;
-    HIP_TRY(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-    c->graph_defs.push_back(g);
-    it = c->graphs.emplace(key, ex).first;
+  // graphs of kGraphSteps consecutive steps (one replay per kGraphSteps tokens) + 1-step graph
+  auto get_graph = [&](int nst, hipGraphExec_t* out) -> int {
+    GraphKey key{B, plan_stride, nst, slots, text_plan, rowstep, tok_plan, margin_plan, stream};
+    auto it = c->graphs.find(key);
+    if (it == c->graphs.end()) {
+      hipGraph_t g;
+      HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      for (int i = 0; i < nst; ++i)
+        ar_launch_step(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, 0, nullptr, 0, 0, nullptr, s);
+      hipError_t le = hipGetLastError();
+      HIP_TRY(hipStreamEndCapture(s, &g));
+      if (le != hipSuccess) return fail(LVX_E_HIP, std::string("capture: ") + hipGetErrorString(le));
+      hipGraphExec_t ex;
+      HIP_TRY(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+      c->graph_defs.push_back(g);
+      it = c->graphs.emplace(key, ex).first;
+    }
+    *out = it->second;
+    return 0;
+  };
+  int left = n_steps;
+  if (left >= kGraphSteps) {
+    hipGraphExec_t gx;
+    if (int r = get_graph(kGraphSteps, &gx)) return r;
+    for (; left >= kGraphSteps; left -= kGraphSteps) HIP_TRY(hipGraphLaunch(gx, s));
   }
-  for (int i = 0; i < n_steps; ++i) HIP_TRY(hipGraphLaunch(it->second, s));
+  if (left > 0) {
+    hipGraphExec_t g1;
+    if (int r = get_graph(1, &g1)) return r;
+    for (; left > 0; --left) HIP_TRY(hipGraphLaunch(g1, s));
+  }
   return LVX_OK;
 }
 

@@ -106,6 +106,9 @@ class Engine:
     def check_errors(self):
         _lib.check(self.lib.lvx_check_errors(self.h, self.stream_handle()))
 
+    def set_option(self, name: str, value: int):
+        _lib.check(self.lib.lvx_set_option(self.h, name.encode(), int(value)))
+
     def set_graphs(self, enable: bool):
         _lib.check(self.lib.lvx_set_graphs(self.h, int(enable)))
 
