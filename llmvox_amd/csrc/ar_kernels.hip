@@ -50,6 +50,7 @@ struct GemvArgs {
   const float* codebook;
   const float* wpe;
   const float* emb_row;  // drop-in row mode when non-null
+  int prefetch;          // inputs of the first group issued before the weights (option "prefetch_in")
 };
 
 template <typename TW> struct WReg;
@@ -94,16 +95,18 @@ __device__ __forceinline__ void wave_ln_to_lds(float4 (&v)[3], const float* __re
 }
 
 template <int K, int IN>
-__device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, float* aux, int g0, int bg) {
+__device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, float* aux, int g0, int bg,
+                                                 const float4 (&xpre)[3], int4 ripre, bool prefetched) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   if (IN == 0 || IN == 3) {
     for (int bb = wave; bb < bg; bb += 4) {  // one wave per row
       const int b = g0 + bb;
+      const bool pre = prefetched && g0 == 0 && bb == wave;  // this row was prefetched before the weights
       float4 v[3];
       if (IN == 0) {
         const float* xr = a.st.x + (size_t)b * D;
 #pragma unroll
-        for (int j = 0; j < 3; ++j) v[j] = *reinterpret_cast<const float4*>(xr + j * 256 + lane * 4);
+        for (int j = 0; j < 3; ++j) v[j] = pre ? xpre[j] : *reinterpret_cast<const float4*>(xr + j * 256 + lane * 4);
       } else if (a.emb_row) {  // drop-in row forward: caller's normalised row + wpe[pos]
         const int p = a.st.rowinfo[0].y;
         const float* wr = a.wpe + (size_t)p * D;
@@ -118,7 +121,7 @@ __device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, f
 #pragma unroll
           for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + j * 256 + lane * 4) = v[j];
       } else {
-        const int4 ri = a.st.rowinfo[b];  // {slot, pos, text id, prev token}, validated by the producer
+        const int4 ri = pre ? ripre : a.st.rowinfo[b];  // {slot, pos, text id, prev}, validated by the producer
         if (ri.x < 0) {
 #pragma unroll
           for (int j = 0; j < 3; ++j) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -215,6 +218,19 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int rg = wave / KW, kp = wave % KW;
   const int row0 = (blockIdx.x * WROWS + rg) * RPW;
+  // inputs of the first batch group first (vmcnt retires in issue order): the LayerNorm /
+  // embedding math then overlaps the weight stream instead of waiting behind it
+  float4 xpre[3];
+  int4 ripre = make_int4(-1, 0, 0, 0);
+  const bool prefetched = a.prefetch && wave < min(BG, a.B);
+  if ((IN == 0 || IN == 3) && prefetched) {
+    if (IN == 0) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) xpre[j] = *reinterpret_cast<const float4*>(a.st.x + (size_t)wave * D + j * 256 + lane * 4);
+    } else {
+      ripre = a.st.rowinfo[wave];
+    }
+  }
   const TW* __restrict__ W = reinterpret_cast<const TW*>(a.W);
   typename WReg<TW>::T wr[RPW][NI];
 #pragma unroll
@@ -227,7 +243,7 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
   for (int g0 = 0; g0 < a.B; g0 += BG) {
     const int bg = min(BG, a.B - g0);
     if (g0) __syncthreads();
-    gemv_stage_input<K, IN>(a, xs, aux, g0, bg);
+    gemv_stage_input<K, IN>(a, xs, aux, g0, bg, xpre, ripre, prefetched);
     __syncthreads();
     float acc[RPW][BG];
 #pragma unroll
@@ -922,6 +938,7 @@ __global__ __launch_bounds__(256) void ar_argmax_kernel(ArState st) {
 int g_opt_gemv_reg = 0;  // runtime A/B switches (lvx_set_option); measured: LDS path faster at B=1
 int g_opt_attn_v2 = 1;
 int g_opt_cproj_b1 = 1;
+int g_opt_prefetch_in = 1;
 
 template <typename TW, int K, int KW, int RPW, int IN, int OUT>
 static void launch_gemv(const GemvArgs& a, hipStream_t s) {
@@ -964,6 +981,7 @@ static void ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B,
   a.codebook = w.codebook;
   a.wpe = w.wpe;
   a.emb_row = emb_row;
+  a.prefetch = g_opt_prefetch_in;
   if (emb_row) hipLaunchKernelGGL(ar_row_state_kernel, dim3(1), dim3(1), 0, s, st, slot, pos);
   for (int l = 0; l < N_LAYER; ++l) {
     a.layer = l;

@@ -371,9 +371,11 @@ int lvx_finalize(lvx_ctx* c) {
   CodecScratch& cs = c->cs;
   const int M = c->cfg.max_codec_frames;
   cs.max_frames = M;
+  cs.ws_floats = (size_t)std::max(M, 256) * 2304 * 4;
   if ((r = c->dalloc(&cs.x, (size_t)M * 768)) || (r = c->dalloc(&cs.t1, (size_t)M * 2304)) ||
       (r = c->dalloc(&cs.t2, (size_t)(M + 4 * 64) * 2304 + (size_t)768 * 4 * M)) ||
-      (r = c->dalloc(&cs.feats, (size_t)M * 512)) ||
+      (r = c->dalloc(&cs.feats, (size_t)M * 512)) || (r = c->dalloc(&cs.gn, (size_t)M * 768)) ||
+      (r = c->dalloc(&cs.ws, (size_t)std::max(M, 256) * 2304 * 4)) ||
       (r = c->dalloc(&cs.att, (size_t)M * (std::min(M, kMaxCodecL) + 4))) ||
       (r = c->dalloc(&cs.stats, (size_t)M * 32 * 2)) || (r = c->dalloc(&cs.spec, (size_t)M * 1282)) ||
       (r = c->dalloc(&cs.frames, (size_t)M * 1280)))
@@ -450,6 +452,7 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   if (n == "gemv_reg") g_opt_gemv_reg = value;
   else if (n == "attn_v2") g_opt_attn_v2 = value;
   else if (n == "cproj_b1") g_opt_cproj_b1 = value;
+  else if (n == "prefetch_in") g_opt_prefetch_in = value;
   else return fail(LVX_E_NAME, "unknown option " + n);
   for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);  // captured kernels change
   c->graphs.clear();
