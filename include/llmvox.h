@@ -103,6 +103,8 @@ int lvx_ar_step(lvx_ctx* ctx, int B, const int32_t* slots_dev, const int32_t* te
 int lvx_ar_steps(lvx_ctx* ctx, int n_steps, int B, const int32_t* slots_dev, const int32_t* text_plan_dev,
                  int plan_stride, int32_t* rowstep_dev, int32_t* tok_plan_dev, float* margin_plan_dev,
                  void* stream);
+/* Copy the logits [B][4096] of the last lvx_ar_step(s) call (diagnostics / tests). */
+int lvx_ar_logits(lvx_ctx* ctx, int B, float* dst_dev, void* stream);
 /* Synchronises the stream and reports (then clears) device-side capacity errors: a slot past
  * max_positions (reference: the block_size AssertionError, src/model.py:205) or a row past
  * the end of its plan. */

@@ -64,6 +64,7 @@ _SIGS = {
     "lvx_ar_step": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _P]),
     "lvx_ar_steps": (_I, [_P, _I, _I, _P, _P, _I, _P, _P, _P, _P]),
     "lvx_check_errors": (_I, [_P, _P]),
+    "lvx_ar_logits": (_I, [_P, _I, _P, _P]),
     "lvx_probe_kernel": (_I, [_P, _I, _I, _P, _I, _P]),
     "lvx_stream_set": (_I, [_P, _I, _I, _I, _P]),
     "lvx_stream_position": (_I, [_P, _I, ctypes.POINTER(_I), _P]),

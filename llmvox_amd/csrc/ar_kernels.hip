@@ -959,6 +959,161 @@ static void launch_gemv(const GemvArgs& a, hipStream_t s) {
   else hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, BGMAX, IN, OUT>), grid, dim3(256), 0, s, a);
 }
 
+// ---------------------------------------------------------------------------------
+// Batched path (bf16 weights, 4 < B <= 64): weight GEMMs on v_mfma_f32_16x16x32_bf16.
+// A block owns 64 weight rows (4 waves x 16) and every batch row; A operand = weight rows
+// straight from global (16 B per lane, each byte read once per step), B operand = the block's
+// normalised inputs staged once in LDS as bf16 [NT*16][K chunk]. Output tile: lane l holds
+// rows 4*(l>>4)+i of its wave's 16 weight rows for batch column l&15 (16x16 C/D mapping).
+//   IN 0: LayerNorm(x)   IN 3: embedding + LayerNorm   IN 1: h (K = 3072, 4 chunks)
+//   IN 4: merged attention output y (written by ar_merge_kernel into st.q)
+// ---------------------------------------------------------------------------------
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+constexpr int MKC = 768;          // K chunk staged in LDS
+constexpr int MXLD = MKC + 8;     // LDS row stride in bf16 (1552 B)
+
+__device__ __forceinline__ uint2 pack4_bf16(float4 v) {
+  return make_uint2((uint32_t)f32_to_bf16(v.x) | ((uint32_t)f32_to_bf16(v.y) << 16),
+                    (uint32_t)f32_to_bf16(v.z) | ((uint32_t)f32_to_bf16(v.w) << 16));
+}
+
+template <int K, int NT, int IN, int OUT>
+__global__ __launch_bounds__(256) void ar_mfma_kernel(GemvArgs a) {
+  constexpr int NCH = K / MKC;
+  constexpr int KS = MKC / 32;  // MFMA k-steps per chunk (24)
+  __shared__ __attribute__((aligned(16))) bf16_t xs[NT * 16 * MXLD];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int n0 = blockIdx.x * 64 + wave * 16;
+  const int B = a.B;
+  const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(a.W);
+  const int wrow = min(n0 + (lane & 15), a.N - 1);  // clamp: padded rows compute garbage, never stored
+  f32x4_t acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float4 g[3];
+  if (IN == 0 || IN == 3) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) g[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
+  }
+  for (int ch = 0; ch < NCH; ++ch) {
+    // this chunk's weight fragments first (independent of the inputs)
+    uint4 wf[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk)
+      wf[kk] = *reinterpret_cast<const uint4*>(W + (size_t)wrow * K + ch * MKC + kk * 32 + 8 * (lane >> 4));
+    if (ch) __syncthreads();
+    // stage the inputs of every batch row (rows >= B are zero)
+    for (int b = wave; b < NT * 16; b += 4) {
+      uint2* dst = reinterpret_cast<uint2*>(xs + b * MXLD);
+      if (b >= B) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) dst[j * 64 + lane] = make_uint2(0u, 0u);
+        continue;
+      }
+      float4 v[3];
+      if (IN == 1 || IN == 4) {
+        const float* src = (IN == 1) ? a.st.h + (size_t)b * K + ch * MKC : a.st.q + (size_t)b * D;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) v[j] = *reinterpret_cast<const float4*>(src + j * 256 + lane * 4);
+      } else if (IN == 0) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) v[j] = *reinterpret_cast<const float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4);
+        wave_ln_regs(v, g);
+      } else {
+        const int4 ri = a.st.rowinfo[b];
+        if (ri.x < 0) {
+#pragma unroll
+          for (int j = 0; j < 3; ++j) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+          const int p = ri.y, prev = ri.w;
+          int tok = ri.z;
+          if (tok < 0) {
+            if (lane == 0 && blockIdx.x == 0) atomicOr(a.st.err, 2);
+            tok = 384;
+          }
+          float ss = 0.f;
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            const int k = j * 256 + lane * 4;
+            if (j == 0) v[j] = *reinterpret_cast<const float4*>(a.text_table + (size_t)tok * TEXT_DIM + k);
+            else if (p == 0) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            else v[j] = *reinterpret_cast<const float4*>(a.codebook + (size_t)prev * SPEECH_DIM + (k - TEXT_DIM));
+            ss += (v[j].x * v[j].x + v[j].y * v[j].y) + (v[j].z * v[j].z + v[j].w * v[j].w);
+          }
+          const float den = fmaxf(sqrtf(wave_sum(ss)), 1e-8f);
+          const float* wr_ = a.wpe + (size_t)p * D;
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            const float4 pe = *reinterpret_cast<const float4*>(wr_ + j * 256 + lane * 4);
+            v[j] = make_float4(v[j].x / den + pe.x, v[j].y / den + pe.y, v[j].z / den + pe.z, v[j].w / den + pe.w);
+          }
+        }
+        if (blockIdx.x == 0)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = v[j];
+        wave_ln_regs(v, g);
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) dst[j * 64 + lane] = pack4_bf16(v[j]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const bf16x8_t af = __builtin_bit_cast(bf16x8_t, wf[kk]);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const bf16x8_t bfr =
+            *reinterpret_cast<const bf16x8_t*>(xs + (t * 16 + (lane & 15)) * MXLD + kk * 32 + 8 * (lane >> 4));
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[t], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int b = t * 16 + (lane & 15);
+    if (b >= B) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = n0 + 4 * (lane >> 4) + i;
+      if (n < a.N) gemv_store<OUT>(a, n, b, acc[t][i]);
+    }
+  }
+}
+
+// merged attention output y[b] = sum_s c_s o_s for the batched path (one block per row)
+__global__ __launch_bounds__(256) void ar_merge_kernel(ArState st) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int4 ri = st.rowinfo[b];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int e = tid + 256 * j, head = e / HD, d = e - head * HD;
+    if (ri.x < 0) { st.q[(size_t)b * D + e] = 0.f; continue; }
+    const int ns = min(NSPLIT, (ri.y + 1 + 63) / 64);
+    const float* ml = st.part_ml + ((size_t)(b * N_HEAD + head) * NSPLIT) * 2;
+    const float* po = st.part_o + ((size_t)(b * N_HEAD + head) * NSPLIT) * HD + d;
+    float M = -INFINITY;
+    for (int i = 0; i < ns; ++i) M = fmaxf(M, ml[2 * i]);
+    float num = 0.f, den = 0.f;
+    for (int i = 0; i < ns; ++i) {
+      const float f = (ml[2 * i] == -INFINITY) ? 0.f : expf(ml[2 * i] - M);
+      num += f * po[(size_t)i * HD];
+      den += f * ml[2 * i + 1];
+    }
+    st.q[(size_t)b * D + e] = num / den;
+  }
+}
+
+int g_opt_mfma_batch = 1;
+
+template <int K, int IN, int OUT>
+static void launch_mfma(const GemvArgs& a, hipStream_t s) {
+  dim3 grid((a.N + 63) / 64);
+  if (a.B <= 16) hipLaunchKernelGGL((ar_mfma_kernel<K, 1, IN, OUT>), grid, dim3(256), 0, s, a);
+  else if (a.B <= 32) hipLaunchKernelGGL((ar_mfma_kernel<K, 2, IN, OUT>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((ar_mfma_kernel<K, 4, IN, OUT>), grid, dim3(256), 0, s, a);
+}
+
 static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_t s) {
   dim3 grid(NSPLIT, N_HEAD, B);
   if (g_opt_attn_v2) {
@@ -983,26 +1138,39 @@ static void ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B,
   a.emb_row = emb_row;
   a.prefetch = g_opt_prefetch_in;
   if (emb_row) hipLaunchKernelGGL(ar_row_state_kernel, dim3(1), dim3(1), 0, s, st, slot, pos);
+  const bool mf = sizeof(TW) == 2 && g_opt_mfma_batch && B > 4 && B <= 64;
   for (int l = 0; l < N_LAYER; ++l) {
     a.layer = l;
     // (layer 0: embed) + LN1 + c_attn + KV append
     a.W = w.w_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
-    if (l == 0) launch_gemv<TW, 768, 1, 2, 3, 0>(a, s);
-    else launch_gemv<TW, 768, 1, 2, 0, 0>(a, s);
+    if (mf) {
+      if (l == 0) launch_mfma<768, 3, 0>(a, s);
+      else launch_mfma<768, 0, 0>(a, s);
+    } else if (l == 0) {
+      launch_gemv<TW, 768, 1, 2, 3, 0>(a, s);
+    } else {
+      launch_gemv<TW, 768, 1, 2, 0, 0>(a, s);
+    }
     launch_attn(st, kvdtype, B, l, s);
     a.W = w.w_aproj[l]; a.N = D;
-    launch_gemv<TW, 768, 1, 1, 2, 1>(a, s);
+    if (mf) {
+      hipLaunchKernelGGL(ar_merge_kernel, dim3(B), dim3(256), 0, s, st);
+      launch_mfma<768, 4, 1>(a, s);
+    } else {
+      launch_gemv<TW, 768, 1, 1, 2, 1>(a, s);
+    }
     a.W = w.w_fc[l]; a.N = DFF; a.ln_w = w.ln2[l];
-    launch_gemv<TW, 768, 1, 2, 0, 2>(a, s);
+    if (mf) launch_mfma<768, 0, 2>(a, s);
+    else launch_gemv<TW, 768, 1, 2, 0, 2>(a, s);
     a.W = w.w_mproj[l]; a.N = D;
-    launch_gemv<TW, 3072, 4, 2, 1, 1>(a, s);
+    if (mf) launch_mfma<3072, 1, 1>(a, s);
+    else launch_gemv<TW, 3072, 4, 2, 1, 1>(a, s);
   }
   a.W = w.w_lm; a.N = VOCAB; a.ln_w = w.lnf; a.dst = logits_dst;
-  launch_gemv<TW, 768, 1, 2, 0, 3>(a, s);
+  if (mf) launch_mfma<768, 0, 3>(a, s);
+  else launch_gemv<TW, 768, 1, 2, 0, 3>(a, s);
 }
 
-// Launch one kernel class of the decode step `iters` times (bench.py times it with HIP events):
-// 0 c_attn(+embed, layer 0)  1 attention  2 c_proj(+merge)  3 c_fc  4 mlp c_proj  5 lm_head  6 argmax
 template <typename TW>
 static int ar_probe_impl(const ArWeights& w, const ArState& st, int kvdtype, int B, int which, int iters,
                          hipStream_t s) {

@@ -453,6 +453,7 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   else if (n == "attn_v2") g_opt_attn_v2 = value;
   else if (n == "cproj_b1") g_opt_cproj_b1 = value;
   else if (n == "prefetch_in") g_opt_prefetch_in = value;
+  else if (n == "mfma_batch") g_opt_mfma_batch = value;
   else return fail(LVX_E_NAME, "unknown option " + n);
   for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);  // captured kernels change
   c->graphs.clear();
@@ -549,6 +550,14 @@ int lvx_ar_step(lvx_ctx* c, int B, const int32_t* slots, const int32_t* text_pla
 int lvx_ar_steps(lvx_ctx* c, int n_steps, int B, const int32_t* slots, const int32_t* text_plan, int plan_stride,
                  int32_t* rowstep, int32_t* tok_plan, float* margin_plan, void* stream) {
   return ar_step_impl(c, n_steps, B, slots, text_plan, plan_stride, rowstep, tok_plan, margin_plan, stream);
+}
+
+int lvx_ar_logits(lvx_ctx* c, int B, float* dst, void* stream) {
+  NEED_FINAL(c);
+  if (B < 1 || B > c->cfg.max_streams || !dst) return fail(LVX_E_ARG, "bad B/dst");
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  HIP_TRY(hipMemcpyAsync(dst, c->st.logits, (size_t)B * VOCAB * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return LVX_OK;
 }
 
 int lvx_check_errors(lvx_ctx* c, void* stream) {

@@ -12,7 +12,7 @@ namespace lvx {
 constexpr int N_LAYER = 4, N_HEAD = 8, D = 768, HD = 96, DFF = 3072, VOCAB = 4096;
 constexpr int TEXT_DIM = 256, SPEECH_DIM = 512, TEXT_VOCAB = 386, BLOCK_SIZE = 8192;
 constexpr int NSPLIT = 16;
-extern int g_opt_gemv_reg, g_opt_attn_v2, g_opt_cproj_b1, g_opt_prefetch_in;  // development A/B switches (lvx_set_option)  // max KV splits per (stream, head) in decode attention
+extern int g_opt_gemv_reg, g_opt_attn_v2, g_opt_cproj_b1, g_opt_prefetch_in, g_opt_mfma_batch;  // development A/B switches (lvx_set_option)  // max KV splits per (stream, head) in decode attention
 
 // Device-resident AR weights. Matrices are [out][in] row-major (torch Linear layout),
 // in the context's weight dtype; vectors and gathered tables are fp32.

@@ -103,6 +103,11 @@ class Engine:
     def probe_kernel(self, which: int, slots: torch.Tensor, iters: int):
         _lib.check(self.lib.lvx_probe_kernel(self.h, which, slots.numel(), _ptr(slots), iters, self.stream_handle()))
 
+    def last_logits(self, B: int) -> torch.Tensor:
+        out = torch.empty(B, 4096, device=self.device, dtype=torch.float32)
+        _lib.check(self.lib.lvx_ar_logits(self.h, B, _ptr(out), self.stream_handle()))
+        return out
+
     def check_errors(self):
         _lib.check(self.lib.lvx_check_errors(self.h, self.stream_handle()))
 
