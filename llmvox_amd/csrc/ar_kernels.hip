@@ -781,7 +781,7 @@ __global__ __launch_bounds__(256) void ar_attn_kernel(ArState st, int layer) {
 // every wave keeps its own online-softmax state (m, l, o[24] per lane) so the loop has no
 // barrier. The 4 wave states are merged once at the end through LDS.
 template <typename TKV>
-__global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer) {
+__global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer, int ns_max) {
   __shared__ float wm_s[4], wl_s[4];
   __shared__ float wo_s[4][HD];
   const int sp = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
@@ -790,7 +790,7 @@ __global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer) 
   const int s = ri.x;
   if (s < 0) return;
   const int t = ri.y + 1;
-  const int ns = min(NSPLIT, (t + ATK - 1) / ATK);
+  const int ns = min(ns_max, (t + ATK - 1) / ATK);
   if (sp >= ns) return;
   const int chunk = (t + ns - 1) / ns;
   const int k0 = sp * chunk, k1 = min(t, k0 + chunk);
@@ -959,175 +959,229 @@ static void launch_gemv(const GemvArgs& a, hipStream_t s) {
   else hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, BGMAX, IN, OUT>), grid, dim3(256), 0, s, a);
 }
 
-// ---------------------------------------------------------------------------------
-// Batched path (bf16 weights, 4 < B <= 64): weight GEMMs on v_mfma_f32_16x16x32_bf16.
-// A block owns 64 weight rows (4 waves x 16) and every batch row; A operand = weight rows
-// straight from global (16 B per lane, each byte read once per step), B operand = the block's
-// normalised inputs staged once in LDS as bf16 [NT*16][K chunk]. Output tile: lane l holds
-// rows 4*(l>>4)+i of its wave's 16 weight rows for batch column l&15 (16x16 C/D mapping).
-//   IN 0: LayerNorm(x)   IN 3: embedding + LayerNorm   IN 1: h (K = 3072, 4 chunks)
-//   IN 4: merged attention output y (written by ar_merge_kernel into st.q)
-// ---------------------------------------------------------------------------------
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
-constexpr int MKC = 768;          // K chunk staged in LDS
-constexpr int MXLD = MKC + 8;     // LDS row stride in bf16 (1552 B)
 
 __device__ __forceinline__ uint2 pack4_bf16(float4 v) {
   return make_uint2((uint32_t)f32_to_bf16(v.x) | ((uint32_t)f32_to_bf16(v.y) << 16),
                     (uint32_t)f32_to_bf16(v.z) | ((uint32_t)f32_to_bf16(v.w) << 16));
 }
 
-template <int K, int NT, int IN, int OUT>
-__global__ __launch_bounds__(256) void ar_mfma_kernel(GemvArgs a) {
-  constexpr int NCH = K / MKC;
-  constexpr int KS = MKC / 32;  // MFMA k-steps per chunk (24)
-  __shared__ __attribute__((aligned(16))) bf16_t xs[NT * 16 * MXLD];
+int g_opt_mfma_batch = 1;
+
+// ---------------------------------------------------------------------------------
+// Batched path v2 (bf16 weights, 4 < B <= 32): every per-row prologue runs ONCE per row into a
+// bf16 operand buffer (LayerNorm / embedding+LayerNorm / split merge), then the weight GEMMs are
+// pure MFMA GEMMs reading both operands from global: a block owns 16 weight rows and K is split
+// over its waves (K/192 waves: 4 for K=768, 16 for K=3072); every lane issues all of its
+// 16-byte fragment loads up front (one memory latency), partial tiles combine through LDS.
+// ---------------------------------------------------------------------------------
+template <int MODE>  // 0: LayerNorm(x)  3: embedding (+ stores x) then LayerNorm
+__global__ __launch_bounds__(256) void ar_rows_kernel(GemvArgs a) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int n0 = blockIdx.x * 64 + wave * 16;
-  const int B = a.B;
-  const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(a.W);
-  const int wrow = min(n0 + (lane & 15), a.N - 1);  // clamp: padded rows compute garbage, never stored
-  f32x4_t acc[NT];
+  const int b = blockIdx.x * 4 + wave;
+  if (b >= a.B) return;
+  float4 g[3], v[3];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float4 g[3];
-  if (IN == 0 || IN == 3) {
+  for (int j = 0; j < 3; ++j) g[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
+  if (MODE == 0) {
 #pragma unroll
-    for (int j = 0; j < 3; ++j) g[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
-  }
-  for (int ch = 0; ch < NCH; ++ch) {
-    // this chunk's weight fragments first (independent of the inputs)
-    uint4 wf[KS];
+    for (int j = 0; j < 3; ++j) v[j] = *reinterpret_cast<const float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4);
+  } else {
+    const int4 ri = a.st.rowinfo[b];
+    if (ri.x < 0) {
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk)
-      wf[kk] = *reinterpret_cast<const uint4*>(W + (size_t)wrow * K + ch * MKC + kk * 32 + 8 * (lane >> 4));
-    if (ch) __syncthreads();
-    // stage the inputs of every batch row (rows >= B are zero)
-    for (int b = wave; b < NT * 16; b += 4) {
-      uint2* dst = reinterpret_cast<uint2*>(xs + b * MXLD);
-      if (b >= B) {
-#pragma unroll
-        for (int j = 0; j < 3; ++j) dst[j * 64 + lane] = make_uint2(0u, 0u);
-        continue;
+      for (int j = 0; j < 3; ++j) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      const int p = ri.y, prev = ri.w;
+      int tok = ri.z;
+      if (tok < 0) {
+        if (lane == 0) atomicOr(a.st.err, 2);
+        tok = 384;
       }
-      float4 v[3];
-      if (IN == 1 || IN == 4) {
-        const float* src = (IN == 1) ? a.st.h + (size_t)b * K + ch * MKC : a.st.q + (size_t)b * D;
+      float4 pe[3];
+      const float* wr_ = a.wpe + (size_t)p * D;
 #pragma unroll
-        for (int j = 0; j < 3; ++j) v[j] = *reinterpret_cast<const float4*>(src + j * 256 + lane * 4);
-      } else if (IN == 0) {
+      for (int j = 0; j < 3; ++j) pe[j] = *reinterpret_cast<const float4*>(wr_ + j * 256 + lane * 4);
+      float ss = 0.f;
 #pragma unroll
-        for (int j = 0; j < 3; ++j) v[j] = *reinterpret_cast<const float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4);
-        wave_ln_regs(v, g);
-      } else {
-        const int4 ri = a.st.rowinfo[b];
-        if (ri.x < 0) {
-#pragma unroll
-          for (int j = 0; j < 3; ++j) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-        } else {
-          const int p = ri.y, prev = ri.w;
-          int tok = ri.z;
-          if (tok < 0) {
-            if (lane == 0 && blockIdx.x == 0) atomicOr(a.st.err, 2);
-            tok = 384;
-          }
-          float ss = 0.f;
-#pragma unroll
-          for (int j = 0; j < 3; ++j) {
-            const int k = j * 256 + lane * 4;
-            if (j == 0) v[j] = *reinterpret_cast<const float4*>(a.text_table + (size_t)tok * TEXT_DIM + k);
-            else if (p == 0) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-            else v[j] = *reinterpret_cast<const float4*>(a.codebook + (size_t)prev * SPEECH_DIM + (k - TEXT_DIM));
-            ss += (v[j].x * v[j].x + v[j].y * v[j].y) + (v[j].z * v[j].z + v[j].w * v[j].w);
-          }
-          const float den = fmaxf(sqrtf(wave_sum(ss)), 1e-8f);
-          const float* wr_ = a.wpe + (size_t)p * D;
-#pragma unroll
-          for (int j = 0; j < 3; ++j) {
-            const float4 pe = *reinterpret_cast<const float4*>(wr_ + j * 256 + lane * 4);
-            v[j] = make_float4(v[j].x / den + pe.x, v[j].y / den + pe.y, v[j].z / den + pe.z, v[j].w / den + pe.w);
-          }
-        }
-        if (blockIdx.x == 0)
-#pragma unroll
-          for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = v[j];
-        wave_ln_regs(v, g);
+      for (int j = 0; j < 3; ++j) {
+        const int k = j * 256 + lane * 4;
+        if (j == 0) v[j] = *reinterpret_cast<const float4*>(a.text_table + (size_t)tok * TEXT_DIM + k);
+        else if (p == 0) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        else v[j] = *reinterpret_cast<const float4*>(a.codebook + (size_t)prev * SPEECH_DIM + (k - TEXT_DIM));
+        ss += (v[j].x * v[j].x + v[j].y * v[j].y) + (v[j].z * v[j].z + v[j].w * v[j].w);
       }
+      const float den = fmaxf(sqrtf(wave_sum(ss)), 1e-8f);
 #pragma unroll
-      for (int j = 0; j < 3; ++j) dst[j * 64 + lane] = pack4_bf16(v[j]);
+      for (int j = 0; j < 3; ++j)
+        v[j] = make_float4(v[j].x / den + pe[j].x, v[j].y / den + pe[j].y, v[j].z / den + pe[j].z, v[j].w / den + pe[j].w);
     }
-    __syncthreads();
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk) {
-      const bf16x8_t af = __builtin_bit_cast(bf16x8_t, wf[kk]);
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const bf16x8_t bfr =
-            *reinterpret_cast<const bf16x8_t*>(xs + (t * 16 + (lane & 15)) * MXLD + kk * 32 + 8 * (lane >> 4));
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[t], 0, 0, 0);
-      }
-    }
+    for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = v[j];
   }
+  wave_ln_regs(v, g);
+  uint2* dst = reinterpret_cast<uint2*>(a.st.xn + (size_t)b * D);
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int b = t * 16 + (lane & 15);
-    if (b >= B) continue;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int n = n0 + 4 * (lane >> 4) + i;
-      if (n < a.N) gemv_store<OUT>(a, n, b, acc[t][i]);
-    }
-  }
+  for (int j = 0; j < 3; ++j) dst[j * 64 + lane] = pack4_bf16(v[j]);
 }
 
-// merged attention output y[b] = sum_s c_s o_s for the batched path (one block per row)
-__global__ __launch_bounds__(256) void ar_merge_kernel(ArState st) {
+// split-KV merge for the batched path: y[b] (bf16) into st.xn
+__global__ __launch_bounds__(256) void ar_merge_bf16_kernel(ArState st, int ns_max) {
   const int b = blockIdx.x, tid = threadIdx.x;
   const int4 ri = st.rowinfo[b];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int e = tid + 256 * j, head = e / HD, d = e - head * HD;
-    if (ri.x < 0) { st.q[(size_t)b * D + e] = 0.f; continue; }
-    const int ns = min(NSPLIT, (ri.y + 1 + 63) / 64);
-    const float* ml = st.part_ml + ((size_t)(b * N_HEAD + head) * NSPLIT) * 2;
-    const float* po = st.part_o + ((size_t)(b * N_HEAD + head) * NSPLIT) * HD + d;
-    float M = -INFINITY;
-    for (int i = 0; i < ns; ++i) M = fmaxf(M, ml[2 * i]);
-    float num = 0.f, den = 0.f;
-    for (int i = 0; i < ns; ++i) {
-      const float f = (ml[2 * i] == -INFINITY) ? 0.f : expf(ml[2 * i] - M);
-      num += f * po[(size_t)i * HD];
-      den += f * ml[2 * i + 1];
+    float y = 0.f;
+    if (ri.x >= 0) {
+      const int ns = min(ns_max, (ri.y + 1 + 63) / 64);
+      const float* ml = st.part_ml + ((size_t)(b * N_HEAD + head) * NSPLIT) * 2;
+      const float* po = st.part_o + ((size_t)(b * N_HEAD + head) * NSPLIT) * HD + d;
+      float M = -INFINITY;
+      for (int i = 0; i < ns; ++i) M = fmaxf(M, ml[2 * i]);
+      float num = 0.f, den = 0.f;
+      for (int i = 0; i < ns; ++i) {
+        const float f = (ml[2 * i] == -INFINITY) ? 0.f : expf(ml[2 * i] - M);
+        num += f * po[(size_t)i * HD];
+        den += f * ml[2 * i + 1];
+      }
+      y = num / den;
     }
-    st.q[(size_t)b * D + e] = num / den;
+    st.xn[(size_t)b * D + e] = f32_to_bf16(y);
   }
 }
 
-int g_opt_mfma_batch = 1;
-
-template <int K, int IN, int OUT>
-static void launch_mfma(const GemvArgs& a, hipStream_t s) {
-  dim3 grid((a.N + 63) / 64);
-  if (a.B <= 16) hipLaunchKernelGGL((ar_mfma_kernel<K, 1, IN, OUT>), grid, dim3(256), 0, s, a);
-  else if (a.B <= 32) hipLaunchKernelGGL((ar_mfma_kernel<K, 2, IN, OUT>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((ar_mfma_kernel<K, 4, IN, OUT>), grid, dim3(256), 0, s, a);
+// OUT as gemv_store, plus OUT 5: h (bf16) = gelu_tanh(v) for the batched mlp c_proj
+template <int K, int NT, int OUT>
+__global__ __launch_bounds__(1024) void ar_mfma2_kernel(GemvArgs a) {
+  constexpr int NW = K / 192;  // waves per block, each a 192-wide K slice (6 MFMA k-steps)
+  __shared__ float red[NW][NT * 256];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int n0 = blockIdx.x * 16;
+  const int B = a.B;
+  const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(a.W);
+  const bf16_t* __restrict__ X = (K == 768) ? a.st.xn : a.st.hb;
+  const int wrow = min(n0 + (lane & 15), a.N - 1);
+  const int k0 = wave * 192 + 8 * (lane >> 4);
+  uint4 wf[6], xf[NT][6];
+#pragma unroll
+  for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(W + (size_t)wrow * K + k0 + kk * 32);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int b = min(t * 16 + (lane & 15), B - 1);  // padded columns recompute row B-1, never stored
+#pragma unroll
+    for (int kk = 0; kk < 6; ++kk) xf[t][kk] = *reinterpret_cast<const uint4*>(X + (size_t)b * K + k0 + kk * 32);
+  }
+  f32x4_t acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < 6; ++kk)
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[kk]),
+                                                       __builtin_bit_cast(bf16x8_t, xf[t][kk]), acc[t], 0, 0, 0);
+  // partial 16 x (NT*16) tiles -> LDS, element (row r, col c) at r * (NT*16) + c
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[wave][(4 * (lane >> 4) + i) * (NT * 16) + t * 16 + (lane & 15)] = acc[t][i];
+  __syncthreads();
+  for (int e = tid; e < 16 * NT * 16; e += NW * 64) {
+    const int r = e / (NT * 16), b = e - r * (NT * 16), n = n0 + r;
+    if (b >= B || n >= a.N) continue;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[w][e];
+    if (OUT == 5) a.st.hb[(size_t)b * DFF + n] = f32_to_bf16(gelu_tanh(v));
+    else gemv_store<OUT>(a, n, b, v);
+  }
 }
 
-static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_t s) {
-  dim3 grid(NSPLIT, N_HEAD, B);
+template <int K, int OUT>
+static void launch_mfma2(const GemvArgs& a, hipStream_t s) {
+  dim3 grid((a.N + 15) / 16), block((K / 192) * 64);
+  if (a.B <= 16) hipLaunchKernelGGL((ar_mfma2_kernel<K, 1, OUT>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((ar_mfma2_kernel<K, 2, OUT>), grid, block, 0, s, a);
+}
+
+static int attn_ns_max(int B) {  // enough splits to fill the chip, no more (early-exit blocks cost)
+  int ns = NSPLIT;
+  while (ns > 1 && ns * N_HEAD * B > 1024) ns >>= 1;
+  return ns;
+}
+
+static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_t s, int ns_max = NSPLIT) {
   if (g_opt_attn_v2) {
-    if (kvdtype == LVX_DTYPE_BF16) hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t>), grid, dim3(256), 0, s, st, l);
-    else hipLaunchKernelGGL((ar_attn_v2_kernel<float>), grid, dim3(256), 0, s, st, l);
+    dim3 grid(ns_max, N_HEAD, B);
+    if (kvdtype == LVX_DTYPE_BF16) hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t>), grid, dim3(256), 0, s, st, l, ns_max);
+    else hipLaunchKernelGGL((ar_attn_v2_kernel<float>), grid, dim3(256), 0, s, st, l, ns_max);
   } else {
+    dim3 grid(NSPLIT, N_HEAD, B);
     if (kvdtype == LVX_DTYPE_BF16) hipLaunchKernelGGL((ar_attn_kernel<bf16_t>), grid, dim3(256), 0, s, st, l);
     else hipLaunchKernelGGL((ar_attn_kernel<float>), grid, dim3(256), 0, s, st, l);
   }
 }
 
+// one op of the decode step, with the B-dependent kernel choice (shared by the step and the probes)
+// op: 0 c_attn (layer 0: + embedding) 1 attention 2 c_proj (+ split merge) 3 c_fc 4 mlp c_proj 5 lm_head
 template <typename TW>
-static void ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B, const float* emb_row, int slot,
-                      int pos, float* logits_dst, hipStream_t s) {
+static void launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtype, int B, hipStream_t s) {
+  const bool mf = sizeof(TW) == 2 && g_opt_mfma_batch && B > 4 && B <= 32;
+  const int nsm = mf ? attn_ns_max(B) : NSPLIT;
+  a.layer = l;
+  switch (op) {
+    case 0:
+      a.W = w.w_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
+      if (mf) {
+        if (l == 0) hipLaunchKernelGGL((ar_rows_kernel<3>), dim3((B + 3) / 4), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((ar_rows_kernel<0>), dim3((B + 3) / 4), dim3(256), 0, s, a);
+        launch_mfma2<768, 0>(a, s);
+      } else if (l == 0) {
+        launch_gemv<TW, 768, 1, 2, 3, 0>(a, s);
+      } else {
+        launch_gemv<TW, 768, 1, 2, 0, 0>(a, s);
+      }
+      break;
+    case 1: launch_attn(a.st, kvdtype, B, l, s, nsm); break;
+    case 2:
+      a.W = w.w_aproj[l]; a.N = D;
+      if (mf) {
+        hipLaunchKernelGGL(ar_merge_bf16_kernel, dim3(B), dim3(256), 0, s, a.st, nsm);
+        launch_mfma2<768, 1>(a, s);
+      } else {
+        launch_gemv<TW, 768, 1, 1, 2, 1>(a, s);
+      }
+      break;
+    case 3:
+      a.W = w.w_fc[l]; a.N = DFF; a.ln_w = w.ln2[l];
+      if (mf) {
+        hipLaunchKernelGGL((ar_rows_kernel<0>), dim3((B + 3) / 4), dim3(256), 0, s, a);
+        launch_mfma2<768, 5>(a, s);
+      } else {
+        launch_gemv<TW, 768, 1, 2, 0, 2>(a, s);
+      }
+      break;
+    case 4:
+      a.W = w.w_mproj[l]; a.N = D;
+      if (mf) launch_mfma2<3072, 1>(a, s);
+      else launch_gemv<TW, 3072, 4, 2, 1, 1>(a, s);
+      break;
+    case 5:
+      a.W = w.w_lm; a.N = VOCAB; a.ln_w = w.lnf;
+      if (mf) {
+        hipLaunchKernelGGL((ar_rows_kernel<0>), dim3((B + 3) / 4), dim3(256), 0, s, a);
+        launch_mfma2<768, 3>(a, s);
+      } else {
+        launch_gemv<TW, 768, 1, 2, 0, 3>(a, s);
+      }
+      break;
+  }
+}
+
+template <typename TW>
+static GemvArgs make_args(const ArWeights& w, const ArState& st, int kvdtype, int B, const float* emb_row) {
   GemvArgs a{};
   a.st = st;
   a.B = B;
@@ -1137,63 +1191,29 @@ static void ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B,
   a.wpe = w.wpe;
   a.emb_row = emb_row;
   a.prefetch = g_opt_prefetch_in;
-  if (emb_row) hipLaunchKernelGGL(ar_row_state_kernel, dim3(1), dim3(1), 0, s, st, slot, pos);
-  const bool mf = sizeof(TW) == 2 && g_opt_mfma_batch && B > 4 && B <= 64;
-  for (int l = 0; l < N_LAYER; ++l) {
-    a.layer = l;
-    // (layer 0: embed) + LN1 + c_attn + KV append
-    a.W = w.w_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
-    if (mf) {
-      if (l == 0) launch_mfma<768, 3, 0>(a, s);
-      else launch_mfma<768, 0, 0>(a, s);
-    } else if (l == 0) {
-      launch_gemv<TW, 768, 1, 2, 3, 0>(a, s);
-    } else {
-      launch_gemv<TW, 768, 1, 2, 0, 0>(a, s);
-    }
-    launch_attn(st, kvdtype, B, l, s);
-    a.W = w.w_aproj[l]; a.N = D;
-    if (mf) {
-      hipLaunchKernelGGL(ar_merge_kernel, dim3(B), dim3(256), 0, s, st);
-      launch_mfma<768, 4, 1>(a, s);
-    } else {
-      launch_gemv<TW, 768, 1, 1, 2, 1>(a, s);
-    }
-    a.W = w.w_fc[l]; a.N = DFF; a.ln_w = w.ln2[l];
-    if (mf) launch_mfma<768, 0, 2>(a, s);
-    else launch_gemv<TW, 768, 1, 2, 0, 2>(a, s);
-    a.W = w.w_mproj[l]; a.N = D;
-    if (mf) launch_mfma<3072, 1, 1>(a, s);
-    else launch_gemv<TW, 3072, 4, 2, 1, 1>(a, s);
-  }
-  a.W = w.w_lm; a.N = VOCAB; a.ln_w = w.lnf; a.dst = logits_dst;
-  if (mf) launch_mfma<768, 0, 3>(a, s);
-  else launch_gemv<TW, 768, 1, 2, 0, 3>(a, s);
+  return a;
 }
 
 template <typename TW>
+static void ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B, const float* emb_row, int slot,
+                      int pos, float* logits_dst, hipStream_t s) {
+  GemvArgs a = make_args<TW>(w, st, kvdtype, B, emb_row);
+  if (emb_row) hipLaunchKernelGGL(ar_row_state_kernel, dim3(1), dim3(1), 0, s, st, slot, pos);
+  for (int l = 0; l < N_LAYER; ++l)
+    for (int op = 0; op < 5; ++op) launch_op<TW>(op, a, w, l, kvdtype, B, s);
+  a.dst = logits_dst;
+  launch_op<TW>(5, a, w, N_LAYER - 1, kvdtype, B, s);
+}
+
+// Launch one op of the decode step `iters` times (bench.py times it with HIP events); layer 1.
+template <typename TW>
 static int ar_probe_impl(const ArWeights& w, const ArState& st, int kvdtype, int B, int which, int iters,
                          hipStream_t s) {
-  GemvArgs a{};
-  a.st = st;
-  a.B = B;
-  a.kv_bf16 = kvdtype == LVX_DTYPE_BF16;
-  a.text_table = w.text_table;
-  a.codebook = w.codebook;
-  a.wpe = w.wpe;
-  a.layer = 1;
+  if (which < 0 || which > 5) return -1;
+  GemvArgs a = make_args<TW>(w, st, kvdtype, B, nullptr);
+  a.dst = st.logits;
   hipLaunchKernelGGL(ar_rowinfo_init_kernel, dim3((B + 63) / 64), dim3(64), 0, s, st, B);
-  for (int i = 0; i < iters; ++i) {
-    switch (which) {
-      case 0: a.W = w.w_attn[1]; a.N = 3 * D; a.ln_w = w.ln1[1]; launch_gemv<TW, 768, 1, 2, 0, 0>(a, s); break;
-      case 1: launch_attn(st, kvdtype, B, 1, s); break;
-      case 2: a.W = w.w_aproj[1]; a.N = D; launch_gemv<TW, 768, 1, 1, 2, 1>(a, s); break;
-      case 3: a.W = w.w_fc[1]; a.N = DFF; a.ln_w = w.ln2[1]; launch_gemv<TW, 768, 1, 2, 0, 2>(a, s); break;
-      case 4: a.W = w.w_mproj[1]; a.N = D; launch_gemv<TW, 3072, 4, 2, 1, 1>(a, s); break;
-      case 5: a.W = w.w_lm; a.N = VOCAB; a.ln_w = w.lnf; a.dst = st.logits; launch_gemv<TW, 768, 1, 2, 0, 3>(a, s); break;
-      default: return -1;
-    }
-  }
+  for (int i = 0; i < iters; ++i) launch_op<TW>(which, a, w, which == 5 ? N_LAYER - 1 : 1, kvdtype, B, s);
   return 0;
 }
 

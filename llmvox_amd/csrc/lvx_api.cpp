@@ -351,7 +351,8 @@ int lvx_finalize(lvx_ctx* c) {
       (r = c->dalloc(&st.err, 4)) || (r = c->dalloc(&st.x, (size_t)S * D)) || (r = c->dalloc(&st.q, (size_t)S * D)) ||
       (r = c->dalloc(&st.part_o, (size_t)S * N_HEAD * NSPLIT * HD)) ||
       (r = c->dalloc(&st.part_ml, (size_t)S * N_HEAD * NSPLIT * 2)) || (r = c->dalloc(&st.h, (size_t)S * DFF)) ||
-      (r = c->dalloc(&st.logits, (size_t)S * VOCAB)) || (r = c->dalloc(&st.rowinfo, S)))
+      (r = c->dalloc(&st.logits, (size_t)S * VOCAB)) || (r = c->dalloc(&st.rowinfo, S)) ||
+      (r = c->dalloc(&st.xn, (size_t)S * D)) || (r = c->dalloc(&st.hb, (size_t)S * DFF)))
     return r;
   HIP_TRY(hipMemset(st.part_o, 0, (size_t)S * N_HEAD * NSPLIT * HD * 4));
   HIP_TRY(hipMemset(st.part_ml, 0, (size_t)S * N_HEAD * NSPLIT * 2 * 4));

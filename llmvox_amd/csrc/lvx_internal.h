@@ -47,6 +47,8 @@ struct ArState {
   float* part_o = nullptr;      // [B][8][NSPLIT][96]
   float* part_ml = nullptr;     // [B][8][NSPLIT][2]
   float* h = nullptr;           // [B][3072]
+  bf16_t* xn = nullptr;         // [B][768] bf16 operand rows (batched path)
+  bf16_t* hb = nullptr;         // [B][3072] bf16 h (batched path)
   float* logits = nullptr;      // [B][4096]
   void* kc = nullptr;           // [4][max_streams][8][max_pos][96]
   void* vc = nullptr;
