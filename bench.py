@@ -198,20 +198,42 @@ def main():
     pcm = torch.empty(S, 320 * chunk, dtype=torch.float32, device=dev)
     pcm_host = torch.empty(S, 320 * chunk, dtype=torch.float32, pin_memory=True)
 
+    # the codec of chunk c runs on a second HIP stream, overlapped with the AR decode of chunk
+    # c+1 (the AR chain is latency-bound and leaves most CUs idle); tok_plan is double-buffered
+    codec_stream = torch.cuda.Stream(device=dev)
+    tok_bufs = [tok_plan, torch.zeros_like(tok_plan)]
+    pcm_bufs = [pcm, torch.empty_like(pcm)]
+    ev_ar = [torch.cuda.Event(), torch.cuda.Event()]
+    ev_codec = [torch.cuda.Event(), torch.cuda.Event()]
+
     def run_chunk(c):
+        i = c & 1
+        main = torch.cuda.current_stream(dev)
+        main.wait_event(ev_codec[i])  # tok_bufs[i] is free again (its decode has read it)
         text_plan.copy_(mine[:, c * chunk:(c + 1) * chunk])
         rowstep.zero_()
-        eng.ar_steps(chunk, slots, text_plan, rowstep, tok_plan)
-        eng.decode_codes(tok_plan, 0, out=pcm)
-        if dist is not None:
-            gather_pcm(pcm, dist, rank, world)  # PCM back to rank 0 (outbound exchange)
-        pcm_host.copy_(pcm, non_blocking=True)
+        eng.ar_steps(chunk, slots, text_plan, rowstep, tok_bufs[i])
+        ev_ar[i].record(main)
+        with torch.cuda.stream(codec_stream):
+            codec_stream.wait_event(ev_ar[i])
+            eng.decode_codes(tok_bufs[i], 0, out=pcm_bufs[i])
+            if dist is not None:
+                gather_pcm(pcm_bufs[i], dist, rank, world)  # PCM back to rank 0 (outbound exchange)
+            pcm_host.copy_(pcm_bufs[i], non_blocking=True)
+            ev_codec[i].record(codec_stream)
 
     def reset_all():
         for s in range(S):
             eng.reset_slot(s)
 
-    # ---- warmup (also captures the graph), then reset to position 0
+    # ---- setup: capture the decode graphs for both token buffers (untimed), warmup, reset
+    reset_all()
+    for i in range(2):
+        rowstep.zero_()
+        text_plan.copy_(mine[:, :chunk])
+        eng.ar_steps(17, slots, text_plan, rowstep, tok_bufs[i])
+        eng.decode_codes(tok_bufs[i], 0, out=pcm_bufs[i])
+    torch.cuda.synchronize()
     reset_all()
     for c in range(Wm):
         run_chunk(c)
@@ -239,7 +261,7 @@ def main():
 
     total_tokens = world * S * K * chunk
     value = total_tokens / dt
-    toks_rank0 = tok_plan[0].cpu().numpy()
+    toks_rank0 = tok_bufs[(K - 1) & 1][0].cpu().numpy()
 
     # ---- p50 first-chunk latency: fresh segment -> first 10-token dump (3,200 samples) on host
     lat = []

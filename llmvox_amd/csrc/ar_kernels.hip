@@ -811,20 +811,28 @@ __global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer, 
   float m = -INFINITY, l = 0.f, o[24];
 #pragma unroll
   for (int i = 0; i < 24; ++i) o[i] = 0.f;
-  for (int kb = k0; kb < k1; kb += ATK) {
+  // register double buffer: the next tile's K/V pieces are in flight while this tile is computed
+  KvPiece<TKV> kp[3], vp[3];
+  auto issue = [&](int kb) {
     const int key = kb + kq;
-    const bool valid = key < k1;
-    float kf[24], vf[24];
-    if (valid) {
-      KvPiece<TKV> kp[3], vp[3];
+    if (key < k1) {
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         kp[i].load(Kg + (size_t)key * HD + part * 24 + i * 8);
         vp[i].load(Vg + (size_t)key * HD + part * 24 + i * 8);
       }
+    }
+  };
+  issue(k0);
+  for (int kb = k0; kb < k1; kb += ATK) {
+    const int key = kb + kq;
+    const bool valid = key < k1;
+    float kf[24], vf[24];
+    if (valid) {
 #pragma unroll
       for (int i = 0; i < 3; ++i) { kp[i].get(kf + 8 * i); vp[i].get(vf + 8 * i); }
     }
+    if (kb + ATK < k1) issue(kb + ATK);
     float sc = 0.f;
     if (valid) {
 #pragma unroll
@@ -1028,26 +1036,39 @@ __global__ __launch_bounds__(256) void ar_rows_kernel(GemvArgs a) {
 
 // split-KV merge for the batched path: y[b] (bf16) into st.xn
 __global__ __launch_bounds__(256) void ar_merge_bf16_kernel(ArState st, int ns_max) {
+  __shared__ float cf[N_HEAD * NSPLIT];
   const int b = blockIdx.x, tid = threadIdx.x;
   const int4 ri = st.rowinfo[b];
+  // every load up front: one (m, l) pair per thread (8 heads x 16 splits) and 3 x 16 partials
+  float2 ml = make_float2(-INFINITY, 0.f);
+  if (tid < N_HEAD * NSPLIT) ml = reinterpret_cast<const float2*>(st.part_ml)[(size_t)b * N_HEAD * NSPLIT + tid];
+  float pv[3][NSPLIT];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int e = tid + 256 * j, head = e / HD, d = e - head * HD;
+    const float* po = st.part_o + ((size_t)(b * N_HEAD + head) * NSPLIT) * HD + d;
+#pragma unroll
+    for (int i = 0; i < NSPLIT; ++i) pv[j][i] = po[(size_t)i * HD];
+  }
+  if (tid < N_HEAD * NSPLIT) {
+    const int ns = ri.x < 0 ? 0 : min(ns_max, (ri.y + 1 + 63) / 64);
+    const bool on = (tid & (NSPLIT - 1)) < ns && ml.x != -INFINITY;
+    float M = on ? ml.x : -INFINITY;
+#pragma unroll
+    for (int o = 1; o < NSPLIT; o <<= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
+    const float f = on ? expf(ml.x - M) : 0.f;
+    float den = f * ml.y;
+#pragma unroll
+    for (int o = 1; o < NSPLIT; o <<= 1) den += __shfl_xor(den, o, 64);
+    cf[tid] = ns > 0 ? f / den : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int e = tid + 256 * j, head = e / HD;
     float y = 0.f;
-    if (ri.x >= 0) {
-      const int ns = min(ns_max, (ri.y + 1 + 63) / 64);
-      const float* ml = st.part_ml + ((size_t)(b * N_HEAD + head) * NSPLIT) * 2;
-      const float* po = st.part_o + ((size_t)(b * N_HEAD + head) * NSPLIT) * HD + d;
-      float M = -INFINITY;
-      for (int i = 0; i < ns; ++i) M = fmaxf(M, ml[2 * i]);
-      float num = 0.f, den = 0.f;
-      for (int i = 0; i < ns; ++i) {
-        const float f = (ml[2 * i] == -INFINITY) ? 0.f : expf(ml[2 * i] - M);
-        num += f * po[(size_t)i * HD];
-        den += f * ml[2 * i + 1];
-      }
-      y = num / den;
-    }
+#pragma unroll
+    for (int i = 0; i < NSPLIT; ++i) y += cf[head * NSPLIT + i] * pv[j][i];
     st.xn[(size_t)b * D + e] = f32_to_bf16(y);
   }
 }
