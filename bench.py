@@ -103,9 +103,10 @@ def probe_kernels(eng, slots, t, wbytes, kvbytes, iters=200):
 
 
 # ---------------------------------------------------------------------------------------
-def cpu_baseline(n_chunks, chunk, max_seconds=60.0):
+def cpu_baseline(n_chunks, chunk, min_seconds=10.0, max_seconds=30.0):
     """The reference CPU eager path (oracle restatement: fp32, B=1, O(t) history/KV cats),
-    on this host's cores, on the same chunked workload (bounded)."""
+    on this host's cores, on the same chunked workload; whole utterances are repeated until
+    at least ``min_seconds`` of CPU work is timed (bounded by ``max_seconds``)."""
     from llmvox_amd import weights as LW
     from oracle import reference_cpu as R
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
@@ -116,22 +117,27 @@ def cpu_baseline(n_chunks, chunk, max_seconds=60.0):
     cb = Wc[R.CODEBOOK_KEY]
     ids = sentence_ids(SENTENCE)
     t0 = time.perf_counter()
-    hist, kv, prev, done = None, None, None, 0
+    done, passes = 0, 0
     with torch.inference_mode():
-        for c in range(n_chunks):
-            toks = []
-            for i in range(c * chunk, (c + 1) * chunk):
-                tid = ids[i] if i < len(ids) else 384
-                te = table[tid].view(1, 1, -1)
-                se = torch.zeros(1, 1, 512) if i == 0 else cb[prev].view(1, 1, -1)
-                x = R.build_input(te, se)
-                hist = x if hist is None else torch.cat([hist, x], dim=1)
-                logits, kv = R.gpt_forward(W, hist, kv)
-                prev = R.greedy_token(logits)
-                toks.append(prev)
-            pcm = R.decode_codes(Wc, torch.tensor([toks]))
-            _ = pcm.numpy().astype("float32").tobytes()
-            done += chunk
+        while time.perf_counter() - t0 < min_seconds:
+            hist, kv, prev = None, None, None
+            passes += 1
+            for c in range(n_chunks):
+                toks = []
+                for i in range(c * chunk, (c + 1) * chunk):
+                    tid = ids[i] if i < len(ids) else 384
+                    te = table[tid].view(1, 1, -1)
+                    se = torch.zeros(1, 1, 512) if i == 0 else cb[prev].view(1, 1, -1)
+                    x = R.build_input(te, se)
+                    hist = x if hist is None else torch.cat([hist, x], dim=1)
+                    logits, kv = R.gpt_forward(W, hist, kv)
+                    prev = R.greedy_token(logits)
+                    toks.append(prev)
+                pcm = R.decode_codes(Wc, torch.tensor([toks]))
+                _ = pcm.numpy().astype("float32").tobytes()
+                done += chunk
+                if time.perf_counter() - t0 > max_seconds:
+                    break
             if time.perf_counter() - t0 > max_seconds:
                 break
     dt = time.perf_counter() - t0
@@ -146,7 +152,7 @@ def cpu_baseline(n_chunks, chunk, max_seconds=60.0):
         pass
     return {"value": done / dt, "unit": "speech tokens/s", "cores": threads, "kind": "port",
             "sample": f"{done} tokens = {done // chunk} x ({chunk} fp32 AR steps + codec decode of {chunk} "
-                      f"frames), 1 stream, oracle/reference_cpu.py, {dt:.1f} s on {cpu}"}
+                      f"frames) over {passes} utterance(s) of {n_chunks * chunk} positions, 1 stream, oracle/reference_cpu.py, {dt:.1f} s on {cpu}"}
 
 
 # ---------------------------------------------------------------------------------------
@@ -160,6 +166,10 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--probe-pos", type=int, default=0,
+                    help="KV position of the roofline probe (default: steps * chunk, where the run ends)")
+    ap.add_argument("--no-graphs", action="store_true",
+                    help="launch the decode step kernel by kernel (for rocprofv3 --pmc passes)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -179,6 +189,8 @@ def main():
                        max_codec_frames=S * chunk)
     dev = eng.device
     torch.cuda.set_device(dev)
+    if args.no_graphs:
+        eng.set_graphs(False)
 
     # ---- text plans: stream 0 of rank 0 speaks the config sentence; others seeded sentences
     n_pos = max(K, Wm) * chunk
@@ -288,14 +300,15 @@ def main():
     rl, kern = None, None
     if not args.no_probe:
         reset_all()
+        ppos = args.probe_pos or K * chunk
         for s in range(S):
-            eng.set_slot(s, K * chunk - 1, 0)
+            eng.set_slot(s, ppos - 1, 0)
         wb = 2 if args.dtype == "bf16" else 4
-        kern = probe_kernels(eng, slots, K * chunk, wb, wb)
+        kern = probe_kernels(eng, slots, ppos, wb, wb)
         dom = max(kern.values(), key=lambda r: r["share_us_per_step"])
         rl = {"bound": "hbm", "kernel": dom["name"], "achieved": round(dom["gbs"], 1), "peak": HBM_PEAK_GBS,
               "unit": "GB/s", "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4), "traffic": None,
-              "bytes_per_launch": dom["bytes"], "avg_us": round(dom["avg_us"], 3)}
+              "bytes_per_launch": dom["bytes"], "avg_us": round(dom["avg_us"], 3), "kv_positions": ppos}
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
             try:
