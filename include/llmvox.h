@@ -113,12 +113,15 @@ int lvx_check_errors(lvx_ctx* ctx, void* stream);
 int lvx_stream_set(lvx_ctx* ctx, int slot, int pos, int prev_token, void* stream);
 /* Measurement hook (bench.py): launch one kernel class of the decode step `iters` times for the
  * batch rows `slots` at their current positions (0 c_attn, 1 attention, 2 c_proj+merge,
- * 3 c_fc, 4 mlp c_proj, 5 lm_head). Writes only scratch and the K/V row at the current
- * position (which the next real step overwrites). */
+ * 3 c_fc (with the bf16 fused MLP at B <= 2: c_fc + gelu + mlp c_proj), 4 mlp c_proj, 5 lm_head).
+ * Writes only scratch and the K/V row at the current position (which the next real step
+ * overwrites). LVX_E_STATE when the op has no kernel of its own at this B (fused). */
 int lvx_probe_kernel(lvx_ctx* ctx, int which, int B, const int32_t* slots_dev, int iters, void* stream);
 /* Host-side view of a slot's position (synchronises the stream). */
 int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
-/* Development switches for in-process A/B timing ("gemv_reg": register-path GEMV for B <= 4). */
+/* Kernel-variant switches for in-process A/B timing: "gemv_reg" (register-path GEMV, B <= 4),
+ * "attn_v2", "cproj_b1", "prefetch_in", "mfma_batch" (bf16 MFMA path, 4 < B <= 32),
+ * "fuse_mlp" (bf16 fused MLP, B <= 2), "fuse_argmax" (greedy select inside lm_head, B <= 4). */
 int lvx_set_option(lvx_ctx* ctx, const char* name, int value);
 /* Enable/disable HIP-graph replay of lvx_ar_step for a given B (default on). */
 int lvx_set_graphs(lvx_ctx* ctx, int enable);

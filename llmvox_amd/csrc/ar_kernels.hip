@@ -24,6 +24,7 @@ namespace lvx {
 //   IN  0: in = LayerNorm(x[b]) * ln_w            (eps 1e-5, no bias; src/model.py:37-38)
 //   IN  1: in = h[b] (fp32, K = 3072)
 //   IN  2: in = merge of the split-KV attention partials (flash-decoding combine)
+//   IN  4: in = LayerNorm(x[b] + sum_c yacc[c][b]) (the fused MLP's pending output)
 //   IN  3: layer-0 c_attn: builds x[b] first (a2-a4: text row, codebook row of the previous
 //          token or 0 at position 0, L2-normalise eps 1e-8, + wpe[pos]; or, for the drop-in
 //          row forward, the caller's row + wpe[pos]), block 0 stores it, then LayerNorm.
@@ -51,7 +52,46 @@ struct GemvArgs {
   const float* wpe;
   const float* emb_row;  // drop-in row mode when non-null
   int prefetch;          // inputs of the first group issued before the weights (option "prefetch_in")
+  // fused MLP (ar_mlp_fused_kernel): its output sits in YCOPIES accumulators until c_proj folds it in
+  float* yacc;           // non-null when the step runs the fused MLP
+  int add_y;             // c_proj: fold the accumulators into x (layers >= 1; 0 at layer 0 = just clear)
 };
+
+// ---------------------------------------------------------------------------------
+// greedy select (streaming_server.py:342-347): argmax with first-index ties, top1-top2 margin,
+// then the slot's prev token / position / plan step advance (shared by ar_argmax_kernel and the
+// fused lm_head tail).
+// ---------------------------------------------------------------------------------
+struct Best {
+  float v, v2;
+  int i;
+};
+__device__ __forceinline__ Best best_merge(Best a, Best c) {
+  const bool cb = (c.v > a.v) || (c.v == a.v && c.i < a.i);
+  Best r;
+  if (cb) { r.v = c.v; r.i = c.i; r.v2 = fmaxf(c.v2, a.v); }
+  else { r.v = a.v; r.i = a.i; r.v2 = fmaxf(a.v2, c.v); }
+  return r;
+}
+
+__device__ __forceinline__ int4 make_rowinfo(const ArState& st, int b, int s, int p, int j, int prev);
+
+__device__ __forceinline__ void argmax_commit(const ArState& st, int b, int4 ri, Best r) {
+  if (!st.rowstep) return;  // measurement probe: no plan bound, state is not advanced
+  const int s = ri.x;
+  const int j = st.rowstep[b];
+  if (j < st.plan_stride) {
+    st.tok_plan[(size_t)b * st.plan_stride + j] = r.i;
+    if (st.margin_plan) st.margin_plan[(size_t)b * st.plan_stride + j] = r.v - r.v2;
+  }
+  st.prev[s] = r.i;
+  st.pos[s] = ri.y + 1;
+  st.rowstep[b] = j + 1;
+  st.rowinfo[b] = make_rowinfo(st, b, s, ri.y + 1, j + 1, r.i);
+}
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
 
 template <typename TW> struct WReg;
 template <> struct WReg<float> {
@@ -94,19 +134,56 @@ __device__ __forceinline__ void wave_ln_to_lds(float4 (&v)[3], const float* __re
   }
 }
 
+// x[b] (IN 0) or x[b] + sum_c yacc[c][b] (IN 4) in the lane layout k = j * 256 + lane * 4: the
+// loads are issued by xrow_issue and summed by xrow_sum, so a prefetch does not wait on them
+template <int IN>
+struct XRow {
+  float4 x[3];
+  float4 y[IN == 4 ? YCOPIES : 1][3];
+};
+template <int IN>
+__device__ __forceinline__ void xrow_issue(const GemvArgs& a, int b, int lane, XRow<IN>& r) {
+  const float* xr = a.st.x + (size_t)b * D;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) r.x[j] = *reinterpret_cast<const float4*>(xr + j * 256 + lane * 4);
+  if constexpr (IN == 4) {
+#pragma unroll
+    for (int c = 0; c < YCOPIES; ++c)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        r.y[c][j] = *reinterpret_cast<const float4*>(a.yacc + ((size_t)c * a.st.max_streams + b) * D + j * 256 + lane * 4);
+  }
+}
+template <int IN>
+__device__ __forceinline__ void xrow_sum(const XRow<IN>& r, float4 (&v)[3]) {
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    float4 t = r.x[j];
+    if constexpr (IN == 4) {
+#pragma unroll
+      for (int c = 0; c < YCOPIES; ++c) { t.x += r.y[c][j].x; t.y += r.y[c][j].y; t.z += r.y[c][j].z; t.w += r.y[c][j].w; }
+    }
+    v[j] = t;
+  }
+}
+
 template <int K, int IN>
 __device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, float* aux, int g0, int bg,
-                                                 const float4 (&xpre)[3], int4 ripre, bool prefetched) {
+                                                 const XRow<IN == 4 ? 4 : 0>& xpre, int4 ripre, bool prefetched) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  if (IN == 0 || IN == 3) {
+  if (IN == 0 || IN == 3 || IN == 4) {
     for (int bb = wave; bb < bg; bb += 4) {  // one wave per row
       const int b = g0 + bb;
       const bool pre = prefetched && g0 == 0 && bb == wave;  // this row was prefetched before the weights
       float4 v[3];
-      if (IN == 0) {
-        const float* xr = a.st.x + (size_t)b * D;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) v[j] = pre ? xpre[j] : *reinterpret_cast<const float4*>(xr + j * 256 + lane * 4);
+      if (IN == 0 || IN == 4) {
+        if (pre) {
+          xrow_sum(xpre, v);
+        } else {
+          XRow<IN == 4 ? 4 : 0> xr;
+          xrow_issue(a, b, lane, xr);
+          xrow_sum(xr, v);
+        }
       } else if (a.emb_row) {  // drop-in row forward: caller's normalised row + wpe[pos]
         const int p = a.st.rowinfo[0].y;
         const float* wr = a.wpe + (size_t)p * D;
@@ -220,13 +297,29 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
   const int row0 = (blockIdx.x * WROWS + rg) * RPW;
   // inputs of the first batch group first (vmcnt retires in issue order): the LayerNorm /
   // embedding math then overlaps the weight stream instead of waiting behind it
-  float4 xpre[3];
+  XRow<IN == 4 ? 4 : 0> xpre;
   int4 ripre = make_int4(-1, 0, 0, 0);
   const bool prefetched = a.prefetch && wave < min(BG, a.B);
-  if ((IN == 0 || IN == 3) && prefetched) {
-    if (IN == 0) {
+  // control record of this lane's epilogue row in the first batch group (bb = lane % BG): the
+  // KV append needs (slot, pos); loading it here keeps it off the epilogue's critical path
+  int4 riep = make_int4(-1, 0, 0, 0);
+  if (OUT == 0) riep = a.st.rowinfo[min(lane % BG, a.B - 1)];
+  // residual epilogue (OUT 1): this lane's (row, batch row) of the first group is (row0 + lane / BG,
+  // lane % BG); its x element (and, for c_proj after a fused MLP, the pending accumulators) is
+  // loaded now instead of behind the dot products
+  float xep = 0.f, yep[YCOPIES];
+  if constexpr (OUT == 1) {
+    const int n = row0 + lane / BG, b = lane % BG;
+    if (lane < RPW * BG && n < a.N && b < a.B) {
+      xep = a.st.x[(size_t)b * D + n];
+      if (IN == 2 && a.yacc)
 #pragma unroll
-      for (int j = 0; j < 3; ++j) xpre[j] = *reinterpret_cast<const float4*>(a.st.x + (size_t)wave * D + j * 256 + lane * 4);
+        for (int c = 0; c < YCOPIES; ++c) yep[c] = a.yacc[((size_t)c * a.st.max_streams + b) * D + n];
+    }
+  }
+  if ((IN == 0 || IN == 3 || IN == 4) && prefetched) {
+    if (IN == 0 || IN == 4) {
+      xrow_issue(a, wave, lane, xpre);
     } else {
       ripre = a.st.rowinfo[wave];
     }
@@ -306,7 +399,7 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
           } else {
             const int c = (n - D) % D, which = (n - D) / D;
             const int head = c / HD, d = c - head * HD;
-            const int4 ri = a.st.rowinfo[b];
+            const int4 ri = g0 == 0 ? riep : a.st.rowinfo[b];
             const int s = ri.x, p = ri.y;
             if (s < 0) continue;
             const size_t idx =
@@ -315,14 +408,81 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
             else reinterpret_cast<float*>(which ? a.st.vc : a.st.kc)[idx] = v;
           }
         } else if (OUT == 1) {
-          a.st.x[(size_t)b * D + n] += v;
+          float* xp = a.st.x + (size_t)b * D + n;
+          float t = g0 == 0 ? xep : *xp;
+          if (IN == 2 && a.yacc) {  // c_proj: fold the fused MLP's accumulators into x and clear them
+#pragma unroll
+            for (int c = 0; c < YCOPIES; ++c) {
+              float* yp = a.yacc + ((size_t)c * a.st.max_streams + b) * D + n;
+              if (a.add_y) t += g0 == 0 ? yep[c] : *yp;
+              *yp = 0.f;
+            }
+          }
+          *xp = t + v;
         } else if (OUT == 2) {
           a.st.h[(size_t)b * DFF + n] = gelu_tanh(v);
         } else {
           a.dst[(size_t)b * a.N + n] = v;
+          if (OUT == 4) part[wave][r][bb] = v;
         }
       }
     }
+  }
+  if constexpr (OUT == 4) {
+    // fused greedy select (B <= BG: one batch group). Each block publishes its top1/top2 per row
+    // as two 8-byte granules with write-through (sc1) atomic stores, drains them, and draws a
+    // ticket; the last arriving block reads every block's granules with sc1 loads (no acquire
+    // fence needed for this hand-off form, cdna_hip_programming.md Guideline 16 R1) and commits.
+    __syncthreads();
+    if (tid < a.B) {
+      Best r{-INFINITY, -INFINITY, 0x7fffffff};
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+#pragma unroll
+        for (int rr = 0; rr < RPW; ++rr) {
+          const int n = (blockIdx.x * 4 + w) * RPW + rr;
+          if (n < a.N) r = best_merge(r, Best{part[w][rr][tid], -INFINITY, n});
+        }
+      gu64* g = ((gu64*)a.st.lmbest) + ((size_t)blockIdx.x * 4 + tid) * 2;
+      __hip_atomic_store(g, ((unsigned long long)(unsigned)r.i << 32) | __float_as_uint(r.v), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(g + 1, (unsigned long long)__float_as_uint(r.v2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned tk = __hip_atomic_fetch_add(((gu32*)a.st.ticket), 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+      part[0][0][0] = (tk == gridDim.x - 1) ? 1.f : 0.f;
+    }
+    __syncthreads();
+    if (part[0][0][0] == 0.f) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (wave < a.B) {  // wave b reduces row b over all blocks
+      // all granule loads in flight at once (one round trip): gridDim.x <= 8 * 64 (host-checked)
+      unsigned long long g0v[8], g1v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int blk = lane + 64 * k;
+        if (blk < (int)gridDim.x) {
+          const gu64* g = ((const gu64*)a.st.lmbest) + ((size_t)blk * 4 + wave) * 2;
+          g0v[k] = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          g1v[k] = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      Best r{-INFINITY, -INFINITY, 0x7fffffff};
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (lane + 64 * k < (int)gridDim.x)
+          r = best_merge(r, Best{__uint_as_float((unsigned)g0v[k]), __uint_as_float((unsigned)g1v[k]), (int)(g0v[k] >> 32)});
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        Best c{__shfl_xor(r.v, o, 64), __shfl_xor(r.v2, o, 64), __shfl_xor(r.i, o, 64)};
+        r = best_merge(r, c);
+      }
+      if (lane == 0) argmax_commit(a.st, wave, a.st.rowinfo[wave], r);
+    }
+    if (tid == 0) __hip_atomic_store(((gu32*)a.st.ticket), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -543,6 +703,14 @@ __global__ __launch_bounds__(256) void ar_cproj_b1_kernel(GemvArgs a) {
     for (int i = 0; i < NSPLIT; ++i) pv[j][i] = po[(size_t)i * HD];
   }
   const int row0 = (blockIdx.x * 4 + wave) * RPW;
+  // residual epilogue operands of lane r < RPW (row row0 + r): x and the fused MLP's accumulators
+  float xep = 0.f, yep[YCOPIES];
+  if (lane < RPW && row0 + lane < a.N) {
+    xep = a.st.x[row0 + lane];
+    if (a.yacc)
+#pragma unroll
+      for (int c = 0; c < YCOPIES; ++c) yep[c] = a.yacc[(size_t)c * a.st.max_streams * D + row0 + lane];
+  }
   const TW* __restrict__ W = reinterpret_cast<const TW*>(a.W);
   typename WReg<TW>::T wr[RPW][3];
 #pragma unroll
@@ -589,7 +757,99 @@ __global__ __launch_bounds__(256) void ar_cproj_b1_kernel(GemvArgs a) {
 #pragma unroll
   for (int r = 0; r < RPW; ++r) {
     const float v = wave_sum(acc[r]);
-    if (lane == r && row0 + r < a.N) a.st.x[row0 + r] += v;
+    if (lane == r && row0 + r < a.N) {
+      float t = xep;
+      if (a.yacc) {
+#pragma unroll
+        for (int c = 0; c < YCOPIES; ++c) {
+          if (a.add_y) t += yep[c];
+          a.yacc[(size_t)c * a.st.max_streams * D + row0 + r] = 0.f;
+        }
+      }
+      a.st.x[row0 + r] = t + v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Fused MLP for B <= 2 rows (bf16 weights; option "fuse_mlp"): block k owns h rows 16k..16k+15:
+//   h = gelu_tanh(c_fc(LayerNorm(x) * ln_2))      (its 16 rows of c_fc, 24.6 KB of weights)
+//   y += mlp.c_proj[:, 16k:16k+16] h               (its 16 columns of c_proj, thread-packed, 24.6 KB)
+// The 768-wide partial is added with no-return fp32 atomics (256 contiguous bytes per wave
+// instruction) into accumulator copy k % YCOPIES; the next c_attn / lm_head prologue reads
+// x + sum of copies, and the next c_proj folds them into x and clears them. This removes the
+// c_fc -> c_proj kernel boundary (one of the per-layer seams); the summation order of y is not
+// fixed, so it is a bf16 performance-mode path only.
+// ---------------------------------------------------------------------------------
+template <int BG>
+__global__ __launch_bounds__(256) void ar_mlp_fused_kernel(GemvArgs a, const bf16_t* __restrict__ Wfc,
+                                                           const bf16_t* __restrict__ Wpk) {
+  __shared__ __attribute__((aligned(16))) float xs[BG][D];
+  __shared__ float hs[BG][16];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int n0 = blockIdx.x * 16;
+  // issue order: x rows (LayerNorm input), c_fc rows, packed c_proj columns
+  float4 xv[3];
+  if (wave < BG) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) xv[j] = *reinterpret_cast<const float4*>(a.st.x + (size_t)wave * D + j * 256 + lane * 4);
+  }
+  uint2 wf[4][3];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      wf[r][i] = *reinterpret_cast<const uint2*>(Wfc + (size_t)(n0 + wave * 4 + r) * D + i * 256 + lane * 4);
+  uint4 wp[6];
+  const uint4* pk = reinterpret_cast<const uint4*>(Wpk + ((size_t)blockIdx.x * 256 + tid) * 48);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) wp[i] = pk[i];
+  if (wave < BG) wave_ln_to_lds(xv, a.ln_w, xs[wave], lane);
+  __syncthreads();
+  float acc[4][BG];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int bb = 0; bb < BG; ++bb) acc[r][bb] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int bb = 0; bb < BG; ++bb) {
+      const float4 x4 = *reinterpret_cast<const float4*>(&xs[bb][i * 256 + lane * 4]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float4 w = WReg<bf16_t>::f(wf[r][i]);
+        acc[r][bb] += (w.x * x4.x + w.y * x4.y) + (w.z * x4.z + w.w * x4.w);
+      }
+    }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int bb = 0; bb < BG; ++bb) {
+      const float v = wave_sum(acc[r][bb]);
+      if (lane == 0) hs[bb][wave * 4 + r] = gelu_tanh(v);
+    }
+  __syncthreads();
+  // thread tid: outputs e = tid + 256 jj; packed weights jj * 16 + j = W[e][n0 + j]
+  float* y = a.yacc + (size_t)(blockIdx.x % YCOPIES) * a.st.max_streams * D;
+#pragma unroll
+  for (int bb = 0; bb < BG; ++bb) {
+    float h[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) h[j] = hs[bb][j];
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const uint4 u = wp[jj * 2 + q];
+        const uint32_t wv[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+          t += __uint_as_float(wv[m] << 16) * h[q * 8 + 2 * m] + __uint_as_float(wv[m] & 0xffff0000u) * h[q * 8 + 2 * m + 1];
+      }
+      atomicAdd(y + (size_t)bb * D + tid + 256 * jj, t);
+    }
   }
 }
 
@@ -888,18 +1148,6 @@ __global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer, 
 // greedy select (streaming_server.py:342-347): argmax with first-index ties, top1-top2
 // margin, then the slot's prev token / position / plan step advance.
 // ---------------------------------------------------------------------------------
-struct Best {
-  float v, v2;
-  int i;
-};
-__device__ __forceinline__ Best best_merge(Best a, Best c) {
-  const bool cb = (c.v > a.v) || (c.v == a.v && c.i < a.i);
-  Best r;
-  if (cb) { r.v = c.v; r.i = c.i; r.v2 = fmaxf(c.v2, a.v); }
-  else { r.v = a.v; r.i = a.i; r.v2 = fmaxf(a.v2, c.v); }
-  return r;
-}
-
 __global__ __launch_bounds__(256) void ar_argmax_kernel(ArState st) {
   __shared__ float sv[4], sv2[4];
   __shared__ int si[4];
@@ -928,15 +1176,7 @@ __global__ __launch_bounds__(256) void ar_argmax_kernel(ArState st) {
   if (tid == 0) {
     Best r{sv[0], sv2[0], si[0]};
     for (int w = 1; w < 4; ++w) r = best_merge(r, Best{sv[w], sv2[w], si[w]});
-    const int j = st.rowstep[b];
-    if (j < st.plan_stride) {
-      st.tok_plan[(size_t)b * st.plan_stride + j] = r.i;
-      if (st.margin_plan) st.margin_plan[(size_t)b * st.plan_stride + j] = r.v - r.v2;
-    }
-    st.prev[s] = r.i;
-    st.pos[s] = ri.y + 1;
-    st.rowstep[b] = j + 1;
-    st.rowinfo[b] = make_rowinfo(st, b, s, ri.y + 1, j + 1, r.i);
+    argmax_commit(st, b, ri, r);
   }
 }
 
@@ -947,12 +1187,20 @@ int g_opt_gemv_reg = 0;  // runtime A/B switches (lvx_set_option); measured: LDS
 int g_opt_attn_v2 = 1;
 int g_opt_cproj_b1 = 1;
 int g_opt_prefetch_in = 1;
+int g_opt_fuse_argmax = 0;  // measured at B = 1: the in-launch tail costs more than the boundary it saves
+int g_opt_fuse_mlp = 1;
 
 template <typename TW, int K, int KW, int RPW, int IN, int OUT>
 static void launch_gemv(const GemvArgs& a, hipStream_t s) {
   const int rows_per_block = (4 / KW) * RPW;
   dim3 grid((a.N + rows_per_block - 1) / rows_per_block);
   constexpr int BGMAX = (K == 768) ? 16 : 4;
+  if constexpr (OUT == 4) {  // fused select: one batch group of <= 4 rows, <= 512 blocks (launch_op checks)
+    if (a.B <= 1) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 1, IN, OUT>), grid, dim3(256), 0, s, a);
+    else if (a.B <= 2) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 2, IN, OUT>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 4, IN, OUT>), grid, dim3(256), 0, s, a);
+    return;
+  }
   if constexpr (IN == 2 && OUT == 1 && K == 768 && KW == 1) {
     if (g_opt_cproj_b1 && a.B == 1) { hipLaunchKernelGGL((ar_cproj_b1_kernel<TW, RPW>), grid, dim3(256), 0, s, a); return; }
   }
@@ -1147,11 +1395,28 @@ static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_
 
 // one op of the decode step, with the B-dependent kernel choice (shared by the step and the probes)
 // op: 0 c_attn (layer 0: + embedding) 1 attention 2 c_proj (+ split merge) 3 c_fc 4 mlp c_proj 5 lm_head
+// fused lm_head + greedy select (B <= 4 GEMV path, fused step only); returns whether op 5 did the select
 template <typename TW>
-static void launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtype, int B, hipStream_t s) {
+static bool fused_select(int B) {
+  static_assert(VOCAB / 8 <= 512 && VOCAB / 8 <= LM_MAX_BLOCKS, "fused select: lm_head grid must fit the tail");
+  return g_opt_fuse_argmax && B <= 4;
+}
+
+template <typename TW>
+static bool fused_mlp(int B) {
+  return sizeof(TW) == 2 && g_opt_fuse_mlp && B <= 2;
+}
+
+// returns false when the op has no kernel of its own at this B (mlp c_proj inside the fused MLP)
+template <typename TW>
+static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtype, int B, hipStream_t s,
+                      bool select = false) {
   const bool mf = sizeof(TW) == 2 && g_opt_mfma_batch && B > 4 && B <= 32;
+  const bool fm = fused_mlp<TW>(B);
   const int nsm = mf ? attn_ns_max(B) : NSPLIT;
   a.layer = l;
+  a.yacc = fm ? a.st.yacc : nullptr;
+  a.add_y = l > 0;
   switch (op) {
     case 0:
       a.W = w.w_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
@@ -1161,6 +1426,8 @@ static void launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
         launch_mfma2<768, 0>(a, s);
       } else if (l == 0) {
         launch_gemv<TW, 768, 1, 2, 3, 0>(a, s);
+      } else if (fm) {
+        launch_gemv<TW, 768, 1, 2, 4, 0>(a, s);
       } else {
         launch_gemv<TW, 768, 1, 2, 0, 0>(a, s);
       }
@@ -1177,7 +1444,12 @@ static void launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       break;
     case 3:
       a.W = w.w_fc[l]; a.N = DFF; a.ln_w = w.ln2[l];
-      if (mf) {
+      if (fm) {
+        const bf16_t* wfc = reinterpret_cast<const bf16_t*>(w.w_fc[l]);
+        const bf16_t* wpk = reinterpret_cast<const bf16_t*>(w.w_mproj_pk[l]);
+        if (B <= 1) hipLaunchKernelGGL((ar_mlp_fused_kernel<1>), dim3(DFF / 16), dim3(256), 0, s, a, wfc, wpk);
+        else hipLaunchKernelGGL((ar_mlp_fused_kernel<2>), dim3(DFF / 16), dim3(256), 0, s, a, wfc, wpk);
+      } else if (mf) {
         hipLaunchKernelGGL((ar_rows_kernel<0>), dim3((B + 3) / 4), dim3(256), 0, s, a);
         launch_mfma2<768, 5>(a, s);
       } else {
@@ -1186,6 +1458,7 @@ static void launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       break;
     case 4:
       a.W = w.w_mproj[l]; a.N = D;
+      if (fm) return false;
       if (mf) launch_mfma2<3072, 1>(a, s);
       else launch_gemv<TW, 3072, 4, 2, 1, 1>(a, s);
       break;
@@ -1194,11 +1467,17 @@ static void launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       if (mf) {
         hipLaunchKernelGGL((ar_rows_kernel<0>), dim3((B + 3) / 4), dim3(256), 0, s, a);
         launch_mfma2<768, 3>(a, s);
+      } else if (select) {
+        if (fm) launch_gemv<TW, 768, 1, 2, 4, 4>(a, s);
+        else launch_gemv<TW, 768, 1, 2, 0, 4>(a, s);
+      } else if (fm) {
+        launch_gemv<TW, 768, 1, 2, 4, 3>(a, s);
       } else {
         launch_gemv<TW, 768, 1, 2, 0, 3>(a, s);
       }
       break;
   }
+  return true;
 }
 
 template <typename TW>
@@ -1215,15 +1494,18 @@ static GemvArgs make_args(const ArWeights& w, const ArState& st, int kvdtype, in
   return a;
 }
 
+// returns whether the greedy select was fused into lm_head
 template <typename TW>
-static void ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B, const float* emb_row, int slot,
-                      int pos, float* logits_dst, hipStream_t s) {
+static bool ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B, const float* emb_row, int slot,
+                      int pos, float* logits_dst, bool select, hipStream_t s) {
   GemvArgs a = make_args<TW>(w, st, kvdtype, B, emb_row);
   if (emb_row) hipLaunchKernelGGL(ar_row_state_kernel, dim3(1), dim3(1), 0, s, st, slot, pos);
   for (int l = 0; l < N_LAYER; ++l)
     for (int op = 0; op < 5; ++op) launch_op<TW>(op, a, w, l, kvdtype, B, s);
   a.dst = logits_dst;
-  launch_op<TW>(5, a, w, N_LAYER - 1, kvdtype, B, s);
+  const bool fused = select && fused_select<TW>(B);
+  launch_op<TW>(5, a, w, N_LAYER - 1, kvdtype, B, s, fused);
+  return fused;
 }
 
 // Launch one op of the decode step `iters` times (bench.py times it with HIP events); layer 1.
@@ -1231,10 +1513,13 @@ template <typename TW>
 static int ar_probe_impl(const ArWeights& w, const ArState& st, int kvdtype, int B, int which, int iters,
                          hipStream_t s) {
   if (which < 0 || which > 5) return -1;
+  if (which == 4 && fused_mlp<TW>(B)) return 1;  // no kernel of its own at this B
   GemvArgs a = make_args<TW>(w, st, kvdtype, B, nullptr);
   a.dst = st.logits;
   hipLaunchKernelGGL(ar_rowinfo_init_kernel, dim3((B + 63) / 64), dim3(64), 0, s, st, B);
-  for (int i = 0; i < iters; ++i) launch_op<TW>(which, a, w, which == 5 ? N_LAYER - 1 : 1, kvdtype, B, s);
+  for (int i = 0; i < iters; ++i)
+    if (!launch_op<TW>(which, a, w, which == 5 ? N_LAYER - 1 : 1, kvdtype, B, s, which == 5 && fused_select<TW>(B)))
+      return 1;  // no kernel of its own at this B
   return 0;
 }
 
@@ -1248,9 +1533,9 @@ void ar_launch_step(const ArWeights& w, const ArState& st, int wdtype, int kvdty
                     const float* emb_row, int slot, int pos, float* logits_out, hipStream_t s) {
   float* dst = mode == 0 ? st.logits : logits_out;
   const float* er = mode == 0 ? nullptr : emb_row;
-  if (wdtype == LVX_DTYPE_BF16) ar_layers<bf16_t>(w, st, kvdtype, B, er, slot, pos, dst, s);
-  else ar_layers<float>(w, st, kvdtype, B, er, slot, pos, dst, s);
-  if (mode == 0) hipLaunchKernelGGL(ar_argmax_kernel, dim3(B), dim3(256), 0, s, st);
+  const bool fused = wdtype == LVX_DTYPE_BF16 ? ar_layers<bf16_t>(w, st, kvdtype, B, er, slot, pos, dst, mode == 0, s)
+                                             : ar_layers<float>(w, st, kvdtype, B, er, slot, pos, dst, mode == 0, s);
+  if (mode == 0 && !fused) hipLaunchKernelGGL(ar_argmax_kernel, dim3(B), dim3(256), 0, s, st);
 }
 
 // ---------------------------------------------------------------------------------

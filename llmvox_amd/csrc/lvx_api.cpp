@@ -179,6 +179,18 @@ static std::vector<float> repack_conv(const std::vector<float>& w, int N, int C,
   return o;
 }
 
+// mlp.c_proj [768][3072] -> [3072/16 blocks][256 threads][3][16]: block k's thread t holds
+// W[t + 256 jj][16 k + j] as 96 contiguous bytes (bf16), the operand order of ar_mlp_fused_kernel
+static std::vector<float> pack_mproj(const std::vector<float>& w) {
+  std::vector<float> o((size_t)D * DFF);
+  size_t q = 0;
+  for (int k = 0; k < DFF / 16; ++k)
+    for (int t = 0; t < 256; ++t)
+      for (int jj = 0; jj < 3; ++jj)
+        for (int j = 0; j < 16; ++j) o[q++] = w[(size_t)(t + 256 * jj) * DFF + 16 * k + j];
+  return o;
+}
+
 extern "C" {
 
 int lvx_version(void) { return 1; }
@@ -270,6 +282,8 @@ int lvx_finalize(lvx_ctx* c) {
     UP_W(c->H(p + "attn.c_proj.weight"), w.w_aproj[i]);
     UP_W(c->H(p + "mlp.c_fc.weight"), w.w_fc[i]);
     UP_W(c->H(p + "mlp.c_proj.weight"), w.w_mproj[i]);
+    if (c->cfg.weight_dtype == LVX_DTYPE_BF16)  // thread-packed copy for the fused MLP (ar_mlp_fused_kernel)
+      UP_W(pack_mproj(c->H(p + "mlp.c_proj.weight")), w.w_mproj_pk[i]);
   }
   UP_F("transformer.ln_f.weight", w.lnf);
   UP_W(c->H("lm_head.weight"), w.w_lm);
@@ -352,8 +366,12 @@ int lvx_finalize(lvx_ctx* c) {
       (r = c->dalloc(&st.part_o, (size_t)S * N_HEAD * NSPLIT * HD)) ||
       (r = c->dalloc(&st.part_ml, (size_t)S * N_HEAD * NSPLIT * 2)) || (r = c->dalloc(&st.h, (size_t)S * DFF)) ||
       (r = c->dalloc(&st.logits, (size_t)S * VOCAB)) || (r = c->dalloc(&st.rowinfo, S)) ||
-      (r = c->dalloc(&st.xn, (size_t)S * D)) || (r = c->dalloc(&st.hb, (size_t)S * DFF)))
+      (r = c->dalloc(&st.xn, (size_t)S * D)) || (r = c->dalloc(&st.hb, (size_t)S * DFF)) ||
+      (r = c->dalloc(&st.lmbest, (size_t)LM_MAX_BLOCKS * 4 * 2)) || (r = c->dalloc(&st.ticket, 4)) ||
+      (r = c->dalloc(&st.yacc, (size_t)YCOPIES * S * D)))
     return r;
+  HIP_TRY(hipMemset(st.yacc, 0, (size_t)YCOPIES * S * D * 4));
+  HIP_TRY(hipMemset(st.ticket, 0, 16));
   HIP_TRY(hipMemset(st.part_o, 0, (size_t)S * N_HEAD * NSPLIT * HD * 4));
   HIP_TRY(hipMemset(st.part_ml, 0, (size_t)S * N_HEAD * NSPLIT * 2 * 4));
   HIP_TRY(hipMemset(st.pos, 0, S * 4));
@@ -455,6 +473,8 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   else if (n == "cproj_b1") g_opt_cproj_b1 = value;
   else if (n == "prefetch_in") g_opt_prefetch_in = value;
   else if (n == "mfma_batch") g_opt_mfma_batch = value;
+  else if (n == "fuse_argmax") g_opt_fuse_argmax = value;
+  else if (n == "fuse_mlp") g_opt_fuse_mlp = value;
   else return fail(LVX_E_NAME, "unknown option " + n);
   for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);  // captured kernels change
   c->graphs.clear();
@@ -581,8 +601,9 @@ int lvx_probe_kernel(lvx_ctx* c, int which, int B, const int32_t* slots, int ite
   HIP_TRY(hipSetDevice(c->cfg.device));
   ArState st = c->st;  // no plan bound: text_plan / rowstep / tok_plan stay null
   st.slots = const_cast<int32_t*>(slots);
-  if (ar_probe(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, which, iters, (hipStream_t)stream))
-    return fail(LVX_E_ARG, "unknown probe kernel id");
+  const int pr = ar_probe(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, which, iters, (hipStream_t)stream);
+  if (pr < 0) return fail(LVX_E_ARG, "unknown probe kernel id");
+  if (pr > 0) return fail(LVX_E_STATE, "this op has no kernel of its own at this batch size (fused into the previous op)");
   HIP_TRY(hipGetLastError());
   return LVX_OK;
 }

@@ -11,8 +11,11 @@ namespace lvx {
 
 constexpr int N_LAYER = 4, N_HEAD = 8, D = 768, HD = 96, DFF = 3072, VOCAB = 4096;
 constexpr int TEXT_DIM = 256, SPEECH_DIM = 512, TEXT_VOCAB = 386, BLOCK_SIZE = 8192;
-constexpr int NSPLIT = 16;
-extern int g_opt_gemv_reg, g_opt_attn_v2, g_opt_cproj_b1, g_opt_prefetch_in, g_opt_mfma_batch;  // development A/B switches (lvx_set_option)  // max KV splits per (stream, head) in decode attention
+constexpr int NSPLIT = 16;  // max KV splits per (stream, head) in decode attention
+constexpr int YCOPIES = 4;          // accumulator copies of the fused MLP (spreads atomic contention)
+constexpr int LM_MAX_BLOCKS = 1024;  // lm_head blocks of the fused argmax tail (4096 rows / 8 per block = 512)
+extern int g_opt_gemv_reg, g_opt_attn_v2, g_opt_cproj_b1, g_opt_prefetch_in, g_opt_mfma_batch, g_opt_fuse_argmax,
+    g_opt_fuse_mlp;  // A/B switches (lvx_set_option)
 
 // Device-resident AR weights. Matrices are [out][in] row-major (torch Linear layout),
 // in the context's weight dtype; vectors and gathered tables are fp32.
@@ -27,6 +30,7 @@ struct ArWeights {
   const void* w_aproj[N_LAYER] = {};  // [768][768]
   const void* w_fc[N_LAYER] = {};     // [3072][768]
   const void* w_mproj[N_LAYER] = {};  // [768][3072]
+  const void* w_mproj_pk[N_LAYER] = {};  // bf16 only: thread-packed copy for the fused MLP (pack_mproj)
   const void* w_lm = nullptr;         // [4096][768]
 };
 
@@ -50,6 +54,9 @@ struct ArState {
   bf16_t* xn = nullptr;         // [B][768] bf16 operand rows (batched path)
   bf16_t* hb = nullptr;         // [B][3072] bf16 h (batched path)
   float* logits = nullptr;      // [B][4096]
+  uint64_t* lmbest = nullptr;   // [LM_MAX_BLOCKS][4][2] per-block top1/top2 granules (fused lm_head + argmax)
+  uint32_t* ticket = nullptr;   // [4] arrival counter of the fused lm_head (reset by its last block)
+  float* yacc = nullptr;        // [YCOPIES][max_streams][768] fused-MLP output accumulators (fp32 atomics)
   void* kc = nullptr;           // [4][max_streams][8][max_pos][96]
   void* vc = nullptr;
   int max_pos = 0, max_streams = 0;

@@ -1,5 +1,5 @@
 """In-process A/B of AR step variants (development tool): python tools/ab_ar.py opt v0 v1 ..."""
-import sys, time
+import os, sys, time
 import torch
 from llmvox_amd.engine import build_engine
 
@@ -7,7 +7,7 @@ opt = sys.argv[1]
 vals = [int(v) for v in sys.argv[2:]] or [0, 1]
 e = build_engine(0, "bf16", "bf16", max_streams=8, max_positions=2048, max_codec_frames=256)
 dev = e.device
-B, stride, n = 1, 512, 256
+B, stride, n = int(os.environ.get("AB_B", "1")), 512, 256
 plan = torch.full((B, stride), 100, dtype=torch.int32, device=dev)
 slots = torch.arange(B, dtype=torch.int32, device=dev)
 rowstep = torch.zeros(B, dtype=torch.int32, device=dev)

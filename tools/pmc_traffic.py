@@ -4,8 +4,8 @@ usage: python tools/pmc_traffic.py FETCH_CSV WRITE_CSV DTYPE [OUT_JSON]
 
 bench.py's roofline probe (``probe_kernels``) runs, for each op k = 0..5, one
 ``ar_rowinfo_init_kernel`` + 10 warm launches, then one ``ar_rowinfo_init_kernel`` + 200 timed
-launches.  The last 12 rowinfo-init dispatches therefore delimit the probe segments; the
-timed segment of op k is the (2k+1)-th.  Bytes per launch = counter sum over the segment / 200.
+launches; the rowinfo-init dispatches delimit the segments and the timed ones are the last
+segments of 200 launches.  Bytes per launch = counter sum over the segment / 200.
 
 Corrections (MI355X_MICROARCH.md, "HBM"): FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
 FETCH_SIZE counts half the bytes of a 16-B/lane coalesced read, so it is doubled; WRITE_SIZE
@@ -22,14 +22,21 @@ ITERS = 200
 
 
 def segments(path, counter):
+    """{op: (bytes per launch, kernel names, launches)} over the timed probe segments (those with
+    ITERS launches after an ar_rowinfo_init_kernel marker); an op with no kernel of its own at this
+    B (the mlp c_proj of the fused MLP) has no segment and is reported with 0 launches."""
     rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-    marks = [i for i, r in enumerate(rows) if "ar_rowinfo_init_kernel" in r["Kernel_Name"]][-12:]
-    out = {}
-    for k in range(6):
-        a = marks[2 * k + 1] + 1
-        b = marks[2 * k + 2] if 2 * k + 2 < len(marks) else len(rows)
-        seg = [r for r in rows[a:b] if not r["Kernel_Name"].startswith("__amd")]
+    marks = [i for i, r in enumerate(rows) if "ar_rowinfo_init_kernel" in r["Kernel_Name"]] + [len(rows)]
+    timed = []
+    for a, b in zip(marks[:-1], marks[1:]):
+        seg = [r for r in rows[a + 1:b] if not r["Kernel_Name"].startswith("__amd")]
+        if len(seg) >= ITERS:
+            timed.append(seg[:ITERS])
+    timed = timed[-6:]
+    ops = list(range(6)) if len(timed) == 6 else [0, 1, 2, 3, 5]
+    out = {k: (0.0, [], 0) for k in range(6)}
+    for k, seg in zip(ops, timed[-len(ops):]):
         out[k] = (sum(float(r["Counter_Value"]) for r in seg) * 1024.0 / ITERS,
                   sorted({r["Kernel_Name"] for r in seg}), len(seg))
     return out
@@ -41,10 +48,15 @@ def main():
                                                              "pmc_traffic.json")
     f, w = segments(fetch, "FETCH_SIZE"), segments(write, "WRITE_SIZE")
     res = json.load(open(dst)) if os.path.exists(dst) else {}
+    names = dict(KNAMES)
+    if f[4][2] == 0:  # mlp c_proj has no kernel of its own (fused MLP at this B)
+        names[3] = "ar_mlp fused (c_fc+gelu+c_proj)"
     for k in range(6):
+        if f[k][2] == 0:
+            continue
         byts = 2.0 * f[k][0] + w[k][0]
-        res[f"{dtype}:{KNAMES[k]}"] = round(byts)
-        print(f"{KNAMES[k]:28s} fetch {2 * f[k][0] / 1e6:8.3f} MB  write {w[k][0] / 1e6:8.3f} MB  "
+        res[f"{dtype}:{names[k]}"] = round(byts)
+        print(f"{names[k]:32s} fetch {2 * f[k][0] / 1e6:8.3f} MB  write {w[k][0] / 1e6:8.3f} MB  "
               f"launches/segment {f[k][2]}  kernels {f[k][1]}")
     json.dump(res, open(dst, "w"), indent=1, sort_keys=True)
 
