@@ -12,7 +12,7 @@ import os
 import torch  # noqa: F401  (loads the HIP runtime that the library then shares)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libllmvox_hip.so")
+LIB_PATH = os.environ.get("LVX_LIB_PATH") or os.path.join(_HERE, "libllmvox_hip.so")  # override: A/B builds
 
 LVX_OK = 0
 LVX_E_ARG = -1

@@ -781,34 +781,38 @@ __global__ __launch_bounds__(256) void ar_cproj_b1_kernel(GemvArgs a) {
 // c_fc -> c_proj kernel boundary (one of the per-layer seams); the summation order of y is not
 // fixed, so it is a bf16 performance-mode path only.
 // ---------------------------------------------------------------------------------
-template <int BG>
+template <int BG, int RB>
 __global__ __launch_bounds__(256) void ar_mlp_fused_kernel(GemvArgs a, const bf16_t* __restrict__ Wfc,
                                                            const bf16_t* __restrict__ Wpk) {
+  constexpr int RW = RB / 4;  // c_fc rows per wave
   __shared__ __attribute__((aligned(16))) float xs[BG][D];
-  __shared__ float hs[BG][16];
+  __shared__ float hs[BG][RB];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int n0 = blockIdx.x * 16;
+  const int n0 = blockIdx.x * RB;
   // issue order: x rows (LayerNorm input), c_fc rows, packed c_proj columns
   float4 xv[3];
   if (wave < BG) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) xv[j] = *reinterpret_cast<const float4*>(a.st.x + (size_t)wave * D + j * 256 + lane * 4);
   }
-  uint2 wf[4][3];
+  uint2 wf[RW][3];
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+  for (int r = 0; r < RW; ++r)
 #pragma unroll
     for (int i = 0; i < 3; ++i)
-      wf[r][i] = *reinterpret_cast<const uint2*>(Wfc + (size_t)(n0 + wave * 4 + r) * D + i * 256 + lane * 4);
-  uint4 wp[6];
-  const uint4* pk = reinterpret_cast<const uint4*>(Wpk + ((size_t)blockIdx.x * 256 + tid) * 48);
+      wf[r][i] = *reinterpret_cast<const uint2*>(Wfc + (size_t)(n0 + wave * RW + r) * D + i * 256 + lane * 4);
+  uint4 wp[RB / 16][6];  // pack of 16 columns g: 96 contiguous bytes per thread
 #pragma unroll
-  for (int i = 0; i < 6; ++i) wp[i] = pk[i];
+  for (int g = 0; g < RB / 16; ++g) {
+    const uint4* pk = reinterpret_cast<const uint4*>(Wpk + (((size_t)blockIdx.x * (RB / 16) + g) * 256 + tid) * 48);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) wp[g][i] = pk[i];
+  }
   if (wave < BG) wave_ln_to_lds(xv, a.ln_w, xs[wave], lane);
   __syncthreads();
-  float acc[4][BG];
+  float acc[RW][BG];
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+  for (int r = 0; r < RW; ++r)
 #pragma unroll
     for (int bb = 0; bb < BG; ++bb) acc[r][bb] = 0.f;
 #pragma unroll
@@ -817,37 +821,37 @@ __global__ __launch_bounds__(256) void ar_mlp_fused_kernel(GemvArgs a, const bf1
     for (int bb = 0; bb < BG; ++bb) {
       const float4 x4 = *reinterpret_cast<const float4*>(&xs[bb][i * 256 + lane * 4]);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < RW; ++r) {
         const float4 w = WReg<bf16_t>::f(wf[r][i]);
         acc[r][bb] += (w.x * x4.x + w.y * x4.y) + (w.z * x4.z + w.w * x4.w);
       }
     }
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+  for (int r = 0; r < RW; ++r)
 #pragma unroll
     for (int bb = 0; bb < BG; ++bb) {
       const float v = wave_sum(acc[r][bb]);
-      if (lane == 0) hs[bb][wave * 4 + r] = gelu_tanh(v);
+      if (lane == 0) hs[bb][wave * RW + r] = gelu_tanh(v);
     }
   __syncthreads();
-  // thread tid: outputs e = tid + 256 jj; packed weights jj * 16 + j = W[e][n0 + j]
+  // thread tid: outputs e = tid + 256 jj; pack g element jj * 16 + j = W[e][n0 + 16 g + j]
   float* y = a.yacc + (size_t)(blockIdx.x % YCOPIES) * a.st.max_streams * D;
 #pragma unroll
   for (int bb = 0; bb < BG; ++bb) {
-    float h[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) h[j] = hs[bb][j];
 #pragma unroll
     for (int jj = 0; jj < 3; ++jj) {
       float t = 0.f;
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const uint4 u = wp[jj * 2 + q];
-        const uint32_t wv[4] = {u.x, u.y, u.z, u.w};
+      for (int g = 0; g < RB / 16; ++g)
 #pragma unroll
-        for (int m = 0; m < 4; ++m)
-          t += __uint_as_float(wv[m] << 16) * h[q * 8 + 2 * m] + __uint_as_float(wv[m] & 0xffff0000u) * h[q * 8 + 2 * m + 1];
-      }
+        for (int q = 0; q < 2; ++q) {
+          const uint4 u = wp[g][jj * 2 + q];
+          const uint32_t wv[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+            t += __uint_as_float(wv[m] << 16) * hs[bb][16 * g + q * 8 + 2 * m] +
+                 __uint_as_float(wv[m] & 0xffff0000u) * hs[bb][16 * g + q * 8 + 2 * m + 1];
+        }
       atomicAdd(y + (size_t)bb * D + tid + 256 * jj, t);
     }
   }
@@ -1447,8 +1451,13 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       if (fm) {
         const bf16_t* wfc = reinterpret_cast<const bf16_t*>(w.w_fc[l]);
         const bf16_t* wpk = reinterpret_cast<const bf16_t*>(w.w_mproj_pk[l]);
-        if (B <= 1) hipLaunchKernelGGL((ar_mlp_fused_kernel<1>), dim3(DFF / 16), dim3(256), 0, s, a, wfc, wpk);
-        else hipLaunchKernelGGL((ar_mlp_fused_kernel<2>), dim3(DFF / 16), dim3(256), 0, s, a, wfc, wpk);
+        if (g_opt_fuse_mlp == 2) {  // 32 h rows per block (96 blocks)
+          if (B <= 1) hipLaunchKernelGGL((ar_mlp_fused_kernel<1, 32>), dim3(DFF / 32), dim3(256), 0, s, a, wfc, wpk);
+          else hipLaunchKernelGGL((ar_mlp_fused_kernel<2, 32>), dim3(DFF / 32), dim3(256), 0, s, a, wfc, wpk);
+        } else {  // 16 h rows per block (192 blocks)
+          if (B <= 1) hipLaunchKernelGGL((ar_mlp_fused_kernel<1, 16>), dim3(DFF / 16), dim3(256), 0, s, a, wfc, wpk);
+          else hipLaunchKernelGGL((ar_mlp_fused_kernel<2, 16>), dim3(DFF / 16), dim3(256), 0, s, a, wfc, wpk);
+        }
       } else if (mf) {
         hipLaunchKernelGGL((ar_rows_kernel<0>), dim3((B + 3) / 4), dim3(256), 0, s, a);
         launch_mfma2<768, 5>(a, s);

@@ -12,7 +12,10 @@ namespace lvx {
 constexpr int N_LAYER = 4, N_HEAD = 8, D = 768, HD = 96, DFF = 3072, VOCAB = 4096;
 constexpr int TEXT_DIM = 256, SPEECH_DIM = 512, TEXT_VOCAB = 386, BLOCK_SIZE = 8192;
 constexpr int NSPLIT = 16;  // max KV splits per (stream, head) in decode attention
-constexpr int YCOPIES = 4;          // accumulator copies of the fused MLP (spreads atomic contention)
+#ifndef LVX_YCOPIES
+#define LVX_YCOPIES 4
+#endif
+constexpr int YCOPIES = LVX_YCOPIES;  // accumulator copies of the fused MLP (spreads atomic contention)
 constexpr int LM_MAX_BLOCKS = 1024;  // lm_head blocks of the fused argmax tail (4096 rows / 8 per block = 512)
 extern int g_opt_gemv_reg, g_opt_attn_v2, g_opt_cproj_b1, g_opt_prefetch_in, g_opt_mfma_batch, g_opt_fuse_argmax,
     g_opt_fuse_mlp;  // A/B switches (lvx_set_option)

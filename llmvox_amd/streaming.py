@@ -374,9 +374,15 @@ class FusedScheduler:
     every stream's SegmentMachine consumes them in order; a stream that hits end-of-audio
     drops its run-ahead tokens and its slot is rewound to position 0; all dumps of the chunk
     are decoded (batched by length) and delivered in order.
+
+    With ``overlap`` (default on a GPU engine) the codec of chunk c runs on a second HIP stream
+    while the AR decode of chunk c+1 runs on the main one: chunk c's items are
+    delivered by the next ``run_chunk`` right after it has launched chunk c+1, or by ``flush``
+    (called by ``run_until_idle`` and by an idle ``run_chunk``).
     """
 
-    def __init__(self, engine, max_chunk: int = 64, max_rows: Optional[int] = None, to_bytes: bool = True):
+    def __init__(self, engine, max_chunk: int = 64, max_rows: Optional[int] = None, to_bytes: bool = True,
+                 overlap: Optional[bool] = None):
         import torch
         self.engine = engine
         self.torch = torch
@@ -394,6 +400,10 @@ class FusedScheduler:
         pin = torch.device(dev).type == "cuda"
         self.plan_h = torch.zeros((R, n), dtype=torch.int32, pin_memory=pin)
         self.slots_h = torch.full((R,), -1, dtype=torch.int32, pin_memory=pin)
+        self.overlap = pin if overlap is None else (overlap and pin)
+        self.codec_stream = torch.cuda.Stream(device=dev) if self.overlap else None
+        self.pcm_h = None      # pinned staging buffer of the decode in flight (grown on demand)
+        self.pending = None    # (event, [(dump index, offset, samples)], order, ready) of the last chunk
 
     def open_stream(self, index=0, dump_size=C.INITIAL_DUMP_SIZE_1, sink=None, **kw) -> FusedStream:
         if not self.free_slots:
@@ -423,6 +433,7 @@ class FusedScheduler:
             ready.append(st)
         ready = ready[: self.max_rows]
         if not ready:
+            self.flush()
             return 0
         n = min(self.max_chunk, min(self._steps_to_dump(st.m) for st in ready))
         plans = {}
@@ -439,6 +450,7 @@ class FusedScheduler:
         self.plan_d.copy_(self.plan_h, non_blocking=True)
         self.rowstep_d.zero_()
         self.engine.ar_steps(n, self.slots_d[:B], self.plan_d[:B], self.rowstep_d[:B], self.tok_d[:B])
+        self.flush()  # the previous chunk's audio, decoded while this chunk's AR steps run
         toks = self.tok_d[:B, :n].cpu().numpy()
         dumps = []  # (stream, tokens)
         order: Dict[FusedStream, List[tuple]] = {st: [] for st in ready}
@@ -458,28 +470,69 @@ class FusedScheduler:
                     # run-ahead past end-of-audio: drop the rest, restart the slot at position 0
                     self.engine.set_slot(st.slot, 0, 0)
                     break
-        pcm = self._decode(dumps)
+        self.engine.check_errors()
+        if self.overlap:
+            self._launch_decode(dumps, order, ready)
+        else:
+            self._deliver(self._decode(dumps), order, ready)
+        return n
+
+    def _deliver(self, pcm, order, ready):
         for st in ready:
             for kind, v in order[st]:
                 st._out(pcm[v] if kind == "audio" else v)
-        self.engine.check_errors()
-        return n
 
-    def _decode(self, dumps):
-        torch = self.torch
-        res: List[object] = [None] * len(dumps)
+    def _groups(self, dumps):
+        """Dump indices batched by length (one codec call per group, within max_codec_frames)."""
         by_len: Dict[int, List[int]] = {}
         for i, (_, toks) in enumerate(dumps):
             by_len.setdefault(len(toks), []).append(i)
         for L, idx in by_len.items():
             cap = max(1, self.engine.max_codec_frames // L)
             for s in range(0, len(idx), cap):
-                grp = idx[s:s + cap]
-                codes = torch.tensor([dumps[i][1] for i in grp], dtype=torch.int32, device=self.engine.device)
-                out = self.engine.decode_codes(codes).cpu().numpy()
-                for k, i in enumerate(grp):
-                    res[i] = out[k].astype("float32").tobytes() if self.to_bytes else out[k]
+                yield L, idx[s:s + cap]
+
+    def _decode(self, dumps):
+        torch = self.torch
+        res: List[object] = [None] * len(dumps)
+        for L, grp in self._groups(dumps):
+            codes = torch.tensor([dumps[i][1] for i in grp], dtype=torch.int32, device=self.engine.device)
+            out = self.engine.decode_codes(codes).cpu().numpy()
+            for k, i in enumerate(grp):
+                res[i] = out[k].astype("float32").tobytes() if self.to_bytes else out[k]
         return res
+
+    def _launch_decode(self, dumps, order, ready):
+        """Queue the chunk's decodes on the codec stream, PCM into pinned host memory; no wait."""
+        torch = self.torch
+        total = 320 * sum(len(t) for _, t in dumps)
+        if self.pcm_h is None or self.pcm_h.numel() < total:
+            self.pcm_h = torch.empty(max(total, 1 << 16) * 2, dtype=torch.float32, pin_memory=True)
+        spans, off = [], 0
+        with torch.cuda.stream(self.codec_stream):
+            for L, grp in self._groups(dumps):
+                codes = torch.tensor([dumps[i][1] for i in grp], dtype=torch.int32, device=self.engine.device)
+                out = self.engine.decode_codes(codes)
+                self.pcm_h[off:off + out.numel()].view(out.shape).copy_(out, non_blocking=True)
+                for k, i in enumerate(grp):
+                    spans.append((i, off + k * 320 * L, 320 * L))
+                off += out.numel()
+            ev = torch.cuda.Event()
+            ev.record(self.codec_stream)
+        self.pending = (ev, spans, order, ready, len(dumps))
+
+    def flush(self):
+        """Deliver the items of the chunk whose decode is in flight (overlap mode)."""
+        if self.pending is None:
+            return
+        ev, spans, order, ready, nd = self.pending
+        self.pending = None
+        ev.synchronize()
+        pcm: List[object] = [None] * nd
+        for i, off, ln in spans:
+            a = self.pcm_h[off:off + ln].numpy()
+            pcm[i] = a.tobytes() if self.to_bytes else a.copy()
+        self._deliver(pcm, order, ready)
 
     def run_until_idle(self, max_chunks: int = 1 << 30) -> int:
         total = 0
@@ -488,4 +541,5 @@ class FusedScheduler:
             if n == 0:
                 break
             total += n
+        self.flush()
         return total

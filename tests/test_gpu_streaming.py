@@ -67,6 +67,7 @@ def test_fused_scheduler_reproduces_reference_stream(handler):
         st.feed(w)
     while len([e for e in st.events if isinstance(e, bytes)]) < 3:
         assert sch.run_chunk() > 0
+    sch.flush()
     assert st.tokens[:130] == a["ids"][:130].tolist()
     chunks = [np.frombuffer(e, dtype=np.float32) for e in st.events if isinstance(e, bytes)]
     for i in range(3):
@@ -89,6 +90,7 @@ def test_fused_rollback_matches_dropin_on_forced_eoa(handler):
     while sum(1 for e in st.tokens) < 120:
         if sch.run_chunk() == 0:
             break
+    sch.flush()
     got = st.events[:len(ref)]
     assert [type(x) for x in got] == [type(x) for x in ref]
     for x, y in zip(got, ref):
@@ -124,3 +126,29 @@ def test_fused_multistream_batch_equals_single(handler):
             one.run_chunk()
         assert st.tokens[:len(batched[i])] == batched[i]
         one.close_stream(st)
+
+
+def test_fused_overlap_delivers_same_items(handler):
+    """Codec on a second HIP stream (deferred delivery) == synchronous decode, item for item."""
+    texts = [WORDS, "hello there world.".split(" ")]
+    res = []
+    for overlap in (False, True):
+        sch = S.FusedScheduler(handler.engine, max_chunk=40, overlap=overlap)
+        sts = []
+        for i, t in enumerate(texts):
+            st = sch.open_stream(index=i % 2, dump_size=10 if i % 2 == 0 else 160)
+            for w in t:
+                st.feed(w)
+            sts.append(st)
+        for _ in range(8):
+            sch.run_chunk()
+        sch.flush()
+        res.append([list(st.events) for st in sts])
+        for st in sts:
+            sch.close_stream(st)
+    assert sch.overlap
+    for a, b in zip(*res):
+        assert len(a) == len(b) and len(a) > 0
+        for x, y in zip(a, b):
+            assert type(x) is type(y)
+            assert x == y
