@@ -177,6 +177,8 @@ def main():
     ap.add_argument("--streams", type=int, default=1, help="streams per GPU (configs[2]: 32)")
     ap.add_argument("--chunk", type=int, default=256)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--kv-dtype", default=None, choices=["bf16", "fp32", "fp8"],
+                    help="KV cache dtype (default: --dtype); fp8 = OCP e4m3fn (configs[4])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
     ap.add_argument("--probe-pos", type=int, default=0,
@@ -198,7 +200,8 @@ def main():
     S, chunk, K, Wm = args.streams, args.chunk, args.steps, args.warmup
     if (K + 0) * chunk > 8192:
         raise SystemExit("steps * chunk must stay within block_size 8192 positions")
-    eng = build_engine(local, args.dtype, args.dtype, max_streams=max(S, 1), max_positions=8192,
+    kvd = args.kv_dtype or args.dtype
+    eng = build_engine(local, args.dtype, kvd, max_streams=max(S, 1), max_positions=8192,
                        max_codec_frames=S * chunk)
     dev = eng.device
     torch.cuda.set_device(dev)
@@ -317,7 +320,10 @@ def main():
         for s in range(S):
             eng.set_slot(s, ppos - 1, 0)
         wb = 2 if args.dtype == "bf16" else 4
-        kern = probe_kernels(eng, slots, ppos, wb, wb)
+        kb = {"bf16": 2, "fp8": 1, "fp32": 4}[kvd]
+        kern = probe_kernels(eng, slots, ppos, wb, kb)
+        # profiles/pmc_traffic.json key prefix (tools/pmc_traffic.py DTYPE argument)
+        pmc_prefix = args.dtype + (f"/kv{kvd}" if kvd != args.dtype else "") + (f"/B{S}" if S > 1 else "")
         dom = max(kern.values(), key=lambda r: r["share_us_per_step"])
         rl = {"bound": "hbm", "kernel": dom["name"], "achieved": round(dom["gbs"], 1), "peak": HBM_PEAK_GBS,
               "unit": "GB/s", "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4), "traffic": None,
@@ -326,11 +332,29 @@ def main():
         if os.path.exists(pmc):
             try:
                 tr = json.load(open(pmc))
-                key = f"{args.dtype}:{dom['name']}"
+                key = f"{pmc_prefix}:{dom['name']}"
                 if key in tr:
                     rl["traffic"] = tr[key]
             except Exception:
                 pass
+
+    # ---- codec: one batched decode of a chunk (S streams x chunk frames), HIP events on the
+    # stream it runs on; algorithmic FLOPs per SURVEY 8(d): 125,566,976 + 3,072 L per frame
+    torch.cuda.synchronize()
+    with torch.cuda.stream(codec_stream):
+        eng.decode_codes(tok_bufs[0], 0, out=pcm_bufs[0])
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c0.record(codec_stream)
+        for _ in range(5):
+            eng.decode_codes(tok_bufs[0], 0, out=pcm_bufs[0])
+        c1.record(codec_stream)
+    c1.synchronize()
+    codec_ms = c0.elapsed_time(c1) / 5
+    codec_flops = S * chunk * (125_566_976 + 3_072 * chunk)
+    codec_peak = 2500.0 if args.dtype == "bf16" else 157.3  # dense bf16 MFMA / exact-f32 MFMA, TFLOP/s
+    codec = {"frames": S * chunk, "avg_ms": round(codec_ms, 3),
+             "achieved": round(codec_flops / (codec_ms * 1e-3) / 1e12, 2), "peak": codec_peak, "unit": "TFLOP/s",
+             "frac": round(codec_flops / (codec_ms * 1e-3) / 1e12 / codec_peak, 4)}
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
@@ -358,6 +382,8 @@ def main():
             "realtime_factor_per_stream": round(value / (world * S) / 75.0, 1),
             "p50_first_chunk_latency_ms": round(p50, 3),
             "roofline": rl,
+            "codec_roofline": codec,
+            "kv_dtype": kvd,
             "cpu_baseline": cpu,
             "kernels": {v["name"]: {"avg_us": round(v["avg_us"], 2), "GB/s": round(v["gbs"], 1)}
                         for v in kern.values()} if kern else None,

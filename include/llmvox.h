@@ -38,13 +38,14 @@ extern "C" {
 
 #define LVX_DTYPE_F32 0
 #define LVX_DTYPE_BF16 1
+#define LVX_DTYPE_FP8 2 /* kv_dtype only: OCP e4m3fn (the gfx950 format), saturating at +-448, unscaled */
 
 typedef struct lvx_ctx lvx_ctx;
 
 typedef struct {
   int device;           /* HIP device ordinal */
   int weight_dtype;     /* LVX_DTYPE_F32 (parity mode; the reference runs fp32) or LVX_DTYPE_BF16 */
-  int kv_dtype;         /* LVX_DTYPE_F32 or LVX_DTYPE_BF16 */
+  int kv_dtype;         /* LVX_DTYPE_F32, LVX_DTYPE_BF16 or LVX_DTYPE_FP8 */
   int max_streams;      /* KV slots (concurrent utterance streams) */
   int max_positions;    /* per-slot KV capacity, <= 8192 (GPTConfig.block_size) */
   int max_codec_frames; /* max sum over streams of frames per codec call */

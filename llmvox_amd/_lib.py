@@ -22,9 +22,11 @@ LVX_E_CAPACITY = -4
 LVX_E_NAME = -5
 LVX_DTYPE_F32 = 0
 LVX_DTYPE_BF16 = 1
+LVX_DTYPE_FP8 = 2  # kv_dtype only (OCP e4m3fn)
 
 DTYPES = {"fp32": LVX_DTYPE_F32, "f32": LVX_DTYPE_F32, "float32": LVX_DTYPE_F32,
-          "bf16": LVX_DTYPE_BF16, "bfloat16": LVX_DTYPE_BF16}
+          "bf16": LVX_DTYPE_BF16, "bfloat16": LVX_DTYPE_BF16,
+          "fp8": LVX_DTYPE_FP8, "e4m3": LVX_DTYPE_FP8}
 
 
 class LvxConfig(ctypes.Structure):

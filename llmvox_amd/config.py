@@ -64,7 +64,7 @@ class InferenceConfig:
     Extra keys that the reference does not have:
       weights        "synthetic" (seeded, reference init scales) or "checkpoint".
       weight_dtype   "fp32" (parity mode, the reference runs fp32) or "bf16".
-      kv_dtype       "fp32" | "bf16".
+      kv_dtype       "fp32" | "bf16" | "fp8" (OCP e4m3fn KV cache).
       max_streams    KV slots per device.
       max_positions  KV capacity per slot (<= block_size 8192).
       seed           seed of the synthetic weights.

@@ -45,7 +45,7 @@ struct GemvArgs {
   int layer;
   const float* ln_w;
   float* dst;
-  int kv_bf16;
+  int kv_dtype;          // LVX_DTYPE_F32 / BF16 / FP8
   // IN 3 inputs
   const float* text_table;
   const float* codebook;
@@ -92,6 +92,14 @@ __device__ __forceinline__ void argmax_commit(const ArState& st, int b, int4 ri,
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
+
+// one K (which 0) or V (which 1) element of the KV cache in its dtype
+__device__ __forceinline__ void store_kv(const GemvArgs& a, int which, size_t idx, float v) {
+  void* base = which ? a.st.vc : a.st.kc;
+  if (a.kv_dtype == LVX_DTYPE_BF16) reinterpret_cast<bf16_t*>(base)[idx] = f32_to_bf16(v);
+  else if (a.kv_dtype == LVX_DTYPE_FP8) reinterpret_cast<fp8_t*>(base)[idx] = f32_to_fp8(v);
+  else reinterpret_cast<float*>(base)[idx] = v;
+}
 
 template <typename TW> struct WReg;
 template <> struct WReg<float> {
@@ -353,7 +361,7 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
 #pragma unroll
           for (int r = 0; r < RPW; ++r) {
             const float4 w = WReg<TW>::f(wr[r][it]);
-            acc[r][bb] += (w.x * xv.x + w.y * xv.y) + (w.z * xv.z + w.w * xv.w);
+            acc[r][bb] = dot4_fma(acc[r][bb], w, xv);
           }
         }
       }
@@ -404,8 +412,7 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
             if (s < 0) continue;
             const size_t idx =
                 ((((size_t)a.layer * a.st.max_streams + s) * N_HEAD + head) * a.st.max_pos + p) * HD + d;
-            if (a.kv_bf16) reinterpret_cast<bf16_t*>(which ? a.st.vc : a.st.kc)[idx] = f32_to_bf16(v);
-            else reinterpret_cast<float*>(which ? a.st.vc : a.st.kc)[idx] = v;
+            store_kv(a, which, idx, v);
           }
         } else if (OUT == 1) {
           float* xp = a.st.x + (size_t)b * D + n;
@@ -504,8 +511,7 @@ __device__ __forceinline__ void gemv_store(const GemvArgs& a, int n, int b, floa
       const int4 ri = a.st.rowinfo[b];
       if (ri.x < 0) return;
       const size_t idx = ((((size_t)a.layer * a.st.max_streams + ri.x) * N_HEAD + head) * a.st.max_pos + ri.y) * HD + d;
-      if (a.kv_bf16) reinterpret_cast<bf16_t*>(which ? a.st.vc : a.st.kc)[idx] = f32_to_bf16(v);
-      else reinterpret_cast<float*>(which ? a.st.vc : a.st.kc)[idx] = v;
+      store_kv(a, which, idx, v);
     }
   } else if (OUT == 1) {
     a.st.x[(size_t)b * D + n] += v;
@@ -642,7 +648,7 @@ __global__ __launch_bounds__(256) void ar_gemv_reg_kernel(GemvArgs a) {
       for (int b = 0; b < BB; ++b) {
         if (b >= B) continue;
         const float4 xv = xin[b][i];
-        acc[r][b] += (w.x * xv.x + w.y * xv.y) + (w.z * xv.z + w.w * xv.w);
+        acc[r][b] = dot4_fma(acc[r][b], w, xv);
       }
     }
   // 5. reduce (+ combine the K-split waves through LDS)
@@ -751,7 +757,7 @@ __global__ __launch_bounds__(256) void ar_cproj_b1_kernel(GemvArgs a) {
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
       const float4 w = WReg<TW>::f(wr[r][i]);
-      acc[r] += (w.x * xv.x + w.y * xv.y) + (w.z * xv.z + w.w * xv.w);
+      acc[r] = dot4_fma(acc[r], w, xv);
     }
   }
 #pragma unroll
@@ -777,9 +783,12 @@ __global__ __launch_bounds__(256) void ar_cproj_b1_kernel(GemvArgs a) {
 //   y += mlp.c_proj[:, 16k:16k+16] h               (its 16 columns of c_proj, thread-packed, 24.6 KB)
 // The 768-wide partial is added with no-return fp32 atomics (256 contiguous bytes per wave
 // instruction) into accumulator copy k % YCOPIES; the next c_attn / lm_head prologue reads
-// x + sum of copies, and the next c_proj folds them into x and clears them. This removes the
-// c_fc -> c_proj kernel boundary (one of the per-layer seams); the summation order of y is not
-// fixed, so it is a bf16 performance-mode path only.
+// x + the copies, the next c_proj folds them into x and clears them. This removes the
+// c_fc -> c_proj kernel boundary (one of the per-layer seams, -6.7 us per step at B = 1).
+// The order in which the 48 blocks of a copy add is not fixed, so results vary run to run at
+// the 1e-7 level: option fuse_mlp = 0 selects the deterministic two-kernel path. (A 2^-32
+// fixed-point variant with 64-bit integer atomics is deterministic but gave back almost all of
+// the gain: measured 94.9 vs 95.6 us per step.)
 // ---------------------------------------------------------------------------------
 template <int BG, int RB>
 __global__ __launch_bounds__(256) void ar_mlp_fused_kernel(GemvArgs a, const bf16_t* __restrict__ Wfc,
@@ -823,7 +832,7 @@ __global__ __launch_bounds__(256) void ar_mlp_fused_kernel(GemvArgs a, const bf1
 #pragma unroll
       for (int r = 0; r < RW; ++r) {
         const float4 w = WReg<bf16_t>::f(wf[r][i]);
-        acc[r][bb] += (w.x * x4.x + w.y * x4.y) + (w.z * x4.z + w.w * x4.w);
+        acc[r][bb] = dot4_fma(acc[r][bb], w, x4);
       }
     }
 #pragma unroll
@@ -849,8 +858,8 @@ __global__ __launch_bounds__(256) void ar_mlp_fused_kernel(GemvArgs a, const bf1
           const uint32_t wv[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
           for (int m = 0; m < 4; ++m)
-            t += __uint_as_float(wv[m] << 16) * hs[bb][16 * g + q * 8 + 2 * m] +
-                 __uint_as_float(wv[m] & 0xffff0000u) * hs[bb][16 * g + q * 8 + 2 * m + 1];
+            t = fmaf(__uint_as_float(wv[m] & 0xffff0000u), hs[bb][16 * g + q * 8 + 2 * m + 1],
+                     fmaf(__uint_as_float(wv[m] << 16), hs[bb][16 * g + q * 8 + 2 * m], t));
         }
       atomicAdd(y + (size_t)bb * D + tid + 256 * jj, t);
     }
@@ -932,6 +941,16 @@ template <> struct KvPiece<bf16_t> {
     v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
     v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xffff0000u);
     v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xffff0000u);
+  }
+};
+template <> struct KvPiece<fp8_t> {
+  uint2 u;
+  __device__ __forceinline__ void load(const fp8_t* p) { u = *reinterpret_cast<const uint2*>(p); }
+  __device__ __forceinline__ void get(float* v) const {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 a = __builtin_amdgcn_cvt_pk_f32_fp8(u.x, false), b = __builtin_amdgcn_cvt_pk_f32_fp8(u.x, true);
+    const f2 c = __builtin_amdgcn_cvt_pk_f32_fp8(u.y, false), d = __builtin_amdgcn_cvt_pk_f32_fp8(u.y, true);
+    v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y; v[4] = c.x; v[5] = c.y; v[6] = d.x; v[7] = d.y;
   }
 };
 
@@ -1386,9 +1405,10 @@ static int attn_ns_max(int B) {  // enough splits to fill the chip, no more (ear
 }
 
 static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_t s, int ns_max = NSPLIT) {
-  if (g_opt_attn_v2) {
+  if (g_opt_attn_v2 || kvdtype == LVX_DTYPE_FP8) {
     dim3 grid(ns_max, N_HEAD, B);
     if (kvdtype == LVX_DTYPE_BF16) hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t>), grid, dim3(256), 0, s, st, l, ns_max);
+    else if (kvdtype == LVX_DTYPE_FP8) hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t>), grid, dim3(256), 0, s, st, l, ns_max);
     else hipLaunchKernelGGL((ar_attn_v2_kernel<float>), grid, dim3(256), 0, s, st, l, ns_max);
   } else {
     dim3 grid(NSPLIT, N_HEAD, B);
@@ -1494,7 +1514,7 @@ static GemvArgs make_args(const ArWeights& w, const ArState& st, int kvdtype, in
   GemvArgs a{};
   a.st = st;
   a.B = B;
-  a.kv_bf16 = kvdtype == LVX_DTYPE_BF16;
+  a.kv_dtype = kvdtype;
   a.text_table = w.text_table;
   a.codebook = w.codebook;
   a.wpe = w.wpe;

@@ -201,8 +201,8 @@ int lvx_create(const lvx_config* cfg, lvx_ctx** out) {
   if (!cfg || !out) return fail(LVX_E_ARG, "null argument");
   if (cfg->weight_dtype != LVX_DTYPE_F32 && cfg->weight_dtype != LVX_DTYPE_BF16)
     return fail(LVX_E_ARG, "weight_dtype must be LVX_DTYPE_F32 or LVX_DTYPE_BF16");
-  if (cfg->kv_dtype != LVX_DTYPE_F32 && cfg->kv_dtype != LVX_DTYPE_BF16)
-    return fail(LVX_E_ARG, "kv_dtype must be LVX_DTYPE_F32 or LVX_DTYPE_BF16");
+  if (cfg->kv_dtype != LVX_DTYPE_F32 && cfg->kv_dtype != LVX_DTYPE_BF16 && cfg->kv_dtype != LVX_DTYPE_FP8)
+    return fail(LVX_E_ARG, "kv_dtype must be LVX_DTYPE_F32, LVX_DTYPE_BF16 or LVX_DTYPE_FP8");
   if (cfg->max_streams < 1 || cfg->max_streams > 1024) return fail(LVX_E_ARG, "max_streams out of range [1,1024]");
   if (cfg->max_positions < 1 || cfg->max_positions > BLOCK_SIZE)
     return fail(LVX_E_ARG, "max_positions out of range [1,8192] (GPTConfig.block_size)");
@@ -378,7 +378,7 @@ int lvx_finalize(lvx_ctx* c) {
   HIP_TRY(hipMemset(st.prev, 0, S * 4));
   HIP_TRY(hipMemset(st.err, 0, 16));
   const size_t kvn = (size_t)N_LAYER * S * N_HEAD * P * HD;
-  const size_t kvb = c->cfg.kv_dtype == LVX_DTYPE_BF16 ? 2 : 4;
+  const size_t kvb = c->cfg.kv_dtype == LVX_DTYPE_BF16 ? 2 : c->cfg.kv_dtype == LVX_DTYPE_FP8 ? 1 : 4;
   {
     char* k;
     char* v;

@@ -6,6 +6,7 @@
 #define LVX_WAVE 64
 
 typedef uint16_t bf16_t;  // raw bf16 bits
+typedef uint8_t fp8_t;    // raw OCP e4m3fn bits (KV cache)
 
 // ---- dtype plumbing -------------------------------------------------------
 __device__ __forceinline__ float bf16_to_f32(bf16_t h) {
@@ -21,6 +22,18 @@ __host__ __device__ __forceinline__ bf16_t f32_to_bf16(float f) {
   if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (bf16_t)((u >> 16) | 0x40);
   u += 0x7fffu + ((u >> 16) & 1u);
   return (bf16_t)(u >> 16);
+}
+
+// f32 -> e4m3fn, round to nearest even, saturated to the finite range (+-448)
+__device__ __forceinline__ fp8_t f32_to_fp8(float f) {
+  f = fminf(fmaxf(f, -448.f), 448.f);
+  return (fp8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(f, f, 0, false) & 0xff);
+}
+
+// a + w.x x.x + w.y x.y + w.z x.z + w.w x.w as an explicit fma chain: the rounding does not
+// depend on how the compiler contracts each unrolled copy, so equal batch rows stay bit-equal
+__device__ __forceinline__ float dot4_fma(float a, float4 w, float4 x) {
+  return fmaf(w.w, x.w, fmaf(w.z, x.z, fmaf(w.y, x.y, fmaf(w.x, x.x, a))));
 }
 
 template <typename T> struct Ld;
