@@ -183,6 +183,8 @@ def main():
     ap.add_argument("--no-probe", action="store_true")
     ap.add_argument("--probe-pos", type=int, default=0,
                     help="KV position of the roofline probe (default: steps * chunk, where the run ends)")
+    ap.add_argument("--codec-overlap", action="store_true",
+                    help="run the codec on a second HIP stream beside the next chunk's AR (measured slower)")
     ap.add_argument("--no-graphs", action="store_true",
                     help="launch the decode step kernel by kernel (for rocprofv3 --pmc passes)")
     args = ap.parse_args()
@@ -226,9 +228,12 @@ def main():
     pcm = torch.empty(S, 320 * chunk, dtype=torch.float32, device=dev)
     pcm_host = torch.empty(S, 320 * chunk, dtype=torch.float32, pin_memory=True)
 
-    # the codec of chunk c runs on a second HIP stream, overlapped with the AR decode of chunk
-    # c+1 (the AR chain is latency-bound and leaves most CUs idle); tok_plan is double-buffered
-    codec_stream = torch.cuda.Stream(device=dev)
+    # the codec of chunk c runs after the AR of chunk c on the same stream. A second stream
+    # (--codec-overlap) was measured slower: the latency-bound AR chain stalls while the codec's
+    # kernels are in flight (22.4 ms AR + 1.2 ms codec = 23.6 ms serial vs 25.5 ms overlapped per
+    # 256-token chunk; CU-partitioned or prioritised streams 28 ms, tools/loop_probe.py).
+    # tok_plan / pcm are double-buffered so the overlapped variant stays correct.
+    codec_stream = torch.cuda.Stream(device=dev) if args.codec_overlap else torch.cuda.current_stream(dev)
     tok_bufs = [tok_plan, torch.zeros_like(tok_plan)]
     pcm_bufs = [pcm, torch.empty_like(pcm)]
     ev_ar = [torch.cuda.Event(), torch.cuda.Event()]

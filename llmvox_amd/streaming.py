@@ -375,14 +375,17 @@ class FusedScheduler:
     drops its run-ahead tokens and its slot is rewound to position 0; all dumps of the chunk
     are decoded (batched by length) and delivered in order.
 
-    With ``overlap`` (default on a GPU engine) the codec of chunk c runs on a second HIP stream
-    while the AR decode of chunk c+1 runs on the main one: chunk c's items are
-    delivered by the next ``run_chunk`` right after it has launched chunk c+1, or by ``flush``
-    (called by ``run_until_idle`` and by an idle ``run_chunk``).
+    With ``overlap=True`` the codec of chunk c runs on a second HIP stream while the AR decode of
+    chunk c+1 runs on the main one: chunk c's items are delivered by the next
+    ``run_chunk`` right after it has launched chunk c+1, or by ``flush`` (called by
+    ``run_until_idle`` and by an idle ``run_chunk``). Off by default: measured on MI355X, the
+    latency-bound AR chain stalls while codec kernels from another queue are in flight, so the
+    overlapped loop is slower than running the codec after the AR on one stream (25.5 vs
+    23.6 ms per 256-token chunk at 1 stream, 65.2 vs 64.4 ms at 32; tools/loop_probe.py).
     """
 
     def __init__(self, engine, max_chunk: int = 64, max_rows: Optional[int] = None, to_bytes: bool = True,
-                 overlap: Optional[bool] = None):
+                 overlap: bool = False):
         import torch
         self.engine = engine
         self.torch = torch
@@ -400,7 +403,7 @@ class FusedScheduler:
         pin = torch.device(dev).type == "cuda"
         self.plan_h = torch.zeros((R, n), dtype=torch.int32, pin_memory=pin)
         self.slots_h = torch.full((R,), -1, dtype=torch.int32, pin_memory=pin)
-        self.overlap = pin if overlap is None else (overlap and pin)
+        self.overlap = bool(overlap) and pin
         self.codec_stream = torch.cuda.Stream(device=dev) if self.overlap else None
         self.pcm_h = None      # pinned staging buffer of the decode in flight (grown on demand)
         self.pending = None    # (event, [(dump index, offset, samples)], order, ready) of the last chunk
