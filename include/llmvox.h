@@ -121,8 +121,9 @@ int lvx_probe_kernel(lvx_ctx* ctx, int which, int B, const int32_t* slots_dev, i
 /* Host-side view of a slot's position (synchronises the stream). */
 int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
 /* Kernel-variant switches for in-process A/B timing: "gemv_reg" (register-path GEMV, B <= 4),
- * "attn_v2", "cproj_b1", "prefetch_in", "mfma_batch" (bf16 MFMA path, 4 < B <= 32),
- * "fuse_mlp" (bf16 fused MLP, B <= 2), "fuse_argmax" (greedy select inside lm_head, B <= 4). */
+ * "attn_v2", "cproj_b1", "prefetch_in", "mfma_batch" (smallest B of the bf16 MFMA path, up to 32; 0 off),
+ * "fuse_mlp" (bf16 fused MLP, B <= 2), "fuse_argmax" (greedy select inside lm_head, B <= 4),
+ * "mfma_ln" (largest B whose batched GEMMs normalise their rows in the prologue, default 16). */
 int lvx_set_option(lvx_ctx* ctx, const char* name, int value);
 /* Enable/disable HIP-graph replay of lvx_ar_step for a given B (default on). */
 int lvx_set_graphs(lvx_ctx* ctx, int enable);

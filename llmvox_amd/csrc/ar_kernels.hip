@@ -1246,7 +1246,10 @@ __device__ __forceinline__ uint2 pack4_bf16(float4 v) {
                     (uint32_t)f32_to_bf16(v.z) | ((uint32_t)f32_to_bf16(v.w) << 16));
 }
 
-int g_opt_mfma_batch = 1;
+int g_opt_mfma_batch = 3;  // smallest B on the batched MFMA path (0: off); measured B = 3: 117 vs 154 us, B = 2: 119 vs 114
+// batched path: LayerNorm / embedding fused into the MFMA GEMM prologue for B <= this value
+// (measured: B = 8 147 vs 156 us/step; B = 32 slower, every block re-normalising 32 rows)
+int g_opt_mfma_ln = 8;
 
 // ---------------------------------------------------------------------------------
 // Batched path v2 (bf16 weights, 4 < B <= 32): every per-row prologue runs ONCE per row into a
@@ -1255,6 +1258,39 @@ int g_opt_mfma_batch = 1;
 // over its waves (K/192 waves: 4 for K=768, 16 for K=3072); every lane issues all of its
 // 16-byte fragment loads up front (one memory latency), partial tiles combine through LDS.
 // ---------------------------------------------------------------------------------
+// x row of the embedding (a2-a4) for control record ri, lane layout k = j * 256 + lane * 4:
+// normalize(cat(text_table[id], codebook[prev] | 0 at position 0), eps 1e-8) + wpe[pos]
+__device__ __forceinline__ void embed_row(const GemvArgs& a, int4 ri, int lane, float4 (&v)[3]) {
+  if (ri.x < 0) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
+  const int p = ri.y, prev = ri.w;
+  int tok = ri.z;
+  if (tok < 0) {
+    if (lane == 0) atomicOr(a.st.err, 2);
+    tok = 384;
+  }
+  float4 pe[3];
+  const float* wr_ = a.wpe + (size_t)p * D;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) pe[j] = *reinterpret_cast<const float4*>(wr_ + j * 256 + lane * 4);
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int k = j * 256 + lane * 4;
+    if (j == 0) v[j] = *reinterpret_cast<const float4*>(a.text_table + (size_t)tok * TEXT_DIM + k);
+    else if (p == 0) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    else v[j] = *reinterpret_cast<const float4*>(a.codebook + (size_t)prev * SPEECH_DIM + (k - TEXT_DIM));
+    ss += (v[j].x * v[j].x + v[j].y * v[j].y) + (v[j].z * v[j].z + v[j].w * v[j].w);
+  }
+  const float den = fmaxf(sqrtf(wave_sum(ss)), 1e-8f);
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+    v[j] = make_float4(v[j].x / den + pe[j].x, v[j].y / den + pe[j].y, v[j].z / den + pe[j].z, v[j].w / den + pe[j].w);
+}
+
 template <int MODE>  // 0: LayerNorm(x)  3: embedding (+ stores x) then LayerNorm
 __global__ __launch_bounds__(256) void ar_rows_kernel(GemvArgs a) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1267,35 +1303,7 @@ __global__ __launch_bounds__(256) void ar_rows_kernel(GemvArgs a) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) v[j] = *reinterpret_cast<const float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4);
   } else {
-    const int4 ri = a.st.rowinfo[b];
-    if (ri.x < 0) {
-#pragma unroll
-      for (int j = 0; j < 3; ++j) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-    } else {
-      const int p = ri.y, prev = ri.w;
-      int tok = ri.z;
-      if (tok < 0) {
-        if (lane == 0) atomicOr(a.st.err, 2);
-        tok = 384;
-      }
-      float4 pe[3];
-      const float* wr_ = a.wpe + (size_t)p * D;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) pe[j] = *reinterpret_cast<const float4*>(wr_ + j * 256 + lane * 4);
-      float ss = 0.f;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const int k = j * 256 + lane * 4;
-        if (j == 0) v[j] = *reinterpret_cast<const float4*>(a.text_table + (size_t)tok * TEXT_DIM + k);
-        else if (p == 0) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-        else v[j] = *reinterpret_cast<const float4*>(a.codebook + (size_t)prev * SPEECH_DIM + (k - TEXT_DIM));
-        ss += (v[j].x * v[j].x + v[j].y * v[j].y) + (v[j].z * v[j].z + v[j].w * v[j].w);
-      }
-      const float den = fmaxf(sqrtf(wave_sum(ss)), 1e-8f);
-#pragma unroll
-      for (int j = 0; j < 3; ++j)
-        v[j] = make_float4(v[j].x / den + pe[j].x, v[j].y / den + pe[j].y, v[j].z / den + pe[j].z, v[j].w / den + pe[j].w);
-    }
+    embed_row(a, a.st.rowinfo[b], lane, v);
 #pragma unroll
     for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = v[j];
   }
@@ -1398,6 +1406,100 @@ static void launch_mfma2(const GemvArgs& a, hipStream_t s) {
   else hipLaunchKernelGGL((ar_mfma2_kernel<K, 2, OUT>), grid, block, 0, s, a);
 }
 
+// Batched GEMM with the per-row prologue fused (K = 768; 4 < B <= 32): every block builds the
+// LayerNorm (MODE 0) or embedding + LayerNorm (MODE 3; block 0 also stores x) of all B rows into
+// an LDS bf16 tile, then runs the MFMA 16 x (NT*16) tile of its 16 weight rows from it. The rows
+// are recomputed by every block (B x 3 KB of x from L2) instead of paying a separate rows kernel
+// and its launch boundary; the weight fragments are in flight while the rows are normalised.
+template <int NT, int OUT, int MODE>
+__global__ __launch_bounds__(256) void ar_mfma_ln_kernel(GemvArgs a) {
+  constexpr int K = 768, NW = 4, R = NT * 16, RW = R / NW;  // rows per wave
+  constexpr int LDX = K + 8;                                 // bf16 row stride (16-B pad)
+  __shared__ __attribute__((aligned(16))) bf16_t xs[R * LDX];
+  __shared__ float red[NW][NT * 256];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int n0 = blockIdx.x * 16;
+  const int B = a.B;
+  // 1. row inputs (x rows or control records) first, then the weight fragments
+  float4 xv[RW][3];
+  int4 ri[RW];
+#pragma unroll
+  for (int i = 0; i < RW; ++i) {
+    const int b = wave + NW * i;
+    if (b < B) {
+      if (MODE == 0) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) xv[i][j] = *reinterpret_cast<const float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4);
+      } else {
+        ri[i] = a.st.rowinfo[b];
+      }
+    }
+  }
+  const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(a.W);
+  const int wrow = min(n0 + (lane & 15), a.N - 1);
+  const int k0 = wave * 192 + 8 * (lane >> 4);
+  uint4 wf[6];
+#pragma unroll
+  for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(W + (size_t)wrow * K + k0 + kk * 32);
+  float4 g[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) g[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
+  // 2. rows -> LayerNorm -> bf16 tile (rows >= B are zero: padded columns, never stored)
+#pragma unroll
+  for (int i = 0; i < RW; ++i) {
+    const int b = wave + NW * i;
+    uint2* dst = reinterpret_cast<uint2*>(xs + b * LDX);
+    if (b < B) {
+      if (MODE == 3) {
+        embed_row(a, ri[i], lane, xv[i]);
+        if (blockIdx.x == 0)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = xv[i][j];
+      }
+      wave_ln_regs(xv[i], g);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) dst[j * 64 + lane] = pack4_bf16(xv[i][j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) dst[j * 64 + lane] = make_uint2(0u, 0u);
+    }
+  }
+  __syncthreads();
+  // 3. MFMA 16x16x32: A = weight rows (lane & 15), B = tile rows (lane & 15) of column block t
+  f32x4_t acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < 6; ++kk)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const uint4 xf = *reinterpret_cast<const uint4*>(xs + (t * 16 + (lane & 15)) * LDX + k0 + kk * 32);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[kk]),
+                                                       __builtin_bit_cast(bf16x8_t, xf), acc[t], 0, 0, 0);
+    }
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[wave][(4 * (lane >> 4) + i) * (NT * 16) + t * 16 + (lane & 15)] = acc[t][i];
+  __syncthreads();
+  for (int e = tid; e < 16 * NT * 16; e += NW * 64) {
+    const int r = e / (NT * 16), b = e - r * (NT * 16), n = n0 + r;
+    if (b >= B || n >= a.N) continue;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[w][e];
+    if (OUT == 5) a.st.hb[(size_t)b * DFF + n] = f32_to_bf16(gelu_tanh(v));
+    else gemv_store<OUT>(a, n, b, v);
+  }
+}
+
+template <int OUT, int MODE>
+static void launch_mfma_ln(const GemvArgs& a, hipStream_t s) {
+  dim3 grid((a.N + 15) / 16), block(256);
+  if (a.B <= 16) hipLaunchKernelGGL((ar_mfma_ln_kernel<1, OUT, MODE>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((ar_mfma_ln_kernel<2, OUT, MODE>), grid, block, 0, s, a);
+}
+
 static int attn_ns_max(int B) {  // enough splits to fill the chip, no more (early-exit blocks cost)
   int ns = NSPLIT;
   while (ns > 1 && ns * N_HEAD * B > 1024) ns >>= 1;
@@ -1421,21 +1523,26 @@ static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_
 // op: 0 c_attn (layer 0: + embedding) 1 attention 2 c_proj (+ split merge) 3 c_fc 4 mlp c_proj 5 lm_head
 // fused lm_head + greedy select (B <= 4 GEMV path, fused step only); returns whether op 5 did the select
 template <typename TW>
+static bool use_mfma(int B) {
+  return sizeof(TW) == 2 && g_opt_mfma_batch && B >= g_opt_mfma_batch && B <= 32;
+}
+
+template <typename TW>
 static bool fused_select(int B) {
   static_assert(VOCAB / 8 <= 512 && VOCAB / 8 <= LM_MAX_BLOCKS, "fused select: lm_head grid must fit the tail");
-  return g_opt_fuse_argmax && B <= 4;
+  return g_opt_fuse_argmax && B <= 4 && !use_mfma<TW>(B);
 }
 
 template <typename TW>
 static bool fused_mlp(int B) {
-  return sizeof(TW) == 2 && g_opt_fuse_mlp && B <= 2;
+  return sizeof(TW) == 2 && g_opt_fuse_mlp && B <= 2 && !use_mfma<TW>(B);
 }
 
 // returns false when the op has no kernel of its own at this B (mlp c_proj inside the fused MLP)
 template <typename TW>
 static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtype, int B, hipStream_t s,
                       bool select = false) {
-  const bool mf = sizeof(TW) == 2 && g_opt_mfma_batch && B > 4 && B <= 32;
+  const bool mf = use_mfma<TW>(B);
   const bool fm = fused_mlp<TW>(B);
   const int nsm = mf ? attn_ns_max(B) : NSPLIT;
   a.layer = l;
@@ -1444,7 +1551,10 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
   switch (op) {
     case 0:
       a.W = w.w_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
-      if (mf) {
+      if (mf && B <= g_opt_mfma_ln) {
+        if (l == 0) launch_mfma_ln<0, 3>(a, s);
+        else launch_mfma_ln<0, 0>(a, s);
+      } else if (mf) {
         if (l == 0) hipLaunchKernelGGL((ar_rows_kernel<3>), dim3((B + 3) / 4), dim3(256), 0, s, a);
         else hipLaunchKernelGGL((ar_rows_kernel<0>), dim3((B + 3) / 4), dim3(256), 0, s, a);
         launch_mfma2<768, 0>(a, s);
@@ -1478,6 +1588,8 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
           if (B <= 1) hipLaunchKernelGGL((ar_mlp_fused_kernel<1, 16>), dim3(DFF / 16), dim3(256), 0, s, a, wfc, wpk);
           else hipLaunchKernelGGL((ar_mlp_fused_kernel<2, 16>), dim3(DFF / 16), dim3(256), 0, s, a, wfc, wpk);
         }
+      } else if (mf && B <= g_opt_mfma_ln) {
+        launch_mfma_ln<5, 0>(a, s);
       } else if (mf) {
         hipLaunchKernelGGL((ar_rows_kernel<0>), dim3((B + 3) / 4), dim3(256), 0, s, a);
         launch_mfma2<768, 5>(a, s);
@@ -1493,7 +1605,9 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       break;
     case 5:
       a.W = w.w_lm; a.N = VOCAB; a.ln_w = w.lnf;
-      if (mf) {
+      if (mf && B <= g_opt_mfma_ln) {
+        launch_mfma_ln<3, 0>(a, s);
+      } else if (mf) {
         hipLaunchKernelGGL((ar_rows_kernel<0>), dim3((B + 3) / 4), dim3(256), 0, s, a);
         launch_mfma2<768, 3>(a, s);
       } else if (select) {

@@ -475,6 +475,7 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   else if (n == "mfma_batch") g_opt_mfma_batch = value;
   else if (n == "fuse_argmax") g_opt_fuse_argmax = value;
   else if (n == "fuse_mlp") g_opt_fuse_mlp = value;
+  else if (n == "mfma_ln") g_opt_mfma_ln = value;
   else return fail(LVX_E_NAME, "unknown option " + n);
   for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);  // captured kernels change
   c->graphs.clear();

@@ -5,7 +5,7 @@ from llmvox_amd.engine import build_engine
 
 opt = sys.argv[1]
 vals = [int(v) for v in sys.argv[2:]] or [0, 1]
-e = build_engine(0, "bf16", "bf16", max_streams=8, max_positions=2048, max_codec_frames=256)
+e = build_engine(0, "bf16", "bf16", max_streams=max(8, int(os.environ.get("AB_B", "1"))), max_positions=2048, max_codec_frames=256)
 dev = e.device
 B, stride, n = int(os.environ.get("AB_B", "1")), 512, 256
 plan = torch.full((B, stride), 100, dtype=torch.int32, device=dev)
