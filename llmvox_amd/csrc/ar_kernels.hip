@@ -514,9 +514,16 @@ __device__ __forceinline__ void gemv_store(const GemvArgs& a, int n, int b, floa
       store_kv(a, which, idx, v);
     }
   } else if (OUT == 1) {
-    a.st.x[(size_t)b * D + n] += v;
+    float* xp = a.st.x + (size_t)b * D + n;
+    float t = *xp;
+    if (a.yacc && a.add_y)  // c_proj: fold the pending split-K partials of the previous mlp c_proj
+#pragma unroll
+      for (int c = 0; c < YCOPIES; ++c) t += a.yacc[((size_t)c * a.st.max_streams + b) * D + n];
+    *xp = t + v;
   } else if (OUT == 2) {
     a.st.h[(size_t)b * DFF + n] = gelu_tanh(v);
+  } else if (OUT == 6) {  // split-K partial of mlp c_proj (K slice blockIdx.y) -> pending copy
+    a.yacc[((size_t)blockIdx.y * a.st.max_streams + b) * D + n] = v;
   } else {
     a.dst[(size_t)b * a.N + n] = v;
   }
@@ -1291,7 +1298,8 @@ __device__ __forceinline__ void embed_row(const GemvArgs& a, int4 ri, int lane, 
     v[j] = make_float4(v[j].x / den + pe[j].x, v[j].y / den + pe[j].y, v[j].z / den + pe[j].z, v[j].w / den + pe[j].w);
 }
 
-template <int MODE>  // 0: LayerNorm(x)  3: embedding (+ stores x) then LayerNorm
+// 0: LayerNorm(x)  4: LayerNorm(x + pending copies)  3: embedding (+ stores x) then LayerNorm
+template <int MODE>
 __global__ __launch_bounds__(256) void ar_rows_kernel(GemvArgs a) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int b = blockIdx.x * 4 + wave;
@@ -1299,9 +1307,10 @@ __global__ __launch_bounds__(256) void ar_rows_kernel(GemvArgs a) {
   float4 g[3], v[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) g[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
-  if (MODE == 0) {
-#pragma unroll
-    for (int j = 0; j < 3; ++j) v[j] = *reinterpret_cast<const float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4);
+  if (MODE == 0 || MODE == 4) {
+    XRow<MODE> r;
+    xrow_issue(a, b, lane, r);
+    xrow_sum(r, v);
   } else {
     embed_row(a, a.st.rowinfo[b], lane, v);
 #pragma unroll
@@ -1352,8 +1361,9 @@ __global__ __launch_bounds__(256) void ar_merge_bf16_kernel(ArState st, int ns_m
   }
 }
 
-// OUT as gemv_store, plus OUT 5: h (bf16) = gelu_tanh(v) for the batched mlp c_proj
-template <int K, int NT, int OUT>
+// OUT as gemv_store, plus OUT 5: h (bf16) = gelu_tanh(v) for the batched mlp c_proj. A block
+// covers K columns starting at blockIdx.y * K of rows of length KTOT (KTOT > K: split K, OUT 6).
+template <int K, int NT, int OUT, int KTOT = K>
 __global__ __launch_bounds__(1024) void ar_mfma2_kernel(GemvArgs a) {
   constexpr int NW = K / 192;  // waves per block, each a 192-wide K slice (6 MFMA k-steps)
   __shared__ float red[NW][NT * 256];
@@ -1361,17 +1371,17 @@ __global__ __launch_bounds__(1024) void ar_mfma2_kernel(GemvArgs a) {
   const int n0 = blockIdx.x * 16;
   const int B = a.B;
   const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(a.W);
-  const bf16_t* __restrict__ X = (K == 768) ? a.st.xn : a.st.hb;
+  const bf16_t* __restrict__ X = (KTOT == 768) ? a.st.xn : a.st.hb;
   const int wrow = min(n0 + (lane & 15), a.N - 1);
-  const int k0 = wave * 192 + 8 * (lane >> 4);
+  const int k0 = blockIdx.y * K + wave * 192 + 8 * (lane >> 4);
   uint4 wf[6], xf[NT][6];
 #pragma unroll
-  for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(W + (size_t)wrow * K + k0 + kk * 32);
+  for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(W + (size_t)wrow * KTOT + k0 + kk * 32);
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int b = min(t * 16 + (lane & 15), B - 1);  // padded columns recompute row B-1, never stored
 #pragma unroll
-    for (int kk = 0; kk < 6; ++kk) xf[t][kk] = *reinterpret_cast<const uint4*>(X + (size_t)b * K + k0 + kk * 32);
+    for (int kk = 0; kk < 6; ++kk) xf[t][kk] = *reinterpret_cast<const uint4*>(X + (size_t)b * KTOT + k0 + kk * 32);
   }
   f32x4_t acc[NT];
 #pragma unroll
@@ -1406,8 +1416,19 @@ static void launch_mfma2(const GemvArgs& a, hipStream_t s) {
   else hipLaunchKernelGGL((ar_mfma2_kernel<K, 2, OUT>), grid, block, 0, s, a);
 }
 
-// Batched GEMM with the per-row prologue fused (K = 768; 4 < B <= 32): every block builds the
-// LayerNorm (MODE 0) or embedding + LayerNorm (MODE 3; block 0 also stores x) of all B rows into
+// mlp c_proj (K = 3072) split into YCOPIES K slices of 768: 4x the blocks of the unsplit GEMM;
+// each slice's partial goes to its pending copy (plain stores, deterministic), folded into x by
+// the next c_proj and read as x + sum of copies by the next c_attn / lm_head prologue
+static void launch_mproj_split(const GemvArgs& a, hipStream_t s) {
+  static_assert(DFF == YCOPIES * 768, "one pending copy per K slice");
+  dim3 grid((a.N + 15) / 16, YCOPIES), block(256);
+  if (a.B <= 16) hipLaunchKernelGGL((ar_mfma2_kernel<768, 1, 6, DFF>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((ar_mfma2_kernel<768, 2, 6, DFF>), grid, block, 0, s, a);
+}
+
+// Batched GEMM with the per-row prologue fused (K = 768; small B): every block builds the
+// LayerNorm (MODE 0), LayerNorm of x + pending copies (MODE 4) or embedding + LayerNorm (MODE 3;
+// block 0 also stores x) of all B rows into
 // an LDS bf16 tile, then runs the MFMA 16 x (NT*16) tile of its 16 weight rows from it. The rows
 // are recomputed by every block (B x 3 KB of x from L2) instead of paying a separate rows kernel
 // and its launch boundary; the weight fragments are in flight while the rows are normalised.
@@ -1427,7 +1448,7 @@ __global__ __launch_bounds__(256) void ar_mfma_ln_kernel(GemvArgs a) {
   for (int i = 0; i < RW; ++i) {
     const int b = wave + NW * i;
     if (b < B) {
-      if (MODE == 0) {
+      if (MODE == 0 || MODE == 4) {
 #pragma unroll
         for (int j = 0; j < 3; ++j) xv[i][j] = *reinterpret_cast<const float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4);
       } else {
@@ -1455,6 +1476,14 @@ __global__ __launch_bounds__(256) void ar_mfma_ln_kernel(GemvArgs a) {
         if (blockIdx.x == 0)
 #pragma unroll
           for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = xv[i][j];
+      } else if (MODE == 4) {  // + the pending split-K copies of the previous mlp c_proj
+#pragma unroll
+        for (int c = 0; c < YCOPIES; ++c)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            const float4 y = *reinterpret_cast<const float4*>(a.yacc + ((size_t)c * a.st.max_streams + b) * D + j * 256 + lane * 4);
+            xv[i][j].x += y.x; xv[i][j].y += y.y; xv[i][j].z += y.z; xv[i][j].w += y.w;
+          }
       }
       wave_ln_regs(xv[i], g);
 #pragma unroll
@@ -1546,17 +1575,17 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
   const bool fm = fused_mlp<TW>(B);
   const int nsm = mf ? attn_ns_max(B) : NSPLIT;
   a.layer = l;
-  a.yacc = fm ? a.st.yacc : nullptr;
+  a.yacc = (fm || mf) ? a.st.yacc : nullptr;
   a.add_y = l > 0;
   switch (op) {
     case 0:
       a.W = w.w_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
       if (mf && B <= g_opt_mfma_ln) {
         if (l == 0) launch_mfma_ln<0, 3>(a, s);
-        else launch_mfma_ln<0, 0>(a, s);
+        else launch_mfma_ln<0, 4>(a, s);
       } else if (mf) {
         if (l == 0) hipLaunchKernelGGL((ar_rows_kernel<3>), dim3((B + 3) / 4), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((ar_rows_kernel<0>), dim3((B + 3) / 4), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((ar_rows_kernel<4>), dim3((B + 3) / 4), dim3(256), 0, s, a);
         launch_mfma2<768, 0>(a, s);
       } else if (l == 0) {
         launch_gemv<TW, 768, 1, 2, 3, 0>(a, s);
@@ -1600,15 +1629,15 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
     case 4:
       a.W = w.w_mproj[l]; a.N = D;
       if (fm) return false;
-      if (mf) launch_mfma2<3072, 1>(a, s);
+      if (mf) launch_mproj_split(a, s);
       else launch_gemv<TW, 3072, 4, 2, 1, 1>(a, s);
       break;
     case 5:
       a.W = w.w_lm; a.N = VOCAB; a.ln_w = w.lnf;
       if (mf && B <= g_opt_mfma_ln) {
-        launch_mfma_ln<3, 0>(a, s);
+        launch_mfma_ln<3, 4>(a, s);
       } else if (mf) {
-        hipLaunchKernelGGL((ar_rows_kernel<0>), dim3((B + 3) / 4), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((ar_rows_kernel<4>), dim3((B + 3) / 4), dim3(256), 0, s, a);
         launch_mfma2<768, 3>(a, s);
       } else if (select) {
         if (fm) launch_gemv<TW, 768, 1, 2, 4, 4>(a, s);
