@@ -17,6 +17,11 @@
 // B streams of the step.
 #include "lvx_internal.h"
 
+// No implicit a*b+c contraction in this file: the compiler would choose per unrolled copy, so a
+// batch row's rounding could depend on which copy (batch position) computed it. Fused
+// multiply-adds are written out (fmaf / MFMA) where they are wanted.
+#pragma clang fp contract(off)
+
 namespace lvx {
 
 // ---------------------------------------------------------------------------------
@@ -1026,7 +1031,7 @@ __global__ __launch_bounds__(256) void ar_attn_kernel(ArState st, int layer) {
         const float* kr = Ks + key * KS_LD + part * 24;
         const float* qr = qs + part * 24;
 #pragma unroll
-        for (int d = 0; d < 24; ++d) acc += qr[d] * kr[d];
+        for (int d = 0; d < 24; ++d) acc = fmaf(qr[d], kr[d], acc);
       }
       acc += __shfl_xor(acc, 1, 64);
       acc += __shfl_xor(acc, 2, 64);
@@ -1046,7 +1051,7 @@ __global__ __launch_bounds__(256) void ar_attn_kernel(ArState st, int layer) {
     if (tid < 2 * HD) {
       float acc = 0.f;
       const int j0 = oh * (ATK / 2), j1 = min(nk, j0 + ATK / 2);
-      for (int j = j0; j < j1; ++j) acc += ps[j] * Vs[j * HD + od];
+      for (int j = j0; j < j1; ++j) acc = fmaf(ps[j], Vs[j * HD + od], acc);
       o = o * alpha + acc;
     }
     l = l * alpha + ((red[4] + red[5]) + (red[6] + red[7]));
@@ -1126,7 +1131,7 @@ __global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer, 
     float sc = 0.f;
     if (valid) {
 #pragma unroll
-      for (int i = 0; i < 24; ++i) sc += q[i] * kf[i];
+      for (int i = 0; i < 24; ++i) sc = fmaf(q[i], kf[i], sc);
     }
     sc += __shfl_xor(sc, 1, 64);
     sc += __shfl_xor(sc, 2, 64);
@@ -1137,7 +1142,7 @@ __global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer, 
     const float p = valid ? expf(sc - mn) : 0.f;
     l = l * alpha + wave_sum(part == 0 ? p : 0.f);
 #pragma unroll
-    for (int i = 0; i < 24; ++i) o[i] = o[i] * alpha + (valid ? p * vf[i] : 0.f);
+    for (int i = 0; i < 24; ++i) o[i] = fmaf(valid ? p : 0.f, valid ? vf[i] : 0.f, o[i] * alpha);
     m = mn;
   }
   // sum o over the 16 key slots of the wave (lanes with equal part)
@@ -1529,6 +1534,194 @@ static void launch_mfma_ln(const GemvArgs& a, hipStream_t s) {
   else hipLaunchKernelGGL((ar_mfma_ln_kernel<2, OUT, MODE>), grid, block, 0, s, a);
 }
 
+// ---------------------------------------------------------------------------------
+// Batched path v3 (bf16 weights, g_opt_mfma_batch <= B <= 64; option "bt"): five kernels per
+// layer and no pending partials, so every x row is final at each kernel boundary:
+//   c_attn       LN1(x) prologue (layer 0: embedding, which also stores x), q / KV-append epilogue
+//   attention    split-KV ar_attn_v2
+//   c_proj       split-KV merge prologue, x += epilogue
+//   c_fc         LN2(x) prologue, gelu -> hb (bf16) epilogue
+//   mlp c_proj   hb operand straight from global, x += epilogue
+// A block owns 16 weight rows (blockIdx.x) x R = NT*16 batch rows (blockIdx.y). K is split over
+// its waves (192 columns = 6 MFMA k-steps each). The weight fragments are issued first (they do not
+// depend on the step), then the per-row prologue builds the bf16 operand tile in LDS; the waves'
+// partial 16 x R tiles are summed through LDS in fixed order (deterministic, equal rows bit-equal).
+// ---------------------------------------------------------------------------------
+template <int K, int NT, int IN, int OUT>
+__global__ __launch_bounds__(K / 192 * 64) void ar_bt_kernel(GemvArgs a, int ns_max) {
+  constexpr int NW = K / 192, R = NT * 16, NTH = NW * 64;
+  constexpr bool STAGE = IN != 1;  // operand tile staged in LDS (K == 768)
+  static_assert(!STAGE || K == 768, "the LDS operand tile holds K = 768 rows");
+  constexpr int LDX = D + 8;  // bf16 row stride of the tile (16-B pad)
+  __shared__ __attribute__((aligned(16))) bf16_t xs[STAGE ? R * LDX : 8];
+  __shared__ float red[NW][16 * R];
+  __shared__ float cf[IN == 2 ? R * N_HEAD * NSPLIT : 1];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int n0 = blockIdx.x * 16, r0 = blockIdx.y * R;
+  const int B = a.B;
+  const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(a.W);
+  const bf16_t* __restrict__ X = K == D ? a.st.xn : a.st.hb;  // IN 1 operand rows
+  const int wrow = min(n0 + (lane & 15), a.N - 1);
+  const int k0 = wave * 192 + 8 * (lane >> 4);
+  uint4 wf[6];
+  if constexpr (IN == 0 || IN == 3) {
+    constexpr int RPW = R / NW;  // rows per wave, normalised 4 at a time
+    float4 g[3];
+#pragma unroll
+    for (int gi = 0; gi < RPW; gi += 4) {
+      float4 xv[4][3];
+      int4 ri[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int b = r0 + wave * RPW + gi + i;
+        if (b < B) {
+          if (IN == 0) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) xv[i][j] = *reinterpret_cast<const float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4);
+          } else {
+            ri[i] = a.st.rowinfo[b];
+          }
+        }
+      }
+      if (gi == 0) {  // weights behind the first row group's inputs (vmcnt retires in issue order)
+#pragma unroll
+        for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(W + (size_t)wrow * K + k0 + kk * 32);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) g[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rr = wave * RPW + gi + i, b = r0 + rr;
+        uint2* dst = reinterpret_cast<uint2*>(xs + rr * LDX);
+        if (b < B) {
+          if (IN == 3) {
+            embed_row(a, ri[i], lane, xv[i]);
+            if (blockIdx.x == 0)
+#pragma unroll
+              for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = xv[i][j];
+          }
+          wave_ln_regs(xv[i], g);
+#pragma unroll
+          for (int j = 0; j < 3; ++j) dst[j * 64 + lane] = pack4_bf16(xv[i][j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 3; ++j) dst[j * 64 + lane] = make_uint2(0u, 0u);
+        }
+      }
+    }
+  } else if constexpr (IN == 2) {
+    // split-KV merge: y = sum_s c_s o_s, c_s = e^{m_s - M} / sum_s' e^{m_s' - M} l_s'
+    // phase A: one thread per (row, head) -> coefficients (zero for unused splits)
+#pragma unroll
+    for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(W + (size_t)wrow * K + k0 + kk * 32);
+    for (int qa = tid; qa < R * N_HEAD; qa += NTH) {
+      const int b = r0 + qa / N_HEAD, head = qa % N_HEAD;
+      float* c = cf + qa * NSPLIT;
+      if (b >= B) {
+#pragma unroll
+        for (int i = 0; i < NSPLIT; ++i) c[i] = 0.f;
+        continue;
+      }
+      const int4 ri = a.st.rowinfo[b];
+      const float2* mlp = reinterpret_cast<const float2*>(a.st.part_ml) + (size_t)(b * N_HEAD + head) * NSPLIT;
+      float2 ml[NSPLIT];
+#pragma unroll
+      for (int i = 0; i < NSPLIT; ++i) ml[i] = i < ns_max ? mlp[i] : make_float2(-INFINITY, 0.f);
+      const int ns = ri.x < 0 ? 0 : min(ns_max, (ri.y + 1 + 63) / 64);
+      float M = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < NSPLIT; ++i) if (i < ns) M = fmaxf(M, ml[i].x);
+      float den = 0.f, f[NSPLIT];
+#pragma unroll
+      for (int i = 0; i < NSPLIT; ++i) {
+        f[i] = (i < ns && ml[i].x != -INFINITY) ? expf(ml[i].x - M) : 0.f;
+        den += f[i] * ml[i].y;
+      }
+      const float inv = ns ? 1.0f / den : 0.f;
+#pragma unroll
+      for (int i = 0; i < NSPLIT; ++i) c[i] = f[i] * inv;
+    }
+    __syncthreads();
+    // phase B: (row, 4-element group) pairs, every used split summed (part_o holds finite values)
+    for (int e = tid; e < R * (D / 4); e += NTH) {
+      const int rr = e / (D / 4), c4 = (e - rr * (D / 4)) * 4, b = r0 + rr;
+      uint2* dst = reinterpret_cast<uint2*>(xs + rr * LDX + c4);
+      if (b >= B) { *dst = make_uint2(0u, 0u); continue; }
+      const int head = c4 / HD, d = c4 - head * HD;
+      const float* po = a.st.part_o + ((size_t)(b * N_HEAD + head) * NSPLIT) * HD + d;
+      const float* c = cf + (rr * N_HEAD + head) * NSPLIT;
+      float4 y = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int i = 0; i < NSPLIT; ++i) {
+        if (i < ns_max) {
+          const float4 p = *reinterpret_cast<const float4*>(po + (size_t)i * HD);
+          y.x += c[i] * p.x; y.y += c[i] * p.y; y.z += c[i] * p.z; y.w += c[i] * p.w;
+        }
+      }
+      *dst = pack4_bf16(y);
+    }
+  } else {  // IN 1: bf16 operand rows (hb, or xn of the separate merge kernel) straight from global
+#pragma unroll
+    for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(W + (size_t)wrow * K + k0 + kk * 32);
+  }
+  if constexpr (STAGE) __syncthreads();
+  f32x4_t acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    uint4 xf[6];
+    if constexpr (STAGE) {
+#pragma unroll
+      for (int kk = 0; kk < 6; ++kk) xf[kk] = *reinterpret_cast<const uint4*>(xs + (t * 16 + (lane & 15)) * LDX + k0 + kk * 32);
+    } else {
+      const int b = min(r0 + t * 16 + (lane & 15), B - 1);  // padded columns recompute row B-1, never stored
+#pragma unroll
+      for (int kk = 0; kk < 6; ++kk) xf[kk] = *reinterpret_cast<const uint4*>(X + (size_t)b * K + k0 + kk * 32);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 6; ++kk)
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[kk]),
+                                                       __builtin_bit_cast(bf16x8_t, xf[kk]), acc[t], 0, 0, 0);
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[wave][(4 * (lane >> 4) + i) * R + t * 16 + (lane & 15)] = acc[t][i];
+  __syncthreads();
+  for (int e = tid; e < 16 * R; e += NTH) {
+    const int r = e / R, c = e - r * R, n = n0 + r, b = r0 + c;
+    if (b >= B || n >= a.N) continue;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[w][e];
+    if (OUT == 5) a.st.hb[(size_t)b * DFF + n] = f32_to_bf16(gelu_tanh(v));
+    else if (OUT == 1) a.st.x[(size_t)b * D + n] += v;
+    else gemv_store<OUT>(a, n, b, v);
+  }
+}
+
+// Measured (tools/bt_sweep.py, us per step at positions 256-511): v3 saves kernels but every block
+// re-reads the fp32 x rows of its batch tile, and per-CU load bandwidth (not launch count) sets the
+// time of these short GEMMs: B = 8 / 16 / 32 v2 149 / 162 / 191 vs v3 172 / 181 / 203 (16-row
+// tiles, separate merge); a fused merge re-reads ns_max partials per row and block: 271 / 302 / 266.
+// v3 therefore runs only where v2 has no kernels (32 < B <= 64: 250 us, 16-row tiles).
+int g_opt_bt = 1;        // 0: off; 1: batched path v3 for 32 < B <= 64; 2: v3 for every batched B
+int g_opt_bt_rows = 16;  // batch rows per block (16 / 32 / 64)
+int g_opt_bt_merge = 0;  // split-KV merge in the c_proj prologue (0: separate ar_merge_bf16 kernel)
+
+template <int K, int IN, int OUT>
+static void launch_bt(const GemvArgs& a, int ns_max, hipStream_t s) {
+  const int R = g_opt_bt_rows <= 16 ? 16 : (g_opt_bt_rows <= 32 ? 32 : 64);
+  const int Bp = (a.B + 15) / 16 * 16;
+  const int NT = (R < Bp ? R : Bp) / 16;
+  dim3 grid((a.N + 15) / 16, (a.B + NT * 16 - 1) / (NT * 16)), block(K / 192 * 64);
+  if (NT == 1) hipLaunchKernelGGL((ar_bt_kernel<K, 1, IN, OUT>), grid, block, 0, s, a, ns_max);
+  else if (NT == 2) hipLaunchKernelGGL((ar_bt_kernel<K, 2, IN, OUT>), grid, block, 0, s, a, ns_max);
+  else if (NT == 3) hipLaunchKernelGGL((ar_bt_kernel<K, 3, IN, OUT>), grid, block, 0, s, a, ns_max);
+  else hipLaunchKernelGGL((ar_bt_kernel<K, 4, IN, OUT>), grid, block, 0, s, a, ns_max);
+}
+
 static int attn_ns_max(int B) {  // enough splits to fill the chip, no more (early-exit blocks cost)
   int ns = NSPLIT;
   while (ns > 1 && ns * N_HEAD * B > 1024) ns >>= 1;
@@ -1552,8 +1745,42 @@ static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_
 // op: 0 c_attn (layer 0: + embedding) 1 attention 2 c_proj (+ split merge) 3 c_fc 4 mlp c_proj 5 lm_head
 // fused lm_head + greedy select (B <= 4 GEMV path, fused step only); returns whether op 5 did the select
 template <typename TW>
+static bool use_bt(int B) {
+  return sizeof(TW) == 2 && g_opt_bt && g_opt_mfma_batch && B >= g_opt_mfma_batch && B <= 64 &&
+         (B > 32 || g_opt_bt == 2);
+}
+
+template <typename TW>
 static bool use_mfma(int B) {
-  return sizeof(TW) == 2 && g_opt_mfma_batch && B >= g_opt_mfma_batch && B <= 32;
+  return sizeof(TW) == 2 && g_opt_mfma_batch && B >= g_opt_mfma_batch && (B <= 32 || use_bt<TW>(B));
+}
+
+// batched path v3: one kernel per op (plus the attention), final x rows at every boundary
+static void launch_op_bt(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtype, int B, hipStream_t s) {
+  const int nsm = attn_ns_max(B);
+  a.layer = l;
+  a.yacc = nullptr;
+  a.add_y = 0;
+  switch (op) {
+    case 0:
+      a.W = w.w_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
+      if (l == 0) launch_bt<768, 3, 0>(a, 0, s);
+      else launch_bt<768, 0, 0>(a, 0, s);
+      break;
+    case 1: launch_attn(a.st, kvdtype, B, l, s, nsm); break;
+    case 2:
+      a.W = w.w_aproj[l]; a.N = D;
+      if (g_opt_bt_merge) {
+        launch_bt<768, 2, 1>(a, nsm, s);
+      } else {
+        hipLaunchKernelGGL(ar_merge_bf16_kernel, dim3(B), dim3(256), 0, s, a.st, nsm);
+        launch_bt<768, 1, 1>(a, 0, s);
+      }
+      break;
+    case 3: a.W = w.w_fc[l]; a.N = DFF; a.ln_w = w.ln2[l]; launch_bt<768, 0, 5>(a, 0, s); break;
+    case 4: a.W = w.w_mproj[l]; a.N = D; launch_bt<3072, 1, 1>(a, 0, s); break;
+    case 5: a.W = w.w_lm; a.N = VOCAB; a.ln_w = w.lnf; launch_bt<768, 0, 3>(a, 0, s); break;
+  }
 }
 
 template <typename TW>
@@ -1571,6 +1798,10 @@ static bool fused_mlp(int B) {
 template <typename TW>
 static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtype, int B, hipStream_t s,
                       bool select = false) {
+  if (use_bt<TW>(B) && !a.emb_row) {
+    launch_op_bt(op, a, w, l, kvdtype, B, s);
+    return true;
+  }
   const bool mf = use_mfma<TW>(B);
   const bool fm = fused_mlp<TW>(B);
   const int nsm = mf ? attn_ns_max(B) : NSPLIT;

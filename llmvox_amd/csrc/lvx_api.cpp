@@ -476,6 +476,9 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   else if (n == "fuse_argmax") g_opt_fuse_argmax = value;
   else if (n == "fuse_mlp") g_opt_fuse_mlp = value;
   else if (n == "mfma_ln") g_opt_mfma_ln = value;
+  else if (n == "bt") g_opt_bt = value;
+  else if (n == "bt_rows") g_opt_bt_rows = value;
+  else if (n == "bt_merge") g_opt_bt_merge = value;
   else return fail(LVX_E_NAME, "unknown option " + n);
   for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);  // captured kernels change
   c->graphs.clear();
