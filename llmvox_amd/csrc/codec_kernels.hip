@@ -15,6 +15,9 @@
 
 #include "lvx_internal.h"
 
+// no implicit a*b+c contraction: rows / frames computed by different unrolled copies round alike
+#pragma clang fp contract(off)
+
 namespace lvx {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -25,9 +28,9 @@ enum { A_PLAIN = 0, A_CONV = 1 };
 enum { E_BIAS = 0, E_BIAS_GELU = 1, E_BIAS_GAMMA_RES = 2, E_BIAS_RES = 3, E_SCALE = 4 };
 
 struct GemmArgs {
-  const float* A; int lda;
+  const void* A; int lda;    // fp32 or bf16 activations (kernel template TA)
   const void* W; int ldw;
-  float* C; int ldc;
+  void* C; int ldc;          // fp32 or bf16 output (kernel template TC)
   const float* bias; const float* gamma; const float* res; int ldr;
   int M, N, K;
   long long sA, sW, sC, sR;  // per-batch strides (elements)
@@ -35,6 +38,7 @@ struct GemmArgs {
   int cin, taps;
   float alpha;
   int ksplit;                // >1: deterministic split-K through the fp32 workspace `ws`
+  int xcd_remap;             // gemm_bf16_kernel: XCD-aware tile order (option codec_xcd)
   float* ws;
 };
 
@@ -86,7 +90,30 @@ constexpr int BM = 64, BN = 64, BK = 32;
 constexpr int LDF = BK + 1;  // fp32 LDS row (conflict-free b32 column reads)
 constexpr int LDH = BK + 8;  // bf16 LDS row (80 B)
 
-template <bool BF, typename TB, int AMODE, int EPI>
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4n __attribute__((ext_vector_type(4)));
+// one 16-B A chunk from global, replaced by zeros when !ok (conv padding) with a select
+__device__ __forceinline__ void g2_ld(u32x4& v, const bf16_t* src, bool ok) {
+  const u32x4 t = *reinterpret_cast<const u32x4*>(src);
+  v = ok ? t : u32x4{0u, 0u, 0u, 0u};
+}
+__device__ __forceinline__ void g2_ld(f32x4n& v, const float* src, bool ok) {
+  const f32x4n t = *reinterpret_cast<const f32x4n*>(src);
+  v = ok ? t : f32x4n{0.f, 0.f, 0.f, 0.f};
+}
+// one A chunk into the bf16 LDS tile: 8 bf16 as they are, or 4 fp32 rounded to bf16
+__device__ __forceinline__ void g2_st(bf16_t* d, u32x4 v) { *reinterpret_cast<u32x4*>(d) = v; }
+__device__ __forceinline__ void g2_st(bf16_t* d, f32x4n f) {
+  *reinterpret_cast<uint2*>(d) = make_uint2((uint32_t)f32_to_bf16(f.x) | ((uint32_t)f32_to_bf16(f.y) << 16),
+                                            (uint32_t)f32_to_bf16(f.z) | ((uint32_t)f32_to_bf16(f.w) << 16));
+}
+
+template <typename TC>
+__device__ __forceinline__ void store_out(TC* p, float v);
+template <> __device__ __forceinline__ void store_out<float>(float* p, float v) { *p = v; }
+template <> __device__ __forceinline__ void store_out<bf16_t>(bf16_t* p, float v) { *p = f32_to_bf16(v); }
+
+template <bool BF, typename TA, typename TB, int AMODE, int EPI, typename TC>
 __global__ __launch_bounds__(256) void gemm_mfma_kernel(GemmArgs g) {
   constexpr int LDSZ = BF ? (BM * LDH / 2) : (BM * LDF);  // in floats
   __shared__ __attribute__((aligned(16))) float As_[LDSZ];
@@ -95,7 +122,7 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(GemmArgs g) {
   const int wm = wave >> 1, wn = wave & 1;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int zb = blockIdx.z / g.ksplit, ks = blockIdx.z - zb * g.ksplit;
-  const float* A = g.A + zb * g.sA;
+  const TA* A = reinterpret_cast<const TA*>(g.A) + zb * g.sA;
   const TB* W = reinterpret_cast<const TB*>(g.W) + zb * g.sW;
   const int lrow = tid >> 2, lseg = (tid & 3) * 8;
   const int am = m0 + lrow, bn = n0 + lrow;
@@ -111,16 +138,16 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(GemmArgs g) {
     const int k = kt * BK + lseg;
     if (am < g.M) {
       if (AMODE == A_PLAIN) {
-        const float* ap = A + (size_t)am * g.lda + k;
-        if (k + 8 <= g.K) load8<float>(ap, av);
+        const TA* ap = A + (size_t)am * g.lda + k;
+        if (k + 8 <= g.K) load8<TA>(ap, av);
         else {
 #pragma unroll
-          for (int i = 0; i < 8; ++i) av[i] = (k + i < g.K) ? ap[i] : 0.f;
+          for (int i = 0; i < 8; ++i) av[i] = (k + i < g.K) ? Ld<TA>::load1(ap + i) : 0.f;
         }
       } else {
         const int tap = k / g.cin, c = k - tap * g.cin;
         const int tt = at + tap - (g.taps - 1) / 2;
-        if (tt >= 0 && tt < g.L) load8<float>(A + ((size_t)ab * g.L + tt) * g.cin + c, av);
+        if (tt >= 0 && tt < g.L) load8<TA>(A + ((size_t)ab * g.L + tt) * g.cin + c, av);
       }
     }
     if (bn < g.N) {
@@ -181,19 +208,19 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(GemmArgs g) {
     }
     return;
   }
-  float* C = g.C + zb * g.sC;
+  TC* C = reinterpret_cast<TC*>(g.C) + zb * g.sC;
   const float* R = g.res ? g.res + zb * g.sR : nullptr;
   const float bias = (EPI != E_SCALE && g.bias) ? g.bias[col] : 0.f;
   const float gam = (EPI == E_BIAS_GAMMA_RES) ? g.gamma[col] : 0.f;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if (row < g.M) C[(size_t)row * g.ldc + col] = gemm_epi<EPI>(g, R, row, col, acc[r], bias, gam);
+    if (row < g.M) store_out<TC>(C + (size_t)row * g.ldc + col, gemm_epi<EPI>(g, R, row, col, acc[r], bias, gam));
   }
 }
 
 // sum the ksplit partials in split order, then the epilogue
-template <int EPI>
+template <int EPI, typename TC>
 __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmArgs g, int batch) {
   const size_t MN = (size_t)g.M * g.N;
   const size_t total = MN * batch;
@@ -206,13 +233,13 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmArgs g, int batch)
     const float* R = g.res ? g.res + zb * g.sR : nullptr;
     const float bias = (EPI != E_SCALE && g.bias) ? g.bias[col] : 0.f;
     const float gam = (EPI == E_BIAS_GAMMA_RES) ? g.gamma[col] : 0.f;
-    g.C[zb * g.sC + (size_t)row * g.ldc + col] = gemm_epi<EPI>(g, R, row, col, v, bias, gam);
+    store_out<TC>(reinterpret_cast<TC*>(g.C) + zb * g.sC + (size_t)row * g.ldc + col, gemm_epi<EPI>(g, R, row, col, v, bias, gam));
   }
 }
 
 static size_t g_ws_floats = 0;  // capacity of the split-K workspace (set by the front end)
 
-template <bool BF, typename TB, int AMODE, int EPI>
+template <bool BF, typename TA, typename TB, int AMODE, int EPI, typename TC>
 static void gemm_launch(GemmArgs g, int batch, hipStream_t s) {
   const int tiles = ((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM) * batch;
   const int nkt = (g.K + BK - 1) / BK;
@@ -222,25 +249,260 @@ static void gemm_launch(GemmArgs g, int batch, hipStream_t s) {
   while (tiles * ks * 2 <= 320 && nkt / (ks * 2) >= 4 && (size_t)(ks * 2) * g.M * g.N * batch <= g_ws_floats) ks *= 2;
   g.ksplit = ks;
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, batch * ks);
-  hipLaunchKernelGGL((gemm_mfma_kernel<BF, TB, AMODE, EPI>), grid, dim3(256), 0, s, g);
+  hipLaunchKernelGGL((gemm_mfma_kernel<BF, TA, TB, AMODE, EPI, TC>), grid, dim3(256), 0, s, g);
   if (ks > 1) {
     const size_t total = (size_t)g.M * g.N * batch;
     const int blocks = (int)std::min<size_t>((total + 255) / 256, 2048);
-    hipLaunchKernelGGL((gemm_splitk_reduce<EPI>), dim3(blocks), dim3(256), 0, s, g, batch);
+    hipLaunchKernelGGL((gemm_splitk_reduce<EPI, TC>), dim3(blocks), dim3(256), 0, s, g, batch);
+  }
+}
+// ---------------------------------------------------------------------------------
+// bf16 weight GEMM for large M (bf16 mode): 128 x 128 block tile, BK 64, 4 waves in 2 x 2, each
+// a 64 x 64 tile of four v_mfma_f32_32x32x16_bf16 accumulators. Operands are bf16 in LDS (double
+// buffered: one barrier per k-tile); the next k-tile's global loads are in flight in registers
+// while the current one is multiplied, and up to two blocks share a CU (73 KB LDS each), so one
+// block's loads overlap the other's MFMAs. A is bf16 (TA = bf16_t: activations written in bf16 by
+// their producer, identical to rounding them here) or fp32 (rounded on the way into LDS), plain
+// or implicit-Conv1d. TC = output type of the plain epilogue (bf16 for the GELU output that only
+// feeds the next GEMM). Rows of every tile are whole 128-B runs: coalesced loads and stores.
+// ---------------------------------------------------------------------------------
+constexpr int G2_BM = 128, G2_BN = 128, G2_BK = 64, G2_LDK = G2_BK + 8;  // bf16 row stride 144 B
+
+template <typename TA> struct ALoad;
+template <> struct ALoad<bf16_t> {  // 4 x 16 B per thread per tile (native vectors: register-resident)
+  u32x4 v[4];
+};
+template <> struct ALoad<float> {  // 8 x 16 B per thread per tile
+  f32x4n v[8];
+};
+
+
+template <typename TA, int AMODE, int EPI, typename TC>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) bf16_t As[2][G2_BM * G2_LDK];
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[2][G2_BN * G2_LDK];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  // XCD-aware tile order: workgroups are dealt round-robin to the 8 XCDs (id % 8), so XCD x gets
+  // the contiguous logical range [x * T/8, (x+1) * T/8); logical tiles walk G2_GM M-tiles down one
+  // N column before moving right, so the ~64 tiles in flight on an XCD share 8 A row-blocks and
+  // 8 weight row-blocks in that XCD's L2 instead of touching all of them.
+  const int ntn = gridDim.x, ntm = gridDim.y, T = ntn * ntm;
+  const int pid = blockIdx.x + ntn * blockIdx.y;
+  int q = pid;
+  if (g.xcd_remap && (T & 7) == 0) q = (pid & 7) * (T >> 3) + (pid >> 3);
+  const int G2_GM = g.xcd_remap ? 8 : 1;
+  const int gsz = G2_GM * ntn, grp = q / gsz, within = q - grp * gsz;
+  const int gm = min(G2_GM, ntm - grp * G2_GM);
+  const int tm = grp * G2_GM + within % gm, tn = within / gm;
+  const int m0 = tm * G2_BM, n0 = tn * G2_BN;
+  const int ks = blockIdx.z;
+  const TA* __restrict__ A = reinterpret_cast<const TA*>(g.A);
+  const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(g.W);
+  const int nkt = g.K / G2_BK;  // K % 64 == 0 (checked by the launcher)
+  const int kt_per = (nkt + g.ksplit - 1) / g.ksplit;
+  const int kt0 = ks * kt_per, kt1 = min(nkt, kt0 + kt_per);
+  // loader geometry: chunk c = tid + 256 i covers row c / ACH, 16-B segment c % ACH
+  constexpr int ACH = sizeof(TA) == 2 ? 8 : 16;  // 16-B chunks per A row of the tile
+  constexpr int AN = G2_BM * ACH / 256;           // chunks per thread (4 bf16 / 8 fp32)
+  constexpr int AROWS = 256 / ACH;                // rows covered per i step
+  const int arow0 = tid / ACH, aseg = (tid % ACH) * (16 / (int)sizeof(TA));
+  // implicit conv: (stream, frame) of this thread's first row; later rows are +AROWS frames
+  int cb0 = 0, ct0 = 0;
+  if (AMODE == A_CONV) { cb0 = (m0 + arow0) / g.L; ct0 = (m0 + arow0) - cb0 * g.L; }
+  ALoad<TA> ar0, ar1;
+  ALoad<bf16_t> br0, br1;
+#define G2_LOAD(kt, ar, br)                                                                                \
+  {                                                                                                        \
+    const int kb = (kt) * G2_BK;                                                                           \
+    _Pragma("unroll") for (int i = 0; i < AN; ++i) {                                                       \
+      /* unconditional loads from a clamped row (rows past M are never stored; conv padding is */         \
+      /* zeroed by a select): no branches, so the waitcnt of each register set stays exact */              \
+      const int m = min(m0 + arow0 + AROWS * i, g.M - 1);                                                  \
+      const TA* src;                                                                                       \
+      bool ok = true;                                                                                      \
+      if (AMODE == A_PLAIN) {                                                                              \
+        src = A + (size_t)m * g.lda + kb + aseg;                                                           \
+      } else {                                                                                             \
+        int b = cb0, t = ct0 + AROWS * i;                                                                  \
+        while (t >= g.L) { t -= g.L; ++b; }                                                                \
+        const int tap = kb / g.cin, c = kb + aseg - tap * g.cin; /* a 64-wide k-tile lies in one tap */   \
+        const int tt = t + tap - (g.taps - 1) / 2;                                                         \
+        ok = tt >= 0 && tt < g.L && b * g.L + t < g.M;                                                     \
+        src = A + ((size_t)b * g.L + min(max(tt, 0), g.L - 1)) * g.cin + c;                                \
+        if (b * g.L + t >= g.M) src = A + (size_t)m * g.cin + c;                                           \
+      }                                                                                                    \
+      g2_ld(ar.v[i], src, ok);                                                                             \
+    }                                                                                                      \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                        \
+      const int c = tid + 256 * i, r = c >> 3, seg = (c & 7) * 8;                                          \
+      const int n = min(n0 + r, g.N - 1); /* rows past N duplicate row N-1 (never stored) */              \
+      br.v[i] = *reinterpret_cast<const u32x4*>(W + (size_t)n * g.ldw + kb + seg);                         \
+    }                                                                                                      \
+  }
+#define G2_STORE(buf, ar, br)                                                                                      \
+  {                                                                                                        \
+    bf16_t* as = As[buf];                                                                                  \
+    bf16_t* bs = Bs[buf];                                                                                  \
+    _Pragma("unroll") for (int i = 0; i < AN; ++i) {                                                       \
+      g2_st(as + (arow0 + AROWS * i) * G2_LDK + aseg, ar.v[i]);                                            \
+    }                                                                                                      \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                        \
+      const int c = tid + 256 * i, r = c >> 3, seg = (c & 7) * 8;                                          \
+      *reinterpret_cast<u32x4*>(bs + r * G2_LDK + seg) = br.v[i];                                          \
+    }                                                                                                      \
+  }
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  // two k-tiles in flight: tile kt+2 is loaded into one register set while tile kt is multiplied
+  // from LDS and tile kt+1 (the other set, issued one step earlier) goes to the other LDS buffer
+#define G2_COMPUTE(buf)                                                                                    \
+  {                                                                                                        \
+    const bf16_t* as = As[buf];                                                                            \
+    const bf16_t* bs = Bs[buf];                                                                            \
+    _Pragma("unroll") for (int kk = 0; kk < G2_BK; kk += 16) {                                             \
+      bf16x8 fa[2], fb[2];                                                                                 \
+      _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                                      \
+        fa[i] = *reinterpret_cast<const bf16x8*>(as + (wm * 64 + i * 32 + (lane & 31)) * G2_LDK + kk + 8 * (lane >> 5)); \
+        fb[i] = *reinterpret_cast<const bf16x8*>(bs + (wn * 64 + i * 32 + (lane & 31)) * G2_LDK + kk + 8 * (lane >> 5)); \
+      }                                                                                                    \
+      _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                        \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                        \
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);              \
+    }                                                                                                      \
+  }
+  // Loads are issued unconditionally (tile index clamped to the last one: a few redundant loads at
+  // the end) so that no load sits under a branch: the compiler's vmcnt for "set 1 has landed" then
+  // leaves set 0's loads in flight instead of draining everything.
+  if (kt0 < kt1) {
+    const int kl = kt1 - 1;
+    G2_LOAD(kt0, ar0, br0);
+    G2_LOAD(min(kt0 + 1, kl), ar1, br1);
+    G2_STORE(0, ar0, br0);
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; kt += 2) {
+      // even step: tile kt in LDS 0, set 1 holds kt+1 (in flight), set 0 is free
+      G2_LOAD(min(kt + 2, kl), ar0, br0);
+      G2_COMPUTE(0);
+      if (kt + 1 >= kt1) break;
+      G2_STORE(1, ar1, br1);
+      __syncthreads();
+      // odd step: tile kt+1 in LDS 1, set 0 holds kt+2, set 1 is free
+      G2_LOAD(min(kt + 3, kl), ar1, br1);
+      G2_COMPUTE(1);
+      if (kt + 2 >= kt1) break;
+      G2_STORE(0, ar0, br0);
+      __syncthreads();
+    }
+  }
+#undef G2_COMPUTE
+#undef G2_LOAD
+#undef G2_STORE
+  // epilogue: acc[i][j][r] = C[row][col], col = n0 + wn*64 + j*32 + (lane & 31),
+  // row = m0 + wm*64 + i*32 + (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = n0 + wn * 64 + j * 32 + (lane & 31);
+    if (col >= g.N) continue;
+    if (g.ksplit > 1) {
+      float* P = g.ws + (size_t)ks * g.M * g.N;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (row < g.M) P[(size_t)row * g.N + col] = acc[i][j][r];
+        }
+      continue;
+    }
+    TC* C = reinterpret_cast<TC*>(g.C);
+    const float bias = (EPI != E_SCALE && g.bias) ? g.bias[col] : 0.f;
+    const float gam = (EPI == E_BIAS_GAMMA_RES) ? g.gamma[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      // residual operands first, all 16 in flight (rows clamped: loads never sit under a branch)
+      float rv[16];
+      if constexpr (EPI == E_BIAS_GAMMA_RES || EPI == E_BIAS_RES) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = min(m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), g.M - 1);
+          rv[r] = g.res[(size_t)row * g.ldr + col];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const float v = acc[i][j][r] + bias;
+        float o;
+        if constexpr (EPI == E_BIAS) o = v;
+        else if constexpr (EPI == E_BIAS_GELU) o = gelu_erf(v);
+        else if constexpr (EPI == E_BIAS_GAMMA_RES) o = rv[r] + gam * v;
+        else if constexpr (EPI == E_BIAS_RES) o = rv[r] + v;
+        else o = acc[i][j][r] * g.alpha;
+        if (row < g.M) store_out<TC>(C + (size_t)row * g.ldc + col, o);
+      }
+    }
   }
 }
 
-// weight GEMMs: bf16 weights -> bf16 MFMA; fp32 weights -> exact fp32 MFMA (parity mode)
-template <typename TW, int AMODE, int EPI>
-static void gemm_w(const GemmArgs& g, int batch, hipStream_t s) {
-  if constexpr (sizeof(TW) == 2) gemm_launch<true, bf16_t, AMODE, EPI>(g, batch, s);
-  else gemm_launch<false, float, AMODE, EPI>(g, batch, s);
+// split-K partials of gemm_bf16_kernel summed in split order, then the epilogue (output TC)
+template <int EPI, typename TC>
+__global__ __launch_bounds__(256) void gemm2_splitk_reduce(GemmArgs g) {
+  const size_t MN = (size_t)g.M * g.N;
+  for (size_t e = (size_t)blockIdx.x * 256 + threadIdx.x; e < MN; e += (size_t)gridDim.x * 256) {
+    const int row = (int)(e / g.N), col = (int)(e - (size_t)row * g.N);
+    float v = 0.f;
+    for (int ks = 0; ks < g.ksplit; ++ks) v += g.ws[(size_t)ks * MN + e];
+    const float bias = (EPI != E_SCALE && g.bias) ? g.bias[col] : 0.f;
+    const float gam = (EPI == E_BIAS_GAMMA_RES) ? g.gamma[col] : 0.f;
+    store_out<TC>(reinterpret_cast<TC*>(g.C) + (size_t)row * g.ldc + col, gemm_epi<EPI>(g, g.res, row, col, v, bias, gam));
+  }
+}
+
+int g_opt_codec_g2 = 1;       // large-M bf16 GEMM (gemm_bf16_kernel) on/off
+int g_opt_codec_xcd = 1;      // its XCD-aware tile order
+int g_opt_codec_g2_min = 1024;  // smallest M that takes it
+
+template <typename TA, int AMODE, int EPI, typename TC>
+static void gemm2_launch(GemmArgs g, hipStream_t s) {
+  const int tiles = ((g.N + G2_BN - 1) / G2_BN) * ((g.M + G2_BM - 1) / G2_BM);
+  const int nkt = g.K / G2_BK;
+  int ks = 1;
+  while (tiles * ks * 2 <= 512 && nkt / (ks * 2) >= 4 && (size_t)(ks * 2) * g.M * g.N <= g_ws_floats) ks *= 2;
+  g.ksplit = ks;
+  g.xcd_remap = g_opt_codec_xcd;
+  dim3 grid((g.N + G2_BN - 1) / G2_BN, (g.M + G2_BM - 1) / G2_BM, ks);
+  hipLaunchKernelGGL((gemm_bf16_kernel<TA, AMODE, EPI, TC>), grid, dim3(256), 0, s, g);
+  if (ks > 1) {
+    const int blocks = (int)std::min<size_t>(((size_t)g.M * g.N + 255) / 256, 2048);
+    hipLaunchKernelGGL((gemm2_splitk_reduce<EPI, TC>), dim3(blocks), dim3(256), 0, s, g);
+  }
+}
+
+
+// weight GEMMs: bf16 weights -> bf16 MFMA (gemm_bf16_kernel for large M); fp32 weights -> exact
+// fp32 MFMA (parity mode). TA / TC: activation types of the operand / output (bf16 only in bf16 mode)
+template <typename TW, typename TA, int AMODE, int EPI, typename TC = float>
+static void gemm_w(const GemmArgs& g, hipStream_t s) {
+  if constexpr (sizeof(TW) == 2) {
+    if (g_opt_codec_g2 && g.M >= g_opt_codec_g2_min) gemm2_launch<TA, AMODE, EPI, TC>(g, s);
+    else gemm_launch<true, TA, bf16_t, AMODE, EPI, TC>(g, 1, s);
+  } else {
+    static_assert(sizeof(TA) == 4 && sizeof(TC) == 4, "parity mode keeps fp32 activations");
+    gemm_launch<false, float, float, AMODE, EPI, float>(g, 1, s);
+  }
 }
 // activation x activation GEMMs (AttnBlock scores / P.V): operands are fp32 in memory
-template <typename TW, int EPI>
+template <typename TW, int EPI, typename TC = float>
 static void gemm_act(const GemmArgs& g, int batch, hipStream_t s) {
-  if constexpr (sizeof(TW) == 2) gemm_launch<true, float, A_PLAIN, EPI>(g, batch, s);
-  else gemm_launch<false, float, A_PLAIN, EPI>(g, batch, s);
+  if constexpr (sizeof(TW) == 2) gemm_launch<true, float, float, A_PLAIN, EPI, TC>(g, batch, s);
+  else gemm_launch<false, float, float, A_PLAIN, EPI, float>(g, batch, s);
 }
 
 // ---------------------------------------------------------------------------------
@@ -248,9 +510,9 @@ static void gemm_act(const GemmArgs& g, int batch, hipStream_t s) {
 // (two-pass fp32) and the transformed output in one kernel, so the following conv / 1x1 GEMM
 // reads a ready operand (decoder/models.py:15-16, 59-68, 109).
 // ---------------------------------------------------------------------------------
-template <bool SWISH>
+template <bool SWISH, typename TO>
 __global__ __launch_bounds__(256) void gn_apply_kernel(const float* __restrict__ x, int L, const float* __restrict__ gw,
-                                                       const float* __restrict__ gb, float* __restrict__ y) {
+                                                       const float* __restrict__ gb, TO* __restrict__ y) {
   __shared__ float red[4];
   const int gi = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   constexpr int CG = CD / GN_G;  // 24 channels
@@ -273,7 +535,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const float* __restrict__
     const int t = e / CG, c = e - t * CG, ch = gi * CG + c;
     float v = (x[off + (size_t)t * CD + c] - mean) * rstd * gw[ch] + gb[ch];
     if (SWISH) v = swishf(v);
-    y[off + (size_t)t * CD + c] = v;
+    store_out<TO>(y + off + (size_t)t * CD + c, v);
   }
 }
 
@@ -341,9 +603,10 @@ __global__ __launch_bounds__(256) void gn_adaln_kernel(const float* __restrict__
 }
 
 // ConvNeXt prologue (modules.py:45-50): depthwise conv k7 pad 3 (+bias) then AdaLN
+template <typename TO>
 __global__ __launch_bounds__(256) void dwconv_adaln_kernel(const float* __restrict__ x, int L, const float* __restrict__ dw,
                                                            const float* __restrict__ dwb, const float* __restrict__ scale,
-                                                           const float* __restrict__ shift, float* __restrict__ y) {
+                                                           const float* __restrict__ shift, TO* __restrict__ y) {
   __shared__ float red[4];
   const int m = blockIdx.x, tid = threadIdx.x, b = m / L, t = m - b * L;
   float v[3];
@@ -362,13 +625,14 @@ __global__ __launch_bounds__(256) void dwconv_adaln_kernel(const float* __restri
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int c = tid + 256 * j;
-    y[(size_t)m * CD + c] = v[j] * scale[c] + shift[c];
+    store_out<TO>(y + (size_t)m * CD + c, v[j] * scale[c] + shift[c]);
   }
 }
 
 // final_layer_norm (affine, eps 1e-6)
+template <typename TO>
 __global__ __launch_bounds__(256) void ln_affine_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                        const float* __restrict__ bb, float* __restrict__ y) {
+                                                        const float* __restrict__ bb, TO* __restrict__ y) {
   __shared__ float red[4];
   const int m = blockIdx.x, tid = threadIdx.x;
   float v[3];
@@ -378,12 +642,13 @@ __global__ __launch_bounds__(256) void ln_affine_kernel(const float* __restrict_
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int c = tid + 256 * j;
-    y[(size_t)m * CD + c] = v[j] * w[c] + bb[c];
+    store_out<TO>(y + (size_t)m * CD + c, v[j] * w[c] + bb[c]);
   }
 }
 
 // features [B][512][L] -> [B*L][512]
-__global__ void feats_transpose_kernel(const float* __restrict__ f, int L, float* __restrict__ out) {
+template <typename TO>
+__global__ void feats_transpose_kernel(const float* __restrict__ f, int L, TO* __restrict__ out) {
   __shared__ float tile[32][33];
   const int b = blockIdx.z, c0 = blockIdx.y * 32, t0 = blockIdx.x * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
@@ -394,7 +659,7 @@ __global__ void feats_transpose_kernel(const float* __restrict__ f, int L, float
   __syncthreads();
   for (int i = ty; i < 32; i += 8) {
     const int t = t0 + i, c = c0 + tx;
-    if (t < L) out[((size_t)b * L + t) * CIN + c] = tile[tx][i];
+    if (t < L) store_out<TO>(out + ((size_t)b * L + t) * CIN + c, tile[tx][i]);
   }
 }
 
@@ -404,6 +669,16 @@ __global__ void codes_gather_kernel(const float* __restrict__ cb, const int32_t*
   const int code = min(max(codes[m], 0), 4095);
   const float4 v = reinterpret_cast<const float4*>(cb + (size_t)code * CIN)[threadIdx.x];
   reinterpret_cast<float4*>(out + (size_t)m * CIN)[threadIdx.x] = v;
+}
+// bf16 mode: the rows as the embed conv's bf16 operand
+__global__ void codes_gather_bf16_kernel(const float* __restrict__ cb, const int32_t* __restrict__ codes,
+                                         bf16_t* __restrict__ out) {
+  const int m = blockIdx.x;
+  const int code = min(max(codes[m], 0), 4095);
+  const float4 v = reinterpret_cast<const float4*>(cb + (size_t)code * CIN)[threadIdx.x];
+  reinterpret_cast<uint2*>(out + (size_t)m * CIN)[threadIdx.x] =
+      make_uint2((uint32_t)f32_to_bf16(v.x) | ((uint32_t)f32_to_bf16(v.y) << 16),
+                 (uint32_t)f32_to_bf16(v.z) | ((uint32_t)f32_to_bf16(v.w) << 16));
 }
 
 // v rows of qkv [B*L][2304] (cols 1536..2303) -> Vt [B][768][ldv]
@@ -573,44 +848,54 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
   float* x = sc.x;
   float* t1 = sc.t1;
   float* t2 = sc.t2;
+  // operands that only feed a weight GEMM are stored in the GEMM's input precision (bf16 in bf16
+  // mode: the GEMM would round them on the way into LDS anyway, so results are unchanged)
+  typedef TW TAct;
+  TAct* gn = reinterpret_cast<TAct*>(sc.gn);  // [M][768] normalised operand of the next conv / 1x1
+  TAct* t2a = reinterpret_cast<TAct*>(t2);    // dwconv+AdaLN / final LN output (pwconv1 / head operand)
+  TAct* t1a = reinterpret_cast<TAct*>(t1);    // GELU(pwconv1) (pwconv2 operand)
   // a3: features, time-major [M][512]
-  if (codes) hipLaunchKernelGGL(codes_gather_kernel, dim3(M), dim3(CIN / 4), 0, s, w.codebook, codes, sc.feats);
-  else hipLaunchKernelGGL(feats_transpose_kernel, dim3((L + 31) / 32, CIN / 32, B), dim3(256), 0, s, feats_in, L, sc.feats);
+  TAct* feats = reinterpret_cast<TAct*>(sc.feats);
+  if (codes) {
+    if constexpr (sizeof(TAct) == 2) hipLaunchKernelGGL(codes_gather_bf16_kernel, dim3(M), dim3(CIN / 4), 0, s, w.codebook, codes, feats);
+    else hipLaunchKernelGGL(codes_gather_kernel, dim3(M), dim3(CIN / 4), 0, s, w.codebook, codes, feats);
+  } else {
+    hipLaunchKernelGGL(feats_transpose_kernel<TAct>, dim3((L + 31) / 32, CIN / 32, B), dim3(256), 0, s, feats_in, L, feats);
+  }
 
-  float* gn = sc.gn;  // [M][768] normalised operand of the next conv / 1x1
   g_ws_floats = sc.ws_floats;
   GemmArgs g{};
   g.ws = sc.ws;
   g.L = L;
   g.M = M;
   // embed Conv1d(512->768, k7, pad 3)
-  g.A = sc.feats; g.lda = CIN; g.cin = CIN; g.taps = 7;
+  g.A = feats; g.lda = CIN; g.cin = CIN; g.taps = 7;
   g.W = w.embed_w; g.ldw = 7 * CIN; g.K = 7 * CIN; g.N = CD;
   g.C = x; g.ldc = CD; g.bias = w.embed_b;
-  gemm_w<TW, A_CONV, E_BIAS>(g, 1, s);
+  gemm_w<TW, TAct, A_CONV, E_BIAS>(g, s);
 
   auto resnet = [&](int i) {  // models.py:58-78
-    hipLaunchKernelGGL((gn_apply_kernel<true>), dim3(GN_G, B), dim3(256), 0, s, x, L, w.rn_n1w[i], w.rn_n1b[i], gn);
+    hipLaunchKernelGGL((gn_apply_kernel<true, TAct>), dim3(GN_G, B), dim3(256), 0, s, x, L, w.rn_n1w[i], w.rn_n1b[i], gn);
     GemmArgs c{};
     c.ws = sc.ws;
     c.L = L; c.M = M; c.cin = CD; c.taps = 3; c.K = 3 * CD; c.N = CD; c.ldw = 3 * CD;
     c.A = gn; c.lda = CD;
     c.W = w.rn_c1w[i]; c.bias = w.rn_c1b[i]; c.C = t1; c.ldc = CD;
-    gemm_w<TW, A_CONV, E_BIAS>(c, 1, s);
-    hipLaunchKernelGGL((gn_apply_kernel<true>), dim3(GN_G, B), dim3(256), 0, s, t1, L, w.rn_n2w[i], w.rn_n2b[i], gn);
+    gemm_w<TW, TAct, A_CONV, E_BIAS>(c, s);
+    hipLaunchKernelGGL((gn_apply_kernel<true, TAct>), dim3(GN_G, B), dim3(256), 0, s, t1, L, w.rn_n2w[i], w.rn_n2b[i], gn);
     c.W = w.rn_c2w[i]; c.bias = w.rn_c2b[i]; c.C = x; c.res = x; c.ldr = CD;
-    gemm_w<TW, A_CONV, E_BIAS_RES>(c, 1, s);
+    gemm_w<TW, TAct, A_CONV, E_BIAS_RES>(c, s);
   };
   resnet(0);
   resnet(1);
   {  // AttnBlock (models.py:107-127)
-    hipLaunchKernelGGL((gn_apply_kernel<false>), dim3(GN_G, B), dim3(256), 0, s, x, L, w.at_nw, w.at_nb, gn);
+    hipLaunchKernelGGL((gn_apply_kernel<false, TAct>), dim3(GN_G, B), dim3(256), 0, s, x, L, w.at_nw, w.at_nb, gn);
     GemmArgs c{};
     c.ws = sc.ws;
     c.L = L; c.M = M; c.K = CD; c.N = 3 * CD; c.ldw = CD;
     c.A = gn; c.lda = CD;
     c.W = w.at_qkv_w; c.bias = w.at_qkv_b; c.C = t1; c.ldc = CFF;
-    gemm_w<TW, A_PLAIN, E_BIAS>(c, 1, s);
+    gemm_w<TW, TAct, A_PLAIN, E_BIAS>(c, s);
     const int ldS = (L + 3) & ~3;
     float* S = sc.att;            // [B][L][ldS]
     float* Vt = t2;               // [B][768][ldS]
@@ -631,15 +916,19 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
     p.M = L; p.N = CD; p.K = L; p.L = L;
     p.A = S; p.lda = ldS; p.sA = (long long)L * ldS;
     p.W = Vt; p.ldw = ldS; p.sW = (long long)CD * ldS;
-    p.C = t1; p.ldc = CFF; p.sC = (long long)L * CFF;  // h overwrites the (consumed) q columns
-    gemm_act<TW, E_BIAS>(p, B, s);
+    if constexpr (sizeof(TAct) == 2) {  // h (bf16) into gn: it only feeds proj_out
+      p.C = gn; p.ldc = CD; p.sC = (long long)L * CD;
+    } else {  // h overwrites the (consumed) q columns
+      p.C = t1; p.ldc = CFF; p.sC = (long long)L * CFF;
+    }
+    gemm_act<TW, E_BIAS, TAct>(p, B, s);
     // proj_out + residual
     GemmArgs o{};
     o.ws = sc.ws;
     o.M = M; o.N = CD; o.K = CD; o.L = L;
-    o.A = t1; o.lda = CFF; o.W = w.at_proj_w; o.ldw = CD; o.bias = w.at_proj_b;
+    o.A = p.C; o.lda = p.ldc; o.W = w.at_proj_w; o.ldw = CD; o.bias = w.at_proj_b;
     o.C = x; o.ldc = CD; o.res = x; o.ldr = CD;
-    gemm_w<TW, A_PLAIN, E_BIAS_RES>(o, 1, s);
+    gemm_w<TW, TAct, A_PLAIN, E_BIAS_RES>(o, s);
   }
   resnet(2);
   resnet(3);
@@ -648,27 +937,27 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
   hipLaunchKernelGGL(gn_adaln_kernel, dim3(M), dim3(256), 0, s, x, L, sc.stats, w.pn_w, w.pn_b,
                      w.ada_scale + (size_t)bw * CD, w.ada_shift + (size_t)bw * CD, x);
   for (int i = 0; i < 12; ++i) {  // ConvNeXt blocks (modules.py:43-60)
-    hipLaunchKernelGGL(dwconv_adaln_kernel, dim3(M), dim3(256), 0, s, x, L, w.dw_w[i], w.dw_b[i],
-                       w.cn_scale[i] + (size_t)bw * CD, w.cn_shift[i] + (size_t)bw * CD, t2);
+    hipLaunchKernelGGL(dwconv_adaln_kernel<TAct>, dim3(M), dim3(256), 0, s, x, L, w.dw_w[i], w.dw_b[i],
+                       w.cn_scale[i] + (size_t)bw * CD, w.cn_shift[i] + (size_t)bw * CD, t2a);
     GemmArgs c{};
     c.ws = sc.ws;
     c.M = M; c.L = L; c.N = CFF; c.K = CD; c.ldw = CD;
-    c.A = t2; c.lda = CD; c.W = w.pw1_w[i]; c.bias = w.pw1_b[i]; c.C = t1; c.ldc = CFF;
-    gemm_w<TW, A_PLAIN, E_BIAS_GELU>(c, 1, s);
+    c.A = t2a; c.lda = CD; c.W = w.pw1_w[i]; c.bias = w.pw1_b[i]; c.C = t1a; c.ldc = CFF;
+    gemm_w<TW, TAct, A_PLAIN, E_BIAS_GELU, TAct>(c, s);
     GemmArgs d{};
     d.ws = sc.ws;
     d.M = M; d.L = L; d.N = CD; d.K = CFF; d.ldw = CFF;
-    d.A = t1; d.lda = CFF; d.W = w.pw2_w[i]; d.bias = w.pw2_b[i]; d.gamma = w.gamma[i];
+    d.A = t1a; d.lda = CFF; d.W = w.pw2_w[i]; d.bias = w.pw2_b[i]; d.gamma = w.gamma[i];
     d.C = x; d.ldc = CD; d.res = x; d.ldr = CD;
-    gemm_w<TW, A_PLAIN, E_BIAS_GAMMA_RES>(d, 1, s);
+    gemm_w<TW, TAct, A_PLAIN, E_BIAS_GAMMA_RES>(d, s);
   }
-  hipLaunchKernelGGL(ln_affine_kernel, dim3(M), dim3(256), 0, s, x, w.fln_w, w.fln_b, t2);
+  hipLaunchKernelGGL(ln_affine_kernel<TAct>, dim3(M), dim3(256), 0, s, x, w.fln_w, w.fln_b, t2a);
   {  // ISTFTHead.out Linear(768 -> 1282)
     GemmArgs h{};
     h.ws = sc.ws;
     h.M = M; h.L = L; h.N = 2 * NB; h.K = CD; h.ldw = CD;
-    h.A = t2; h.lda = CD; h.W = w.head_w; h.bias = w.head_b; h.C = sc.spec; h.ldc = 2 * NB;
-    gemm_w<TW, A_PLAIN, E_BIAS>(h, 1, s);
+    h.A = t2a; h.lda = CD; h.W = w.head_w; h.bias = w.head_b; h.C = sc.spec; h.ldc = 2 * NB;
+    gemm_w<TW, TAct, A_PLAIN, E_BIAS>(h, s);
   }
   hipLaunchKernelGGL(istft_frames_kernel, dim3(M), dim3(256), 0, s, sc.spec,
                      reinterpret_cast<const float2*>(w.twiddle), w.window, sc.frames);

@@ -12,16 +12,17 @@ typedef uint8_t fp8_t;    // raw OCP e4m3fn bits (KV cache)
 __device__ __forceinline__ float bf16_to_f32(bf16_t h) {
   return __uint_as_float(((uint32_t)h) << 16);
 }
-// round-to-nearest-even; NaN stays NaN (quiet)
+// round-to-nearest-even; NaN stays NaN (quiet). On the device this is gfx950's v_cvt_pk_bf16_f32
+// (same rounding, branch-free); the host form is the bit-exact software equivalent.
 __host__ __device__ __forceinline__ bf16_t f32_to_bf16(float f) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  uint32_t u = __float_as_uint(f);
+  return __builtin_bit_cast(bf16_t, (__bf16)f);
 #else
   uint32_t u; __builtin_memcpy(&u, &f, 4);
-#endif
   if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (bf16_t)((u >> 16) | 0x40);
   u += 0x7fffu + ((u >> 16) & 1u);
   return (bf16_t)(u >> 16);
+#endif
 }
 
 // f32 -> e4m3fn, round to nearest even, saturated to the finite range (+-448)

@@ -1,0 +1,77 @@
+"""Codec decode in bf16 mode (bf16 weights and bf16 GEMM operands, fp32 accumulation and fp32
+residual stream). No bit-exactness claim against the fp32 reference; the bar is a relative RMS
+error of the waveform, measured against the fp32 parity-mode engine (itself pinned to the
+reference's golden PCM by test_gpu_parity.py) and against the golden PCM directly. The large-M
+GEMM (gemm_bf16_kernel, 128x128 tiles) and the small-M GEMM must agree to bf16 summation-order
+noise.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def engs():
+    from llmvox_amd.engine import build_engine
+    e16 = build_engine(0, "bf16", "bf16", max_streams=2, max_positions=64, max_codec_frames=4096)
+    e32 = build_engine(0, "fp32", "fp32", max_streams=2, max_positions=64, max_codec_frames=4096)
+    yield e16, e32
+    e16.close()
+    e32.close()
+
+
+def _rel_rms(a, b):
+    a = a.astype(np.float64)
+    b = b.astype(np.float64)
+    return float(np.sqrt(np.mean((a - b) ** 2)) / np.sqrt(np.mean(b ** 2)))
+
+
+@pytest.mark.parametrize("L", [10, 90])
+def test_bf16_decode_close_to_golden(engs, L):
+    e16, _ = engs
+    c = np.load(os.path.join(GOLDEN, "codec_golden.npz"))
+    codes = torch.from_numpy(c[f"codes_{L}"]).to(e16.device)
+    pcm = e16.decode_codes(codes).cpu().numpy()
+    assert _rel_rms(pcm, c[f"pcm_{L}"]) < 0.02
+
+
+@pytest.mark.parametrize("S,L", [(8, 256), (16, 128), (3, 700)])
+def test_bf16_large_m_close_to_fp32(engs, S, L):
+    e16, e32 = engs
+    g = torch.Generator().manual_seed(S * 1000 + L)
+    codes = torch.randint(0, 4096, (S, L), generator=g).to(e16.device)
+    p16 = e16.decode_codes(codes).cpu().numpy()
+    p32 = e32.decode_codes(codes).cpu().numpy()
+    for b in range(S):
+        assert _rel_rms(p16[b], p32[b]) < 0.02, b
+
+
+def test_large_m_gemm_agrees_with_small_m_gemm(engs):
+    e16, _ = engs
+    g = torch.Generator().manual_seed(5)
+    codes = torch.randint(0, 4096, (8, 256), generator=g).to(e16.device)
+    big = e16.decode_codes(codes).cpu().numpy()
+    e16.set_option("codec_g2", 0)
+    try:
+        small = e16.decode_codes(codes).cpu().numpy()
+    finally:
+        e16.set_option("codec_g2", 1)
+    assert _rel_rms(big, small) < 5e-3
+
+
+def test_bf16_streams_independent(engs):
+    """a stream decoded inside a batch == the same stream decoded in a batch of other content
+    (same M, so the same kernels and split-K choices): bit-equal"""
+    e16, _ = engs
+    g = torch.Generator().manual_seed(9)
+    codes = torch.randint(0, 4096, (6, 200), generator=g).to(e16.device)
+    a = e16.decode_codes(codes).cpu().numpy()
+    perm = [3, 0, 5, 1, 4, 2]
+    b = e16.decode_codes(codes[perm]).cpu().numpy()
+    for i, p in enumerate(perm):
+        np.testing.assert_array_equal(b[i], a[p])
