@@ -13,6 +13,14 @@ Multi-GPU (--gpus N under torch.distributed.run): one process per GPU, each runn
 stream(s) (independent utterance streams: weak scaling); rank 0 scatters the text-id plans
 and gathers the PCM over RCCL (the path's only exchange, BASELINE north_star).
 
+--config selects the other BASELINE.json workloads (per GPU; weak scaling over --gpus):
+  2  32 streams batched, 256-token chunks (configs[2])
+  3  the service path: FusedScheduler replica streams (replica index = stream % 2, initial dump
+     10 / 160, x3 growth to 1280) over one utterance of --utt-tokens 2048 per step; every dump is
+     decoded as its own codec call and delivered as f32le bytes on the host (configs[3])
+  4  8 streams, fp8 (e4m3fn) KV cache + fp8 codec weights, KV reset every --reset-every chunks
+     (a new sentence), 256-token chunks (configs[4])
+
 Prints ONE JSON line (rank 0).
 """
 from __future__ import annotations
@@ -116,7 +124,18 @@ def probe_kernels(eng, slots, t, wbytes, kvbytes, iters=200):
 
 
 # ---------------------------------------------------------------------------------------
-def cpu_baseline(n_chunks, chunk, min_seconds=10.0, max_seconds=30.0):
+def dump_schedule(n_tokens, first, max_dump=1280):
+    """The reference's dump sizes (streaming_server.py:357-422): first, x3 growth capped at
+    max_dump, the remainder flushed at the end of the utterance."""
+    out, ds, left = [], first, n_tokens
+    while left > 0:
+        out.append(min(ds, left))
+        left -= out[-1]
+        ds = min(ds * 3, max_dump)
+    return out
+
+
+def cpu_baseline(n_chunks, chunk, min_seconds=10.0, max_seconds=30.0, schedule=None):
     """The reference CPU eager path (oracle restatement: fp32, B=1, O(t) history/KV cats),
     on this host's cores, on the same chunked workload; whole utterances are repeated until
     at least ``min_seconds`` of CPU work is timed (bounded by ``max_seconds``)."""
@@ -129,15 +148,17 @@ def cpu_baseline(n_chunks, chunk, min_seconds=10.0, max_seconds=30.0):
     table = torch.from_numpy(tt)
     cb = Wc[R.CODEBOOK_KEY]
     ids = sentence_ids(SENTENCE)
+    schedule = schedule or [chunk] * n_chunks
+    starts = np.concatenate([[0], np.cumsum(schedule)]).astype(int).tolist()
     t0 = time.perf_counter()
     done, passes = 0, 0
     with torch.inference_mode():
         while time.perf_counter() - t0 < min_seconds:
             hist, kv, prev = None, None, None
             passes += 1
-            for c in range(n_chunks):
+            for c in range(len(schedule)):
                 toks = []
-                for i in range(c * chunk, (c + 1) * chunk):
+                for i in range(starts[c], starts[c + 1]):
                     tid = ids[i] if i < len(ids) else 384
                     te = table[tid].view(1, 1, -1)
                     se = torch.zeros(1, 1, 512) if i == 0 else cb[prev].view(1, 1, -1)
@@ -148,7 +169,7 @@ def cpu_baseline(n_chunks, chunk, min_seconds=10.0, max_seconds=30.0):
                     toks.append(prev)
                 pcm = R.decode_codes(Wc, torch.tensor([toks]))
                 _ = pcm.numpy().astype("float32").tobytes()
-                done += chunk
+                done += len(toks)
                 if time.perf_counter() - t0 > max_seconds:
                     break
             if time.perf_counter() - t0 > max_seconds:
@@ -164,8 +185,121 @@ def cpu_baseline(n_chunks, chunk, min_seconds=10.0, max_seconds=30.0):
     except OSError:
         pass
     return {"value": done / dt, "unit": "speech tokens/s", "cores": threads, "kind": "port",
-            "sample": f"{done} tokens = {done // chunk} x ({chunk} fp32 AR steps + codec decode of {chunk} "
-                      f"frames) over {passes} utterance(s) of {n_chunks * chunk} positions, 1 stream, oracle/reference_cpu.py, {dt:.1f} s on {cpu}"}
+            "sample": f"{done} tokens: fp32 AR steps + one codec decode per dump of {schedule[:8]} tokens, "
+                      f"over {passes} utterance(s) of {sum(schedule)} positions, 1 stream, oracle/reference_cpu.py, "
+                      f"{dt:.1f} s on {cpu}"}
+
+
+# ---------------------------------------------------------------------------------------
+def run_config3(args, eng, world, rank, local, dist):
+    """configs[3]: the service path. Every GPU runs --streams replica streams through
+    FusedScheduler (streaming.py: the reference's audio_generator_sync semantics, continuous
+    batching, one HIP-graph replay per decode step, one codec call per dump, f32le bytes on the
+    host). Stream g uses replica index g % 2 (initial dump 10 / 160, x3 to 1280,
+    streaming_server.py:357-422). One step = one utterance of --utt-tokens tokens per stream; the
+    utterance's tail below the dump size is flushed (the reference flushes it at end-of-audio)."""
+    from llmvox_amd.streaming import FusedScheduler
+    dev = eng.device
+    S, N, K, Wm = args.streams, args.utt_tokens, args.steps, args.warmup
+    sched = FusedScheduler(eng, max_chunk=256, to_bytes=True)
+    rng = np.random.default_rng(1234 + rank)
+
+    def utterance():
+        streams = []
+        for s in range(S):
+            g = rank * S + s
+            st = sched.open_stream(index=g % 2, dump_size=10 if g % 2 == 0 else 160)
+            for w in (SENTENCE if g == 0 else random_sentence(rng)).split(" "):
+                st.feed(w)
+            streams.append(st)
+        t0 = time.perf_counter()
+        first = None
+        while min(len(st.tokens) for st in streams) < N:
+            if sched.run_chunk() == 0:
+                raise RuntimeError("scheduler went idle before the utterance ended")
+            if first is None and any(st.events for st in streams):
+                first = (time.perf_counter() - t0) * 1e3
+        sched.flush()
+        rest = []  # the tail below the current dump size: flushed as one last dump (end of audio)
+        for st in streams:
+            if st.m.speech_outputs:
+                rest.append(st.m.speech_outputs)
+                st.m.speech_outputs = []
+        if rest:
+            for L in sorted({len(r) for r in rest}):
+                grp = [r for r in rest if len(r) == L]
+                codes = torch.tensor(grp, dtype=torch.int32, device=dev)
+                for row in eng.decode_codes(codes).cpu().numpy():
+                    _ = row.astype("float32").tobytes()
+        n_tok = sum(len(st.tokens) for st in streams)
+        for st in streams:
+            sched.close_stream(st)
+        return n_tok, first
+
+    for _ in range(Wm):
+        utterance()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    toks, firsts = 0, []
+    for _ in range(K):
+        n, f = utterance()
+        toks += n
+        firsts.append(f)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    eng.check_errors()
+    if dist is not None:
+        tt = torch.tensor([dt, toks], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
+        dt, toks = float(tt[0].item()), int(tt[1].item())
+    value = toks / dt
+
+    kern, rl = None, None
+    if not args.no_probe:
+        slots = torch.arange(S, dtype=torch.int32, device=dev)
+        for s in range(S):
+            eng.set_slot(s, N - 1, 0)
+        wb = 2 if args.dtype == "bf16" else 4
+        kb = {"bf16": 2, "fp8": 1, "fp32": 4}[args.kv_dtype or args.dtype]
+        kern = probe_kernels(eng, slots, N, wb, kb)
+        dom = max(kern.values(), key=lambda r: r["share_us_per_step"])
+        rl = {"bound": "hbm", "kernel": dom["name"], "achieved": round(dom["gbs"], 1), "peak": HBM_PEAK_GBS,
+              "unit": "GB/s", "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4), "traffic": None,
+              "bytes_per_launch": dom["bytes"], "avg_us": round(dom["avg_us"], 3), "kv_positions": N}
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(0, 0, schedule=dump_schedule(N, 10))
+    if rank == 0:
+        out = {
+            "metric": "speech tokens/sec (+ 24kHz audio samples/sec = 320 x tokens/s; p50 first-chunk latency)",
+            "value": round(value, 1), "unit": "speech tokens/s", "n_gpus": world, "steps": K, "warmup": Wm,
+            "ms_per_step": round(dt / K * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic (config sentence + seeded random sentences -> ByT5 ids, seeded synthetic weights)",
+            "config": {"workload": f"configs[3]: FusedScheduler service path, {S} replica stream(s)/GPU "
+                                   f"(initial dump 10/160, x3 to 1280), {N} tokens per utterance, "
+                                   "one codec call per dump, f32le bytes on the host",
+                       "streams_per_gpu": S, "utterance_tokens": N, "dump_schedule_replica0": dump_schedule(N, 10),
+                       "dump_schedule_replica1": dump_schedule(N, 160),
+                       "parallelism": f"streams sharded over {world} GPU(s)"},
+            "audio_samples_per_s": round(320 * value, 1),
+            "realtime_factor_per_stream": round(value / (world * S) / 75.0, 1),
+            "p50_first_chunk_latency_ms": round(statistics.median(firsts), 3),
+            "roofline": rl, "kv_dtype": args.kv_dtype or args.dtype,
+            "codec_weights": args.codec_dtype or args.dtype, "cpu_baseline": cpu,
+            "kernels": {v["name"]: {"avg_us": round(v["avg_us"], 2), "GB/s": round(v["gbs"], 1)}
+                        for v in kern.values()} if kern else None,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 # ---------------------------------------------------------------------------------------
@@ -187,7 +321,20 @@ def main():
                     help="run the codec on a second HIP stream beside the next chunk's AR (measured slower)")
     ap.add_argument("--no-graphs", action="store_true",
                     help="launch the decode step kernel by kernel (for rocprofv3 --pmc passes)")
+    ap.add_argument("--config", type=int, default=1, choices=[1, 2, 3, 4],
+                    help="BASELINE.json workload (1: default; 2: 32 streams; 3: scheduler replicas; 4: fp8)")
+    ap.add_argument("--codec-dtype", default=None, choices=["fp8"], help="fp8 codec weights (configs[4])")
+    ap.add_argument("--utt-tokens", type=int, default=2048, help="configs[3]: tokens per utterance (one step)")
+    ap.add_argument("--reset-every", type=int, default=4,
+                    help="configs[4]: chunks per sentence (KV reset at every sentence start)")
     args = ap.parse_args()
+    if args.config == 2 and args.streams == 1:
+        args.streams = 32
+    if args.config == 4:
+        if args.streams == 1:
+            args.streams = 8
+        args.kv_dtype = args.kv_dtype or "fp8"
+        args.codec_dtype = args.codec_dtype or "fp8"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -204,11 +351,14 @@ def main():
         raise SystemExit("steps * chunk must stay within block_size 8192 positions")
     kvd = args.kv_dtype or args.dtype
     eng = build_engine(local, args.dtype, kvd, max_streams=max(S, 1), max_positions=8192,
-                       max_codec_frames=S * chunk)
+                       max_codec_frames=max(S * chunk, 1280 * S if args.config == 3 else 0),
+                       codec_dtype=args.codec_dtype)
     dev = eng.device
     torch.cuda.set_device(dev)
     if args.no_graphs:
         eng.set_graphs(False)
+    if args.config == 3:
+        return run_config3(args, eng, world, rank, local, dist)
 
     # ---- text plans: stream 0 of rank 0 speaks the config sentence; others seeded sentences
     n_pos = max(K, Wm) * chunk
@@ -239,11 +389,19 @@ def main():
     ev_ar = [torch.cuda.Event(), torch.cuda.Event()]
     ev_codec = [torch.cuda.Event(), torch.cuda.Event()]
 
+    reset_every = args.reset_every if args.config == 4 else 0
+
     def run_chunk(c):
         i = c & 1
         main = torch.cuda.current_stream(dev)
         main.wait_event(ev_codec[i])  # tok_bufs[i] is free again (its decode has read it)
-        text_plan.copy_(mine[:, c * chunk:(c + 1) * chunk])
+        cc = c
+        if reset_every:  # configs[4]: a new sentence every reset_every chunks, KV reset per sentence
+            cc = c % reset_every
+            if cc == 0:
+                for s_ in range(S):
+                    eng.reset_slot(s_)
+        text_plan.copy_(mine[:, cc * chunk:(cc + 1) * chunk])
         rowstep.zero_()
         eng.ar_steps(chunk, slots, text_plan, rowstep, tok_bufs[i])
         ev_ar[i].record(main)
@@ -321,7 +479,7 @@ def main():
     rl, kern = None, None
     if not args.no_probe:
         reset_all()
-        ppos = args.probe_pos or K * chunk
+        ppos = args.probe_pos or (min(K, reset_every) if reset_every else K) * chunk
         for s in range(S):
             eng.set_slot(s, ppos - 1, 0)
         wb = 2 if args.dtype == "bf16" else 4
@@ -379,8 +537,9 @@ def main():
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic (config 64-char sentence -> ByT5 ids, seeded synthetic weights at reference init scales)",
-            "config": {"workload": f"configs[{1 if S == 1 else 2}]: 30M LLMVoX {args.dtype}, {S} stream(s)/GPU, "
-                                   f"{chunk}-token chunk, greedy AR + WavTokenizer decode + PCM to host",
+            "config": {"workload": f"configs[{args.config if args.config != 1 or S == 1 else 2}]: 30M LLMVoX {args.dtype}, "
+                                   f"{S} stream(s)/GPU, {chunk}-token chunk, greedy AR + WavTokenizer decode + PCM to host"
+                                   + (f", fp8 KV + fp8 codec weights, KV reset every {reset_every} chunks" if reset_every else ""),
                        "streams_per_gpu": S, "chunk_tokens": chunk, "positions": K * chunk,
                        "parallelism": f"streams sharded over {world} GPU(s), RCCL scatter text / gather PCM"},
             "audio_samples_per_s": round(320 * value, 1),
@@ -389,6 +548,7 @@ def main():
             "roofline": rl,
             "codec_roofline": codec,
             "kv_dtype": kvd,
+            "codec_weights": args.codec_dtype or args.dtype,
             "cpu_baseline": cpu,
             "kernels": {v["name"]: {"avg_us": round(v["avg_us"], 2), "GB/s": round(v["gbs"], 1)}
                         for v in kern.values()} if kern else None,

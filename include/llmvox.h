@@ -38,7 +38,8 @@ extern "C" {
 
 #define LVX_DTYPE_F32 0
 #define LVX_DTYPE_BF16 1
-#define LVX_DTYPE_FP8 2 /* kv_dtype only: OCP e4m3fn (the gfx950 format), saturating at +-448, unscaled */
+#define LVX_DTYPE_FP8 2 /* kv_dtype: OCP e4m3fn (the gfx950 format), saturating at +-448, unscaled;
+                           codec_dtype: e4m3fn codec GEMM weights with one fp32 scale per output row */
 
 typedef struct lvx_ctx lvx_ctx;
 
@@ -49,6 +50,8 @@ typedef struct {
   int max_streams;      /* KV slots (concurrent utterance streams) */
   int max_positions;    /* per-slot KV capacity, <= 8192 (GPTConfig.block_size) */
   int max_codec_frames; /* max sum over streams of frames per codec call */
+  int codec_dtype;      /* codec conv / linear weight storage: 0 = weight_dtype, or LVX_DTYPE_FP8 (needs
+                           weight_dtype BF16: fp8 weights, bf16 operands, fp32 accumulation) */
 } lvx_config;
 
 /* ---- lifetime ----------------------------------------------------------- */

@@ -32,7 +32,7 @@ DTYPES = {"fp32": LVX_DTYPE_F32, "f32": LVX_DTYPE_F32, "float32": LVX_DTYPE_F32,
 class LvxConfig(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("weight_dtype", ctypes.c_int), ("kv_dtype", ctypes.c_int),
                 ("max_streams", ctypes.c_int), ("max_positions", ctypes.c_int),
-                ("max_codec_frames", ctypes.c_int)]
+                ("max_codec_frames", ctypes.c_int), ("codec_dtype", ctypes.c_int)]
 
 
 class LvxError(RuntimeError):

@@ -39,6 +39,7 @@ struct GemmArgs {
   float alpha;
   int ksplit;                // >1: deterministic split-K through the fp32 workspace `ws`
   int xcd_remap;             // gemm_bf16_kernel: XCD-aware tile order (option codec_xcd)
+  const float* wscale;       // fp8 weights: per-output-column scale (w = q * s), else null
   float* ws;
 };
 
@@ -91,6 +92,7 @@ constexpr int LDF = BK + 1;  // fp32 LDS row (conflict-free b32 column reads)
 constexpr int LDH = BK + 8;  // bf16 LDS row (80 B)
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2n __attribute__((ext_vector_type(2)));
 typedef float f32x4n __attribute__((ext_vector_type(4)));
 // one 16-B A chunk from global, replaced by zeros when !ok (conv padding) with a select
 __device__ __forceinline__ void g2_ld(u32x4& v, const bf16_t* src, bool ok) {
@@ -268,6 +270,29 @@ static void gemm_launch(GemmArgs g, int batch, hipStream_t s) {
 // ---------------------------------------------------------------------------------
 constexpr int G2_BM = 128, G2_BN = 128, G2_BK = 64, G2_LDK = G2_BK + 8;  // bf16 row stride 144 B
 
+template <typename TB> struct BLoad;
+template <> struct BLoad<bf16_t> {  // 4 x 8 bf16 per thread per tile
+  u32x4 v[4];
+};
+template <> struct BLoad<fp8_t> {  // 4 x 8 e4m3 per thread per tile
+  u32x2n v[4];
+};
+// 8 weights into the bf16 LDS tile: as they are, or e4m3 -> bf16 (exact: 3 mantissa bits fit)
+__device__ __forceinline__ void g2_stb(bf16_t* d, u32x4 v) { *reinterpret_cast<u32x4*>(d) = v; }
+__device__ __forceinline__ void g2_stb(bf16_t* d, u32x2n v) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  u32x4 o;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const f2 a = __builtin_amdgcn_cvt_pk_f32_fp8(v[h], false), b = __builtin_amdgcn_cvt_pk_f32_fp8(v[h], true);
+    o[2 * h] = (__float_as_uint(a.x) >> 16) | (__float_as_uint(a.y) & 0xffff0000u);
+    o[2 * h + 1] = (__float_as_uint(b.x) >> 16) | (__float_as_uint(b.y) & 0xffff0000u);
+  }
+  *reinterpret_cast<u32x4*>(d) = o;
+}
+__device__ __forceinline__ void g2_ldb(u32x4& v, const bf16_t* p) { v = *reinterpret_cast<const u32x4*>(p); }
+__device__ __forceinline__ void g2_ldb(u32x2n& v, const fp8_t* p) { v = *reinterpret_cast<const u32x2n*>(p); }
+
 template <typename TA> struct ALoad;
 template <> struct ALoad<bf16_t> {  // 4 x 16 B per thread per tile (native vectors: register-resident)
   u32x4 v[4];
@@ -277,7 +302,7 @@ template <> struct ALoad<float> {  // 8 x 16 B per thread per tile
 };
 
 
-template <typename TA, int AMODE, int EPI, typename TC>
+template <typename TA, typename TB, int AMODE, int EPI, typename TC>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) bf16_t As[2][G2_BM * G2_LDK];
   __shared__ __attribute__((aligned(16))) bf16_t Bs[2][G2_BN * G2_LDK];
@@ -298,7 +323,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
   const int m0 = tm * G2_BM, n0 = tn * G2_BN;
   const int ks = blockIdx.z;
   const TA* __restrict__ A = reinterpret_cast<const TA*>(g.A);
-  const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(g.W);
+  const TB* __restrict__ W = reinterpret_cast<const TB*>(g.W);
   const int nkt = g.K / G2_BK;  // K % 64 == 0 (checked by the launcher)
   const int kt_per = (nkt + g.ksplit - 1) / g.ksplit;
   const int kt0 = ks * kt_per, kt1 = min(nkt, kt0 + kt_per);
@@ -311,7 +336,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
   int cb0 = 0, ct0 = 0;
   if (AMODE == A_CONV) { cb0 = (m0 + arow0) / g.L; ct0 = (m0 + arow0) - cb0 * g.L; }
   ALoad<TA> ar0, ar1;
-  ALoad<bf16_t> br0, br1;
+  BLoad<TB> br0, br1;
 #define G2_LOAD(kt, ar, br)                                                                                \
   {                                                                                                        \
     const int kb = (kt) * G2_BK;                                                                           \
@@ -337,7 +362,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
     _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                        \
       const int c = tid + 256 * i, r = c >> 3, seg = (c & 7) * 8;                                          \
       const int n = min(n0 + r, g.N - 1); /* rows past N duplicate row N-1 (never stored) */              \
-      br.v[i] = *reinterpret_cast<const u32x4*>(W + (size_t)n * g.ldw + kb + seg);                         \
+      g2_ldb(br.v[i], W + (size_t)n * g.ldw + kb + seg);                                                   \
     }                                                                                                      \
   }
 #define G2_STORE(buf, ar, br)                                                                                      \
@@ -349,7 +374,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
     }                                                                                                      \
     _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                        \
       const int c = tid + 256 * i, r = c >> 3, seg = (c & 7) * 8;                                          \
-      *reinterpret_cast<u32x4*>(bs + r * G2_LDK + seg) = br.v[i];                                          \
+      g2_stb(bs + r * G2_LDK + seg, br.v[i]);                                                              \
     }                                                                                                      \
   }
 
@@ -410,6 +435,13 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
   for (int j = 0; j < 2; ++j) {
     const int col = n0 + wn * 64 + j * 32 + (lane & 31);
     if (col >= g.N) continue;
+    if constexpr (sizeof(TB) == 1) {  // fp8 weights: per-row dequantisation scale
+      const float sc = g.wscale[col];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] *= sc;
+    }
     if (g.ksplit > 1) {
       float* P = g.ws + (size_t)ks * g.M * g.N;
 #pragma unroll
@@ -467,9 +499,9 @@ __global__ __launch_bounds__(256) void gemm2_splitk_reduce(GemmArgs g) {
 
 int g_opt_codec_g2 = 1;       // large-M bf16 GEMM (gemm_bf16_kernel) on/off
 int g_opt_codec_xcd = 1;      // its XCD-aware tile order
-int g_opt_codec_g2_min = 1024;  // smallest M that takes it
+int g_opt_codec_g2_min = 128;  // smallest M that takes it (measured: M = 256 0.86 vs 1.04 ms, M = 10 0.64 vs 0.59)
 
-template <typename TA, int AMODE, int EPI, typename TC>
+template <typename TA, typename TB, int AMODE, int EPI, typename TC>
 static void gemm2_launch(GemmArgs g, hipStream_t s) {
   const int tiles = ((g.N + G2_BN - 1) / G2_BN) * ((g.M + G2_BM - 1) / G2_BM);
   const int nkt = g.K / G2_BK;
@@ -478,7 +510,7 @@ static void gemm2_launch(GemmArgs g, hipStream_t s) {
   g.ksplit = ks;
   g.xcd_remap = g_opt_codec_xcd;
   dim3 grid((g.N + G2_BN - 1) / G2_BN, (g.M + G2_BM - 1) / G2_BM, ks);
-  hipLaunchKernelGGL((gemm_bf16_kernel<TA, AMODE, EPI, TC>), grid, dim3(256), 0, s, g);
+  hipLaunchKernelGGL((gemm_bf16_kernel<TA, TB, AMODE, EPI, TC>), grid, dim3(256), 0, s, g);
   if (ks > 1) {
     const int blocks = (int)std::min<size_t>(((size_t)g.M * g.N + 255) / 256, 2048);
     hipLaunchKernelGGL((gemm2_splitk_reduce<EPI, TC>), dim3(blocks), dim3(256), 0, s, g);
@@ -491,7 +523,8 @@ static void gemm2_launch(GemmArgs g, hipStream_t s) {
 template <typename TW, typename TA, int AMODE, int EPI, typename TC = float>
 static void gemm_w(const GemmArgs& g, hipStream_t s) {
   if constexpr (sizeof(TW) == 2) {
-    if (g_opt_codec_g2 && g.M >= g_opt_codec_g2_min) gemm2_launch<TA, AMODE, EPI, TC>(g, s);
+    if (g.wscale) gemm2_launch<TA, fp8_t, AMODE, EPI, TC>(g, s);  // fp8 codec weights: any M
+    else if (g_opt_codec_g2 && g.M >= g_opt_codec_g2_min) gemm2_launch<TA, bf16_t, AMODE, EPI, TC>(g, s);
     else gemm_launch<true, TA, bf16_t, AMODE, EPI, TC>(g, 1, s);
   } else {
     static_assert(sizeof(TA) == 4 && sizeof(TC) == 4, "parity mode keeps fp32 activations");
@@ -870,7 +903,7 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
   g.M = M;
   // embed Conv1d(512->768, k7, pad 3)
   g.A = feats; g.lda = CIN; g.cin = CIN; g.taps = 7;
-  g.W = w.embed_w; g.ldw = 7 * CIN; g.K = 7 * CIN; g.N = CD;
+  g.W = w.embed_w; g.wscale = w.embed_s; g.ldw = 7 * CIN; g.K = 7 * CIN; g.N = CD;
   g.C = x; g.ldc = CD; g.bias = w.embed_b;
   gemm_w<TW, TAct, A_CONV, E_BIAS>(g, s);
 
@@ -880,10 +913,10 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
     c.ws = sc.ws;
     c.L = L; c.M = M; c.cin = CD; c.taps = 3; c.K = 3 * CD; c.N = CD; c.ldw = 3 * CD;
     c.A = gn; c.lda = CD;
-    c.W = w.rn_c1w[i]; c.bias = w.rn_c1b[i]; c.C = t1; c.ldc = CD;
+    c.W = w.rn_c1w[i]; c.wscale = w.rn_c1s[i]; c.bias = w.rn_c1b[i]; c.C = t1; c.ldc = CD;
     gemm_w<TW, TAct, A_CONV, E_BIAS>(c, s);
     hipLaunchKernelGGL((gn_apply_kernel<true, TAct>), dim3(GN_G, B), dim3(256), 0, s, t1, L, w.rn_n2w[i], w.rn_n2b[i], gn);
-    c.W = w.rn_c2w[i]; c.bias = w.rn_c2b[i]; c.C = x; c.res = x; c.ldr = CD;
+    c.W = w.rn_c2w[i]; c.wscale = w.rn_c2s[i]; c.bias = w.rn_c2b[i]; c.C = x; c.res = x; c.ldr = CD;
     gemm_w<TW, TAct, A_CONV, E_BIAS_RES>(c, s);
   };
   resnet(0);
@@ -894,7 +927,7 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
     c.ws = sc.ws;
     c.L = L; c.M = M; c.K = CD; c.N = 3 * CD; c.ldw = CD;
     c.A = gn; c.lda = CD;
-    c.W = w.at_qkv_w; c.bias = w.at_qkv_b; c.C = t1; c.ldc = CFF;
+    c.W = w.at_qkv_w; c.wscale = w.at_qkv_s; c.bias = w.at_qkv_b; c.C = t1; c.ldc = CFF;
     gemm_w<TW, TAct, A_PLAIN, E_BIAS>(c, s);
     const int ldS = (L + 3) & ~3;
     float* S = sc.att;            // [B][L][ldS]
@@ -926,7 +959,7 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
     GemmArgs o{};
     o.ws = sc.ws;
     o.M = M; o.N = CD; o.K = CD; o.L = L;
-    o.A = p.C; o.lda = p.ldc; o.W = w.at_proj_w; o.ldw = CD; o.bias = w.at_proj_b;
+    o.A = p.C; o.lda = p.ldc; o.W = w.at_proj_w; o.wscale = w.at_proj_s; o.ldw = CD; o.bias = w.at_proj_b;
     o.C = x; o.ldc = CD; o.res = x; o.ldr = CD;
     gemm_w<TW, TAct, A_PLAIN, E_BIAS_RES>(o, s);
   }
@@ -942,12 +975,12 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
     GemmArgs c{};
     c.ws = sc.ws;
     c.M = M; c.L = L; c.N = CFF; c.K = CD; c.ldw = CD;
-    c.A = t2a; c.lda = CD; c.W = w.pw1_w[i]; c.bias = w.pw1_b[i]; c.C = t1a; c.ldc = CFF;
+    c.A = t2a; c.lda = CD; c.W = w.pw1_w[i]; c.wscale = w.pw1_s[i]; c.bias = w.pw1_b[i]; c.C = t1a; c.ldc = CFF;
     gemm_w<TW, TAct, A_PLAIN, E_BIAS_GELU, TAct>(c, s);
     GemmArgs d{};
     d.ws = sc.ws;
     d.M = M; d.L = L; d.N = CD; d.K = CFF; d.ldw = CFF;
-    d.A = t1a; d.lda = CFF; d.W = w.pw2_w[i]; d.bias = w.pw2_b[i]; d.gamma = w.gamma[i];
+    d.A = t1a; d.lda = CFF; d.W = w.pw2_w[i]; d.wscale = w.pw2_s[i]; d.bias = w.pw2_b[i]; d.gamma = w.gamma[i];
     d.C = x; d.ldc = CD; d.res = x; d.ldr = CD;
     gemm_w<TW, TAct, A_PLAIN, E_BIAS_GAMMA_RES>(d, s);
   }
@@ -956,7 +989,7 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
     GemmArgs h{};
     h.ws = sc.ws;
     h.M = M; h.L = L; h.N = 2 * NB; h.K = CD; h.ldw = CD;
-    h.A = t2a; h.lda = CD; h.W = w.head_w; h.bias = w.head_b; h.C = sc.spec; h.ldc = 2 * NB;
+    h.A = t2a; h.lda = CD; h.W = w.head_w; h.wscale = w.head_s; h.bias = w.head_b; h.C = sc.spec; h.ldc = 2 * NB;
     gemm_w<TW, TAct, A_PLAIN, E_BIAS>(h, s);
   }
   hipLaunchKernelGGL(istft_frames_kernel, dim3(M), dim3(256), 0, s, sc.spec,

@@ -125,6 +125,26 @@ struct GraphKey {
   }
 };
 
+// host f32 -> OCP e4m3fn (gfx950 fp8), round to nearest even, saturated to +-448, NaN -> 0x7f
+static uint8_t f32_to_e4m3_host(float x) {
+  if (std::isnan(x)) return 0x7f;
+  const uint8_t sign = std::signbit(x) ? 0x80 : 0x00;
+  double a = std::fabs((double)x);
+  if (a >= 448.0) return sign | 0x7e;
+  if (a < std::ldexp(1.0, -6)) {  // subnormal: value = mant * 2^-9 (mant 8 is the smallest normal)
+    const int q = (int)std::nearbyint(a * 512.0);
+    return sign | (uint8_t)q;
+  }
+  int e;
+  const double m = std::frexp(a, &e);  // a = m * 2^e, m in [0.5, 1)
+  int mant = (int)std::nearbyint((m * 2.0 - 1.0) * 8.0);
+  int ex = e - 1;
+  if (mant == 8) { mant = 0; ++ex; }
+  int code = ((ex + 7) << 3) | mant;
+  if (code > 0x7e) code = 0x7e;
+  return sign | (uint8_t)code;
+}
+
 struct lvx_ctx {
   lvx_config cfg{};
   std::map<std::string, std::vector<float>> host;  // staged fp32 weights (released at finalize)
@@ -167,6 +187,26 @@ struct lvx_ctx {
     *out = d;
     return 0;
   }
+  // codec GEMM weights: the weight dtype, or e4m3fn with one scale per output row (codec_dtype FP8:
+  // s = max|w_row| / 448, q = RNE(w / s) saturated; dequantised exactly to bf16 in the GEMM loader)
+  int upload_cw(const std::vector<float>& v, int rows, const void** out, const float** scale_out) {
+    if (cfg.codec_dtype != LVX_DTYPE_FP8) return upload_w(v, out);
+    const size_t K = v.size() / rows;
+    std::vector<uint8_t> q(v.size());
+    std::vector<float> sc(rows);
+    for (int n = 0; n < rows; ++n) {
+      float mx = 0.f;
+      for (size_t k = 0; k < K; ++k) mx = std::max(mx, std::fabs(v[n * K + k]));
+      const float s = mx > 0.f ? mx / 448.f : 1.f;
+      sc[n] = s;
+      for (size_t k = 0; k < K; ++k) q[n * K + k] = f32_to_e4m3_host(v[n * K + k] / s);
+    }
+    uint8_t* d;
+    if (int r = dalloc(&d, q.size())) return r;
+    HIP_TRY(hipMemcpy(d, q.data(), q.size(), hipMemcpyHostToDevice));
+    *out = d;
+    return upload_f32(sc, scale_out);
+  }
   const std::vector<float>& H(const std::string& k) { return host.at(k); }
 };
 
@@ -207,6 +247,8 @@ int lvx_create(const lvx_config* cfg, lvx_ctx** out) {
   if (cfg->max_positions < 1 || cfg->max_positions > BLOCK_SIZE)
     return fail(LVX_E_ARG, "max_positions out of range [1,8192] (GPTConfig.block_size)");
   if (cfg->max_codec_frames < 1) return fail(LVX_E_ARG, "max_codec_frames must be >= 1");
+  if (cfg->codec_dtype != 0 && !(cfg->codec_dtype == LVX_DTYPE_FP8 && cfg->weight_dtype == LVX_DTYPE_BF16))
+    return fail(LVX_E_ARG, "codec_dtype must be 0 or LVX_DTYPE_FP8 (with weight_dtype LVX_DTYPE_BF16)");
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess || ndev == 0) return fail(LVX_E_HIP, "no HIP device available");
@@ -290,7 +332,10 @@ int lvx_finalize(lvx_ctx* c) {
   // ---- codec ----
   CodecWeights& cw = c->cw;
   cw.codebook = w.codebook;
-  UP_W(repack_conv(c->H("backbone.embed.weight"), 768, 512, 7), cw.embed_w);
+#define UP_CW(vec, rows, dst, sdst) \
+  if ((r = c->upload_cw((vec), (rows), &(dst), &(sdst)))) return r;
+  cw.wfp8 = c->cfg.codec_dtype == LVX_DTYPE_FP8;
+  UP_CW(repack_conv(c->H("backbone.embed.weight"), 768, 512, 7), 768, cw.embed_w, cw.embed_s);
   UP_F("backbone.embed.bias", cw.embed_b);
   UP_F("backbone.norm.scale.weight", cw.ada_scale);
   UP_F("backbone.norm.shift.weight", cw.ada_shift);
@@ -301,9 +346,9 @@ int lvx_finalize(lvx_ctx* c) {
     UP_F(p + "norm1.bias", cw.rn_n1b[ri]);
     UP_F(p + "norm2.weight", cw.rn_n2w[ri]);
     UP_F(p + "norm2.bias", cw.rn_n2b[ri]);
-    UP_W(repack_conv(c->H(p + "conv1.weight"), 768, 768, 3), cw.rn_c1w[ri]);
+    UP_CW(repack_conv(c->H(p + "conv1.weight"), 768, 768, 3), 768, cw.rn_c1w[ri], cw.rn_c1s[ri]);
     UP_F(p + "conv1.bias", cw.rn_c1b[ri]);
-    UP_W(repack_conv(c->H(p + "conv2.weight"), 768, 768, 3), cw.rn_c2w[ri]);
+    UP_CW(repack_conv(c->H(p + "conv2.weight"), 768, 768, 3), 768, cw.rn_c2w[ri], cw.rn_c2s[ri]);
     UP_F(p + "conv2.bias", cw.rn_c2b[ri]);
     ++ri;
   }
@@ -318,9 +363,9 @@ int lvx_finalize(lvx_ctx* c) {
       auto& b = c->H(p + n + ".bias");
       qkvb.insert(qkvb.end(), b.begin(), b.end());
     }
-    UP_W(qkv, cw.at_qkv_w);
+    UP_CW(qkv, 3 * 768, cw.at_qkv_w, cw.at_qkv_s);
     if ((r = c->upload_f32(qkvb, &cw.at_qkv_b))) return r;
-    UP_W(c->H(p + "proj_out.weight"), cw.at_proj_w);
+    UP_CW(c->H(p + "proj_out.weight"), 768, cw.at_proj_w, cw.at_proj_s);
     UP_F(p + "proj_out.bias", cw.at_proj_b);
   }
   UP_F("backbone.pos_net.5.weight", cw.pn_w);
@@ -331,15 +376,15 @@ int lvx_finalize(lvx_ctx* c) {
     UP_F(p + "dwconv.bias", cw.dw_b[i]);
     UP_F(p + "norm.scale.weight", cw.cn_scale[i]);
     UP_F(p + "norm.shift.weight", cw.cn_shift[i]);
-    UP_W(c->H(p + "pwconv1.weight"), cw.pw1_w[i]);
+    UP_CW(c->H(p + "pwconv1.weight"), 2304, cw.pw1_w[i], cw.pw1_s[i]);
     UP_F(p + "pwconv1.bias", cw.pw1_b[i]);
-    UP_W(c->H(p + "pwconv2.weight"), cw.pw2_w[i]);
+    UP_CW(c->H(p + "pwconv2.weight"), 768, cw.pw2_w[i], cw.pw2_s[i]);
     UP_F(p + "pwconv2.bias", cw.pw2_b[i]);
     UP_F(p + "gamma", cw.gamma[i]);
   }
   UP_F("backbone.final_layer_norm.weight", cw.fln_w);
   UP_F("backbone.final_layer_norm.bias", cw.fln_b);
-  UP_W(c->H("head.out.weight"), cw.head_w);
+  UP_CW(c->H("head.out.weight"), 1282, cw.head_w, cw.head_s);
   UP_F("head.out.bias", cw.head_b);
   {
     std::vector<float> win(1280);
@@ -356,6 +401,7 @@ int lvx_finalize(lvx_ctx* c) {
   }
 #undef UP_F
 #undef UP_W
+#undef UP_CW
   // ---- AR state ----
   ArState& st = c->st;
   const int S = c->cfg.max_streams, P = c->cfg.max_positions;

@@ -103,6 +103,14 @@ struct CodecWeights {
   const float* gamma[12] = {};
   const float* fln_w = nullptr; const float* fln_b = nullptr;
   const void* head_w = nullptr; const float* head_b = nullptr;  // [1282][768]
+  // codec_dtype FP8: every matrix above is e4m3fn [N][K] and *_s is its per-row scale [N]
+  // (w = q * s); null in bf16 / fp32 storage
+  int wfp8 = 0;
+  const float* embed_s = nullptr;
+  const float* rn_c1s[4] = {}; const float* rn_c2s[4] = {};
+  const float* at_qkv_s = nullptr; const float* at_proj_s = nullptr;
+  const float* pw1_s[12] = {}; const float* pw2_s[12] = {};
+  const float* head_s = nullptr;
   const float* window = nullptr;  // [1280] periodic Hann
   const float* twiddle = nullptr; // FFT tables (see istft)
 };

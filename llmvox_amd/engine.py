@@ -21,20 +21,22 @@ def _ptr(t: Optional[torch.Tensor]):
 
 class Engine:
     def __init__(self, device_index: int = 0, weight_dtype: str = "fp32", kv_dtype: str = "fp32",
-                 max_streams: int = 8, max_positions: int = 8192, max_codec_frames: int = 1280):
+                 max_streams: int = 8, max_positions: int = 8192, max_codec_frames: int = 1280,
+                 codec_dtype: Optional[str] = None):
         self.lib = _lib.load()
         if not torch.cuda.is_available():
             raise RuntimeError("llmvox_amd needs a ROCm GPU (MI355X); there is no CPU path")
         self.device = torch.device(f"cuda:{device_index}")
         self.device_index = device_index
         cfg = _lib.LvxConfig(device_index, _lib.DTYPES[weight_dtype], _lib.DTYPES[kv_dtype], max_streams,
-                             max_positions, max_codec_frames)
+                             max_positions, max_codec_frames, _lib.DTYPES[codec_dtype] if codec_dtype else 0)
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
             _lib.check(self.lib.lvx_create(ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
         self.weight_dtype = weight_dtype
         self.kv_dtype = kv_dtype
+        self.codec_dtype = codec_dtype or weight_dtype
         self.max_streams = max_streams
         self.max_positions = max_positions
         self.max_codec_frames = max_codec_frames
@@ -159,10 +161,11 @@ class Engine:
 
 
 def build_engine(device_index=0, weight_dtype="fp32", kv_dtype="fp32", seed=1234, max_streams=8,
-                 max_positions=8192, max_codec_frames=1280, weights=None) -> Engine:
-    """Engine loaded with ``weights`` = (gpt, codec, text_table) or the seeded synthetic set."""
+                 max_positions=8192, max_codec_frames=1280, weights=None, codec_dtype=None) -> Engine:
+    """Engine loaded with ``weights`` = (gpt, codec, text_table) or the seeded synthetic set.
+    codec_dtype "fp8": codec GEMM weights stored as e4m3fn with per-row scales (configs[4])."""
     from .weights import synthetic_all
-    e = Engine(device_index, weight_dtype, kv_dtype, max_streams, max_positions, max_codec_frames)
+    e = Engine(device_index, weight_dtype, kv_dtype, max_streams, max_positions, max_codec_frames, codec_dtype)
     gw, cw, tt = weights if weights is not None else synthetic_all(seed)
     e.load_weights(gw, cw, tt)
     return e
