@@ -1,0 +1,208 @@
+"""HTTP streaming-TTS service on the fused HIP path.
+
+The reference serves ``POST /tts`` (streaming_server.py:494-540): a text producer routes words to
+two replica queues (switching after every sentence, :184-248), two ``audio_generator_sync``
+consumer threads turn them into f32le PCM chunks (:250-426), and ``audio_generator_async``
+(:428-469) streams the chunks in speaking order as ``application/octet-stream``.
+
+Here one ``FusedScheduler`` thread serves every request: each request opens the two replica
+streams (index 0 with initial dump 10, index 1 with 160; streaming.py mirrors the per-token
+semantics), the request text is routed with the reference's rules (``route_text``), and all
+open streams of all requests are decoded together (continuous batching, one HIP-graph replay per
+step, codec per dump). The response body is the same byte stream the reference produces: raw
+f32le mono 24 kHz chunks, in order, no framing.
+
+Differences, on purpose:
+  * the text is spoken as given. The reference hands it to an LLM first and, through
+    ``"text" in request`` being False for a pydantic model (:209), actually routes /tts requests
+    to its ASR branch; the intended text path is what is built here, the LLM (an upstream text
+    source) is out of scope. The request text is followed by the EOS token,
+    as an LLM stream would end, so the replica that receives it ends the response at its
+    end-of-audio token.
+  * ``max_tokens`` bounds a request (the reference relies on the model emitting end-of-audio;
+    synthetic weights never do): when a request's streams have generated that many tokens each,
+    their undumped tail is decoded and the response ends.
+"""
+
+import threading
+from queue import Queue
+from typing import List, Optional
+
+from . import config as C
+from .streaming import FusedScheduler, audio_chunks, route_text
+
+
+class _Session:
+    def __init__(self, streams, queues):
+        self.streams = streams
+        self.queues = queues
+        self.done = False
+
+
+class TTSService:
+    """Owns the scheduler thread. ``submit(text)`` returns a session whose two queues carry the
+    replica outputs (bytes and 0 / 1 / 'end' signals); ``chunks(session)`` yields the PCM bytes
+    in speaking order (audio_generator_async semantics) and closes the session at the end."""
+
+    def __init__(self, engine, max_chunk: int = 64, max_tokens: Optional[int] = None, eos: str = C.EOS_TOKEN,
+                 eoa_id: int = C.EOA_TOKEN_ID, dumps=(C.INITIAL_DUMP_SIZE_1, C.INITIAL_DUMP_SIZE_2)):
+        self.engine = engine
+        self.sched = FusedScheduler(engine, max_chunk=max_chunk, to_bytes=True)
+        self.max_tokens = max_tokens or max(1, engine.max_positions - max_chunk - 1)
+        self.eos = eos
+        self.eoa_id = eoa_id
+        self.dumps = dumps
+        self.sessions: List[_Session] = []
+        self.lock = threading.Condition()
+        self.running = True
+        self.error: Optional[BaseException] = None
+        self.thread = threading.Thread(target=self._loop, name="lvx-tts-scheduler", daemon=True)
+        self.thread.start()
+
+    # -- request side --
+    def submit(self, text: str) -> _Session:
+        if self.error is not None:
+            raise RuntimeError("TTS scheduler thread failed") from self.error
+        queues = [Queue(), Queue()]
+        with self.lock:
+            if len(self.sched.free_slots) < 2:
+                raise RuntimeError("no free KV slots: too many concurrent requests")
+            streams = [self.sched.open_stream(index=i, dump_size=self.dumps[i], sink=queues[i], eoa_id=self.eoa_id)
+                       for i in range(2)]
+
+            class _Feed:  # route_text puts words on "queues"; here they go straight to the streams
+                def __init__(self, st):
+                    self.st = st
+
+                def put(self, w):
+                    self.st.feed(w)
+
+            route_text(text.split() + [self.eos], [_Feed(streams[0]), _Feed(streams[1])], eos=self.eos)
+            s = _Session(streams, queues)
+            self.sessions.append(s)
+            self.lock.notify_all()
+        return s
+
+    def chunks(self, session: _Session, timeout: float = 0.05):
+        try:
+            for item in audio_chunks(session.queues[0], session.queues[1], timeout=timeout,
+                                     stop=lambda: self.error is not None):
+                yield item
+        finally:
+            self.close(session)
+        if self.error is not None:
+            raise RuntimeError("TTS scheduler thread failed") from self.error
+
+    def close(self, session: _Session):
+        with self.lock:
+            if session in self.sessions:
+                self.sessions.remove(session)
+            for st in session.streams:
+                if st in self.sched.streams:
+                    self.sched.close_stream(st)
+
+    def shutdown(self):
+        with self.lock:
+            self.running = False
+            self.lock.notify_all()
+        self.thread.join(timeout=5)
+
+    # -- scheduler thread --
+    def _cap(self):
+        """End every session whose streams reached max_tokens: decode their undumped tails in
+        speaking order, then 'end' on both queues."""
+        for s in list(self.sessions):
+            if s.done or min(len(st.tokens) for st in s.streams) < self.max_tokens:
+                continue
+            s.done = True
+            tails = [(st, st.m.speech_outputs) for st in s.streams if st.m.speech_outputs]
+            for st, toks in tails:
+                st.m.speech_outputs = []
+                import torch
+                codes = torch.tensor([toks], dtype=torch.int32, device=self.engine.device)
+                st._out(self.engine.decode_codes(codes).cpu().numpy()[0].astype("float32").tobytes())
+            for q in s.queues:
+                q.put("end")
+            for st in s.streams:
+                if st in self.sched.streams:
+                    self.sched.close_stream(st)
+
+    def _loop(self):
+        try:
+            while True:
+                with self.lock:
+                    if not self.running:
+                        return
+                    n = self.sched.run_chunk() if self.sched.streams else 0
+                    if n:
+                        self._cap()
+                    else:
+                        self.lock.wait(timeout=0.01)
+        except BaseException as e:  # surfaced to every waiting request
+            self.error = e
+
+
+def create_app(service):
+    """FastAPI app with the reference's /tts contract (TTSRequest {text} -> octet-stream)."""
+    from fastapi import FastAPI, HTTPException
+    from fastapi.responses import StreamingResponse
+    from pydantic import BaseModel
+
+    class TTSRequest(BaseModel):
+        text: str
+
+    app = FastAPI(title="llmvox_amd streaming TTS")
+
+    @app.post("/tts")
+    def tts(request: TTSRequest):
+        try:
+            session = service.submit(request.text)
+        except RuntimeError as e:
+            raise HTTPException(status_code=503, detail=str(e))
+        return StreamingResponse(service.chunks(session), media_type="application/octet-stream")
+
+    @app.get("/health")
+    def health():
+        return {"ok": service.error is None, "sessions": len(service.sessions)}
+
+    return app
+
+
+def main(argv=None):
+    """python -m llmvox_amd.server [--port 8000] [--dtype bf16] [--ckpt ... --wavtokenizer ...]"""
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=8000)
+    ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--kv-dtype", default=None, choices=["bf16", "fp32", "fp8"])
+    ap.add_argument("--max-streams", type=int, default=64)
+    ap.add_argument("--max-positions", type=int, default=8192)
+    ap.add_argument("--ckpt", default=None, help="LLMVoX checkpoint (ckpt_english_tiny.pt)")
+    ap.add_argument("--wavtokenizer", default=None, help="WavTokenizer Lightning checkpoint")
+    ap.add_argument("--text-embed", default=None,
+                    help="ByT5 encoder state dict (torch, weights_only) for the 386-row text table")
+    ap.add_argument("--seed", type=int, default=1234, help="synthetic weights for whatever is not given")
+    a = ap.parse_args(argv)
+    from .engine import build_engine
+    from . import weights as W
+    gw, cw, tt = W.synthetic_all(a.seed)
+    if a.ckpt:
+        gw = W.load_llmvox_checkpoint(a.ckpt)
+    if a.wavtokenizer:
+        cw = W.load_wavtokenizer_checkpoint(a.wavtokenizer)
+    if a.text_embed:
+        import torch
+        sd = torch.load(a.text_embed, map_location="cpu", weights_only=True)
+        tt = W.load_text_embed_from_t5({k: v.float().numpy() for k, v in sd.items()})
+    weights = (gw, cw, tt)
+    eng = build_engine(a.device, a.dtype, a.kv_dtype or a.dtype, seed=a.seed, max_streams=a.max_streams,
+                       max_positions=a.max_positions, max_codec_frames=C.MAX_DUMP_SIZE * 2, weights=weights)
+    svc = TTSService(eng)
+    import uvicorn
+    uvicorn.run(create_app(svc), host=a.host, port=a.port)
+
+
+if __name__ == "__main__":
+    main()
