@@ -1307,7 +1307,7 @@ __device__ __forceinline__ void embed_row(const GemvArgs& a, int4 ri, int lane, 
 template <int MODE>
 __global__ __launch_bounds__(256) void ar_rows_kernel(GemvArgs a) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int b = blockIdx.x * 4 + wave;
+  const int b = blockIdx.x * (blockDim.x >> 6) + wave;
   if (b >= a.B) return;
   float4 g[3], v[3];
 #pragma unroll
@@ -1316,6 +1316,9 @@ __global__ __launch_bounds__(256) void ar_rows_kernel(GemvArgs a) {
     XRow<MODE> r;
     xrow_issue(a, b, lane, r);
     xrow_sum(r, v);
+    if (MODE == 4)  // fold the pending copies into x here (one wave owns the row): the next c_proj
+#pragma unroll      // then adds its output to a final x instead of re-reading the copies
+      for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = v[j];
   } else {
     embed_row(a, a.st.rowinfo[b], lane, v);
 #pragma unroll
@@ -1327,7 +1330,9 @@ __global__ __launch_bounds__(256) void ar_rows_kernel(GemvArgs a) {
   for (int j = 0; j < 3; ++j) dst[j * 64 + lane] = pack4_bf16(v[j]);
 }
 
-// split-KV merge for the batched path: y[b] (bf16) into st.xn
+// split-KV merge for the batched path: y[b] (bf16) into st.xn. NS = ns_max (the attention's split
+// count at this B): only the splits that can exist are loaded
+template <int NS>
 __global__ __launch_bounds__(256) void ar_merge_bf16_kernel(ArState st, int ns_max) {
   __shared__ float cf[N_HEAD * NSPLIT];
   const int b = blockIdx.x, tid = threadIdx.x;
@@ -1335,13 +1340,13 @@ __global__ __launch_bounds__(256) void ar_merge_bf16_kernel(ArState st, int ns_m
   // every load up front: one (m, l) pair per thread (8 heads x 16 splits) and 3 x 16 partials
   float2 ml = make_float2(-INFINITY, 0.f);
   if (tid < N_HEAD * NSPLIT) ml = reinterpret_cast<const float2*>(st.part_ml)[(size_t)b * N_HEAD * NSPLIT + tid];
-  float pv[3][NSPLIT];
+  float pv[3][NS];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int e = tid + 256 * j, head = e / HD, d = e - head * HD;
     const float* po = st.part_o + ((size_t)(b * N_HEAD + head) * NSPLIT) * HD + d;
 #pragma unroll
-    for (int i = 0; i < NSPLIT; ++i) pv[j][i] = po[(size_t)i * HD];
+    for (int i = 0; i < NS; ++i) pv[j][i] = po[(size_t)i * HD];
   }
   if (tid < N_HEAD * NSPLIT) {
     const int ns = ri.x < 0 ? 0 : min(ns_max, (ri.y + 1 + 63) / 64);
@@ -1361,9 +1366,16 @@ __global__ __launch_bounds__(256) void ar_merge_bf16_kernel(ArState st, int ns_m
     const int e = tid + 256 * j, head = e / HD;
     float y = 0.f;
 #pragma unroll
-    for (int i = 0; i < NSPLIT; ++i) y += cf[head * NSPLIT + i] * pv[j][i];
+    for (int i = 0; i < NS; ++i) y += cf[head * NSPLIT + i] * pv[j][i];
     st.xn[(size_t)b * D + e] = f32_to_bf16(y);
   }
+}
+
+static void launch_merge_bf16(const ArState& st, int B, int nsm, hipStream_t s) {
+  if (nsm <= 2) hipLaunchKernelGGL(ar_merge_bf16_kernel<2>, dim3(B), dim3(256), 0, s, st, nsm);
+  else if (nsm <= 4) hipLaunchKernelGGL(ar_merge_bf16_kernel<4>, dim3(B), dim3(256), 0, s, st, nsm);
+  else if (nsm <= 8) hipLaunchKernelGGL(ar_merge_bf16_kernel<8>, dim3(B), dim3(256), 0, s, st, nsm);
+  else hipLaunchKernelGGL(ar_merge_bf16_kernel<NSPLIT>, dim3(B), dim3(256), 0, s, st, nsm);
 }
 
 // OUT as gemv_store, plus OUT 5: h (bf16) = gelu_tanh(v) for the batched mlp c_proj. A block
@@ -1773,7 +1785,7 @@ static void launch_op_bt(int op, GemvArgs& a, const ArWeights& w, int l, int kvd
       if (g_opt_bt_merge) {
         launch_bt<768, 2, 1>(a, nsm, s);
       } else {
-        hipLaunchKernelGGL(ar_merge_bf16_kernel, dim3(B), dim3(256), 0, s, a.st, nsm);
+        launch_merge_bf16(a.st, B, nsm, s);
         launch_bt<768, 1, 1>(a, 0, s);
       }
       break;
@@ -1815,8 +1827,8 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
         if (l == 0) launch_mfma_ln<0, 3>(a, s);
         else launch_mfma_ln<0, 4>(a, s);
       } else if (mf) {
-        if (l == 0) hipLaunchKernelGGL((ar_rows_kernel<3>), dim3((B + 3) / 4), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((ar_rows_kernel<4>), dim3((B + 3) / 4), dim3(256), 0, s, a);
+        if (l == 0) hipLaunchKernelGGL((ar_rows_kernel<3>), dim3(B), dim3(64), 0, s, a);
+        else hipLaunchKernelGGL((ar_rows_kernel<4>), dim3(B), dim3(64), 0, s, a);
         launch_mfma2<768, 0>(a, s);
       } else if (l == 0) {
         launch_gemv<TW, 768, 1, 2, 3, 0>(a, s);
@@ -1830,7 +1842,8 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
     case 2:
       a.W = w.w_aproj[l]; a.N = D;
       if (mf) {
-        hipLaunchKernelGGL(ar_merge_bf16_kernel, dim3(B), dim3(256), 0, s, a.st, nsm);
+        if (B > g_opt_mfma_ln) a.add_y = 0;  // ar_rows_kernel<4> of this layer's c_attn folded them
+        launch_merge_bf16(a.st, B, nsm, s);
         launch_mfma2<768, 1>(a, s);
       } else {
         launch_gemv<TW, 768, 1, 1, 2, 1>(a, s);
@@ -1851,7 +1864,7 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       } else if (mf && B <= g_opt_mfma_ln) {
         launch_mfma_ln<5, 0>(a, s);
       } else if (mf) {
-        hipLaunchKernelGGL((ar_rows_kernel<0>), dim3((B + 3) / 4), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((ar_rows_kernel<0>), dim3(B), dim3(64), 0, s, a);
         launch_mfma2<768, 5>(a, s);
       } else {
         launch_gemv<TW, 768, 1, 2, 0, 2>(a, s);
@@ -1868,7 +1881,7 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       if (mf && B <= g_opt_mfma_ln) {
         launch_mfma_ln<3, 4>(a, s);
       } else if (mf) {
-        hipLaunchKernelGGL((ar_rows_kernel<4>), dim3((B + 3) / 4), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((ar_rows_kernel<4>), dim3(B), dim3(64), 0, s, a);
         launch_mfma2<768, 3>(a, s);
       } else if (select) {
         if (fm) launch_gemv<TW, 768, 1, 2, 4, 4>(a, s);

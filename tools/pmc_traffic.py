@@ -31,14 +31,22 @@ def segments(path, counter):
     timed = []
     for a, b in zip(marks[:-1], marks[1:]):
         seg = [r for r in rows[a + 1:b] if not r["Kernel_Name"].startswith("__amd")]
-        if len(seg) >= ITERS:
+        # a probe segment starts with ITERS launches of one op = ITERS x (1 kernel, or 2 kernels
+        # alternating: rows + GEMM, merge + GEMM); anything after it (the codec probe behind the
+        # last op) is cut off; decode-loop segments and warm-ups (10 launches) do not qualify
+        nm = [r["Kernel_Name"] for r in seg]
+        if len(nm) >= ITERS and all(x == nm[0] for x in nm[:ITERS]):
             timed.append(seg[:ITERS])
-    timed = timed[-6:]
+        elif (len(nm) >= 2 * ITERS and nm[0] != nm[1] and all(nm[2 * i] == nm[0] for i in range(ITERS))
+              and all(nm[2 * i + 1] == nm[1] for i in range(ITERS))):
+            timed.append(seg[:2 * ITERS])
+    fused = any("mlp_fused" in r["Kernel_Name"] for t in timed for r in t[:1])
+    timed = timed[-5:] if fused else timed[-6:]  # the fused MLP: five probed ops
     ops = list(range(6)) if len(timed) == 6 else [0, 1, 2, 3, 5]
     out = {k: (0.0, [], 0) for k in range(6)}
     for k, seg in zip(ops, timed[-len(ops):]):
         out[k] = (sum(float(r["Counter_Value"]) for r in seg) * 1024.0 / ITERS,
-                  sorted({r["Kernel_Name"] for r in seg}), len(seg))
+                  sorted({r["Kernel_Name"].split("(")[0] for r in seg}), len(seg))
     return out
 
 
