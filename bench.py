@@ -190,6 +190,37 @@ def cpu_baseline(n_chunks, chunk, min_seconds=10.0, max_seconds=30.0, schedule=N
                       f"{dt:.1f} s on {cpu}"}
 
 
+class _HostCollectives:
+    """torch.distributed facade for the gloo rehearsal: device tensors go through host copies."""
+
+    def __init__(self, d):
+        self.d = d
+        self.ReduceOp = d.ReduceOp
+
+    def __getattr__(self, k):
+        return getattr(self.d, k)
+
+    def _host(self, t):
+        return None if t is None else t.cpu()
+
+    def scatter(self, out, chunks, src=0):
+        o = out.cpu()
+        self.d.scatter(o, [c.cpu() for c in chunks] if chunks is not None else None, src=src)
+        out.copy_(o)
+
+    def gather(self, t, out, dst=0):
+        o = [x.cpu() for x in out] if out is not None else None
+        self.d.gather(t.cpu(), o, dst=dst)
+        if out is not None:
+            for x, y in zip(out, o):
+                x.copy_(y)
+
+    def all_reduce(self, t, op=None):
+        h = t.cpu()
+        self.d.all_reduce(h, op=op)
+        t.copy_(h)
+
+
 # ---------------------------------------------------------------------------------------
 def run_config3(args, eng, world, rank, local, dist):
     """configs[3]: the service path. Every GPU runs --streams replica streams through
@@ -254,10 +285,11 @@ def run_config3(args, eng, world, rank, local, dist):
     dt = time.perf_counter() - t0
     eng.check_errors()
     if dist is not None:
-        tt = torch.tensor([dt, toks], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
-        dt, toks = float(tt[0].item()), int(tt[1].item())
+        t_dt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t_tok = torch.tensor([toks], dtype=torch.float64, device=dev)
+        dist.all_reduce(t_dt, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t_tok, op=dist.ReduceOp.SUM)
+        dt, toks = float(t_dt.item()), int(t_tok.item())
     value = toks / dt
 
     kern, rl = None, None
@@ -321,6 +353,8 @@ def main():
                     help="run the codec on a second HIP stream beside the next chunk's AR (measured slower)")
     ap.add_argument("--no-graphs", action="store_true",
                     help="launch the decode step kernel by kernel (for rocprofv3 --pmc passes)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse the multi-rank path on one GPU (collectives on host copies)")
     ap.add_argument("--config", type=int, default=1, choices=[1, 2, 3, 4],
                     help="BASELINE.json workload (1: default; 2: 32 streams; 3: scheduler replicas; 4: fp8)")
     ap.add_argument("--codec-dtype", default=None, choices=["fp8"], help="fp8 codec weights (configs[4])")
@@ -342,8 +376,14 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if args.dist_backend == "gloo":  # rehearsal: every rank may share one GPU
+            local = local % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+            dist = _HostCollectives(dist)
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
 
     from llmvox_amd.engine import build_engine
     S, chunk, K, Wm = args.streams, args.chunk, args.steps, args.warmup
