@@ -1106,44 +1106,48 @@ __global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer, 
   float m = -INFINITY, l = 0.f, o[24];
 #pragma unroll
   for (int i = 0; i < 24; ++i) o[i] = 0.f;
-  // register double buffer: the next tile's K/V pieces are in flight while this tile is computed
-  KvPiece<TKV> kp[3], vp[3];
-  auto issue = [&](int kb) {
-    const int key = kb + kq;
-    if (key < k1) {
+  // Two tiles in flight: tile kb+128 is loaded into one register set while tile kb (in that set,
+  // issued two tiles ago) is consumed and tile kb+64 is landing in the other. Loads are
+  // unconditional (key clamped to the last valid one, invalid lanes masked after) so that no load
+  // sits under a branch: the compiler's vmcnt for "this set has landed" then leaves the other set
+  // in flight instead of draining every outstanding load.
+  KvPiece<TKV> kp0[3], vp0[3], kp1[3], vp1[3];
+  auto issue = [&](int kb, KvPiece<TKV>(&kp)[3], KvPiece<TKV>(&vp)[3]) {
+    const int key = min(kb + kq, k1 - 1);
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        kp[i].load(Kg + (size_t)key * HD + part * 24 + i * 8);
-        vp[i].load(Vg + (size_t)key * HD + part * 24 + i * 8);
-      }
+    for (int i = 0; i < 3; ++i) {
+      kp[i].load(Kg + (size_t)key * HD + part * 24 + i * 8);
+      vp[i].load(Vg + (size_t)key * HD + part * 24 + i * 8);
     }
   };
-  issue(k0);
-  for (int kb = k0; kb < k1; kb += ATK) {
-    const int key = kb + kq;
-    const bool valid = key < k1;
+  auto tile = [&](int kb, const KvPiece<TKV>(&kp)[3], const KvPiece<TKV>(&vp)[3]) {
+    const bool valid = kb + kq < k1;
     float kf[24], vf[24];
-    if (valid) {
 #pragma unroll
-      for (int i = 0; i < 3; ++i) { kp[i].get(kf + 8 * i); vp[i].get(vf + 8 * i); }
-    }
-    if (kb + ATK < k1) issue(kb + ATK);
+    for (int i = 0; i < 3; ++i) { kp[i].get(kf + 8 * i); vp[i].get(vf + 8 * i); }
     float sc = 0.f;
-    if (valid) {
 #pragma unroll
-      for (int i = 0; i < 24; ++i) sc = fmaf(q[i], kf[i], sc);
-    }
+    for (int i = 0; i < 24; ++i) sc = fmaf(q[i], kf[i], sc);
     sc += __shfl_xor(sc, 1, 64);
     sc += __shfl_xor(sc, 2, 64);
     if (!valid) sc = -INFINITY;
     const float mn = fmaxf(m, wave_max(sc));
-    if (mn == -INFINITY) continue;  // this wave has no key in this tile yet (wave-uniform)
+    if (mn == -INFINITY) return;  // this wave has no key in this tile yet (wave-uniform)
     const float alpha = (m == -INFINITY) ? 0.f : expf(m - mn);
     const float p = valid ? expf(sc - mn) : 0.f;
     l = l * alpha + wave_sum(part == 0 ? p : 0.f);
 #pragma unroll
     for (int i = 0; i < 24; ++i) o[i] = fmaf(valid ? p : 0.f, valid ? vf[i] : 0.f, o[i] * alpha);
     m = mn;
+  };
+  issue(k0, kp0, vp0);
+  issue(k0 + ATK, kp1, vp1);
+  for (int kb = k0; kb < k1; kb += 2 * ATK) {
+    tile(kb, kp0, vp0);
+    issue(kb + 2 * ATK, kp0, vp0);
+    if (kb + ATK >= k1) break;
+    tile(kb + ATK, kp1, vp1);
+    issue(kb + 3 * ATK, kp1, vp1);
   }
   // sum o over the 16 key slots of the wave (lanes with equal part)
 #pragma unroll
@@ -1734,9 +1738,11 @@ static void launch_bt(const GemvArgs& a, int ns_max, hipStream_t s) {
   else hipLaunchKernelGGL((ar_bt_kernel<K, 4, IN, OUT>), grid, block, 0, s, a, ns_max);
 }
 
+int g_opt_attn_blocks = 512;  // split count target: ns * 8 heads * B <= this (batched paths); measured
+// (tools/step_sweep.py, us/step): B = 32 at t < 256: 1024 -> 164, 512 -> 155, 256 -> 152; B = 8: 144 / 135
 static int attn_ns_max(int B) {  // enough splits to fill the chip, no more (early-exit blocks cost)
   int ns = NSPLIT;
-  while (ns > 1 && ns * N_HEAD * B > 1024) ns >>= 1;
+  while (ns > 1 && ns * N_HEAD * B > g_opt_attn_blocks) ns >>= 1;
   return ns;
 }
 
