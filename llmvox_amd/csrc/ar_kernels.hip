@@ -1384,15 +1384,21 @@ static void launch_merge_bf16(const ArState& st, int B, int nsm, hipStream_t s) 
 
 // OUT as gemv_store, plus OUT 5: h (bf16) = gelu_tanh(v) for the batched mlp c_proj. A block
 // covers K columns starting at blockIdx.y * K of rows of length KTOT (KTOT > K: split K, OUT 6).
-template <int K, int NT, int OUT, int KTOT = K>
-__global__ __launch_bounds__(1024) void ar_mfma2_kernel(GemvArgs a) {
+// XM 1 (c_fc, option ln_stats): the operand is LayerNorm(x) built on the fly from the bf16 copy of
+// x and the per-row statistics the previous c_proj (OUT 7) left in 48 column-block partials
+// (mean, M2 over 16 columns each, combined here with Chan's formula): no separate rows kernel.
+// OUT 7 (c_proj): x += v, plus that bf16 copy and this block's (mean, M2) of its 16 columns.
+template <int K, int NT, int OUT, int KTOT = K, int XM = 0>
+__global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   constexpr int NW = K / 192;  // waves per block, each a 192-wide K slice (6 MFMA k-steps)
   __shared__ float red[NW][NT * 256];
+  __shared__ float xo[OUT == 7 ? 16 * NT * 16 : 1];
+  __shared__ float2 rs[XM == 1 ? NT * 16 : 1];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int n0 = blockIdx.x * 16;
   const int B = a.B;
   const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(a.W);
-  const bf16_t* __restrict__ X = (KTOT == 768) ? a.st.xn : a.st.hb;
+  const bf16_t* __restrict__ X = XM == 1 ? a.st.xb : ((KTOT == 768) ? a.st.xn : a.st.hb);
   const int wrow = min(n0 + (lane & 15), a.N - 1);
   const int k0 = blockIdx.y * K + wave * 192 + 8 * (lane >> 4);
   uint4 wf[6], xf[NT][6];
@@ -1403,6 +1409,57 @@ __global__ __launch_bounds__(1024) void ar_mfma2_kernel(GemvArgs a) {
     const int b = min(t * 16 + (lane & 15), B - 1);  // padded columns recompute row B-1, never stored
 #pragma unroll
     for (int kk = 0; kk < 6; ++kk) xf[t][kk] = *reinterpret_cast<const uint4*>(X + (size_t)b * KTOT + k0 + kk * 32);
+  }
+  if constexpr (XM == 1) {
+    float4 g[6][2];
+#pragma unroll
+    for (int kk = 0; kk < 6; ++kk) {
+      g[kk][0] = *reinterpret_cast<const float4*>(a.ln_w + k0 + kk * 32);
+      g[kk][1] = *reinterpret_cast<const float4*>(a.ln_w + k0 + kk * 32 + 4);
+    }
+    if (tid < NT * 16 * 4) {  // 4 lanes per row, 12 column blocks each, all loads issued at once
+      const int rr = tid >> 2, q = tid & 3;
+      const int b = min(rr, B - 1);
+      const float2* xs = reinterpret_cast<const float2*>(a.st.xstat) + (size_t)b * (D / 16) + q * 12;
+      float2 p[12];
+#pragma unroll
+      for (int j = 0; j < 12; ++j) p[j] = xs[j];
+      float mean = 0.f, m2 = 0.f;  // Chan's combine of equal-count (16) groups, in a fixed order
+#pragma unroll
+      for (int j = 0; j < 12; ++j) {
+        const float d = p[j].x - mean, w = 1.0f / (j + 1);
+        mean = mean + d * w;
+        m2 = m2 + p[j].y + d * d * (16.0f * j * w);
+      }
+#pragma unroll
+      for (int o = 1; o < 4; o <<= 1) {  // pairs of equal counts n: M2 += (mb - ma)^2 n / 2
+        const float mb = __shfl_xor(mean, o, 64), m2b = __shfl_xor(m2, o, 64);
+        const float d = mb - mean;
+        const float n = 192.0f * o;
+        m2 = m2 + m2b + d * d * (n * 0.5f);
+        mean = (mean + mb) * 0.5f;  // symmetric: both lanes of the pair hold the same result
+      }
+      if (q == 0) rs[rr] = make_float2(mean, 1.0f / sqrtf(m2 * (1.0f / D) + 1e-5f));
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const float2 st = rs[t * 16 + (lane & 15)];
+#pragma unroll
+      for (int kk = 0; kk < 6; ++kk) {
+        const uint4 u = xf[t][kk];
+        const float gv[8] = {g[kk][0].x, g[kk][0].y, g[kk][0].z, g[kk][0].w, g[kk][1].x, g[kk][1].y, g[kk][1].z, g[kk][1].w};
+        const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+        uint32_t o4[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float lo = (__uint_as_float(w4[q] << 16) - st.x) * st.y * gv[2 * q];
+          const float hi = (__uint_as_float(w4[q] & 0xffff0000u) - st.x) * st.y * gv[2 * q + 1];
+          o4[q] = (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+        }
+        xf[t][kk] = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+      }
+    }
   }
   f32x4_t acc[NT];
 #pragma unroll
@@ -1425,17 +1482,42 @@ __global__ __launch_bounds__(1024) void ar_mfma2_kernel(GemvArgs a) {
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) v += red[w][e];
-    if (OUT == 5) a.st.hb[(size_t)b * DFF + n] = f32_to_bf16(gelu_tanh(v));
-    else gemv_store<OUT>(a, n, b, v);
+    if (OUT == 5) {
+      a.st.hb[(size_t)b * DFF + n] = f32_to_bf16(gelu_tanh(v));
+    } else if (OUT == 7) {
+      const float xn = a.st.x[(size_t)b * D + n] + v;
+      a.st.x[(size_t)b * D + n] = xn;
+      a.st.xb[(size_t)b * D + n] = f32_to_bf16(xn);
+      xo[e] = xn;
+    } else {
+      gemv_store<OUT>(a, n, b, v);
+    }
+  }
+  if constexpr (OUT == 7) {  // (mean, M2) of this block's 16 columns for every batch row
+    __syncthreads();
+    if (tid < NT * 16 && tid < B) {
+      float mean = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mean += xo[r * (NT * 16) + tid];
+      mean *= 1.0f / 16;
+      float m2 = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float d = xo[r * (NT * 16) + tid] - mean;
+        m2 += d * d;
+      }
+      reinterpret_cast<float2*>(a.st.xstat)[(size_t)tid * (D / 16) + blockIdx.x] = make_float2(mean, m2);
+    }
   }
 }
 
-template <int K, int OUT>
+template <int K, int OUT, int XM = 0>
 static void launch_mfma2(const GemvArgs& a, hipStream_t s) {
   dim3 grid((a.N + 15) / 16), block((K / 192) * 64);
-  if (a.B <= 16) hipLaunchKernelGGL((ar_mfma2_kernel<K, 1, OUT>), grid, block, 0, s, a);
-  else hipLaunchKernelGGL((ar_mfma2_kernel<K, 2, OUT>), grid, block, 0, s, a);
+  if (a.B <= 16) hipLaunchKernelGGL((ar_mfma2_kernel<K, 1, OUT, K, XM>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((ar_mfma2_kernel<K, 2, OUT, K, XM>), grid, block, 0, s, a);
 }
+int g_opt_ln_stats = 1;  // batched v2: c_fc normalises from c_proj's row statistics (no rows kernel)
 
 // mlp c_proj (K = 3072) split into YCOPIES K slices of 768: 4x the blocks of the unsplit GEMM;
 // each slice's partial goes to its pending copy (plain stores, deterministic), folded into x by
@@ -1850,7 +1932,8 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       if (mf) {
         if (B > g_opt_mfma_ln) a.add_y = 0;  // ar_rows_kernel<4> of this layer's c_attn folded them
         launch_merge_bf16(a.st, B, nsm, s);
-        launch_mfma2<768, 1>(a, s);
+        if (B > g_opt_mfma_ln && g_opt_ln_stats) launch_mfma2<768, 7>(a, s);  // + bf16 x and row stats
+        else launch_mfma2<768, 1>(a, s);
       } else {
         launch_gemv<TW, 768, 1, 1, 2, 1>(a, s);
       }
@@ -1869,6 +1952,8 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
         }
       } else if (mf && B <= g_opt_mfma_ln) {
         launch_mfma_ln<5, 0>(a, s);
+      } else if (mf && g_opt_ln_stats) {
+        launch_mfma2<768, 5, 1>(a, s);  // LayerNorm from c_proj's statistics in the prologue
       } else if (mf) {
         hipLaunchKernelGGL((ar_rows_kernel<0>), dim3(B), dim3(64), 0, s, a);
         launch_mfma2<768, 5>(a, s);

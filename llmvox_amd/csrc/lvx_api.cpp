@@ -413,6 +413,7 @@ int lvx_finalize(lvx_ctx* c) {
       (r = c->dalloc(&st.part_ml, (size_t)S * N_HEAD * NSPLIT * 2)) || (r = c->dalloc(&st.h, (size_t)S * DFF)) ||
       (r = c->dalloc(&st.logits, (size_t)S * VOCAB)) || (r = c->dalloc(&st.rowinfo, S)) ||
       (r = c->dalloc(&st.xn, (size_t)S * D)) || (r = c->dalloc(&st.hb, (size_t)S * DFF)) ||
+      (r = c->dalloc(&st.xb, (size_t)S * D)) || (r = c->dalloc(&st.xstat, (size_t)(D / 16) * S * 2)) ||
       (r = c->dalloc(&st.lmbest, (size_t)LM_MAX_BLOCKS * 4 * 2)) || (r = c->dalloc(&st.ticket, 4)) ||
       (r = c->dalloc(&st.yacc, (size_t)YCOPIES * S * D)))
     return r;
@@ -529,6 +530,7 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   else if (n == "codec_g2_min") g_opt_codec_g2_min = value;
   else if (n == "codec_xcd") g_opt_codec_xcd = value;
   else if (n == "attn_blocks") g_opt_attn_blocks = value;
+  else if (n == "ln_stats") g_opt_ln_stats = value;
   else return fail(LVX_E_NAME, "unknown option " + n);
   for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);  // captured kernels change
   c->graphs.clear();

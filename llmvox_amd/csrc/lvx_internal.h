@@ -18,7 +18,7 @@ constexpr int NSPLIT = 16;  // max KV splits per (stream, head) in decode attent
 constexpr int YCOPIES = LVX_YCOPIES;  // accumulator copies of the fused MLP (spreads atomic contention)
 constexpr int LM_MAX_BLOCKS = 1024;  // lm_head blocks of the fused argmax tail (4096 rows / 8 per block = 512)
 extern int g_opt_gemv_reg, g_opt_attn_v2, g_opt_cproj_b1, g_opt_prefetch_in, g_opt_mfma_batch, g_opt_fuse_argmax,
-    g_opt_fuse_mlp, g_opt_mfma_ln, g_opt_bt, g_opt_bt_rows, g_opt_bt_merge, g_opt_codec_g2, g_opt_codec_g2_min, g_opt_codec_xcd, g_opt_attn_blocks;  // A/B switches (lvx_set_option)
+    g_opt_fuse_mlp, g_opt_mfma_ln, g_opt_bt, g_opt_bt_rows, g_opt_bt_merge, g_opt_codec_g2, g_opt_codec_g2_min, g_opt_codec_xcd, g_opt_attn_blocks, g_opt_ln_stats;  // A/B switches (lvx_set_option)
 
 // Device-resident AR weights. Matrices are [out][in] row-major (torch Linear layout),
 // in the context's weight dtype; vectors and gathered tables are fp32.
@@ -56,6 +56,8 @@ struct ArState {
   float* h = nullptr;           // [B][3072]
   bf16_t* xn = nullptr;         // [B][768] bf16 operand rows (batched path)
   bf16_t* hb = nullptr;         // [B][3072] bf16 h (batched path)
+  bf16_t* xb = nullptr;         // [B][768] bf16 copy of x after c_proj (batched path, option ln_stats)
+  float* xstat = nullptr;       // [max_streams][48 column blocks][2] (mean, M2) of x over 16 columns
   float* logits = nullptr;      // [B][4096]
   uint64_t* lmbest = nullptr;   // [LM_MAX_BLOCKS][4][2] per-block top1/top2 granules (fused lm_head + argmax)
   uint32_t* ticket = nullptr;   // [4] arrival counter of the fused lm_head (reset by its last block)
