@@ -1075,8 +1075,11 @@ __global__ __launch_bounds__(256) void ar_attn_kernel(ArState st, int layer) {
 // V pieces (48 B bf16 each) load straight to registers, the score needs two quad shuffles, and
 // every wave keeps its own online-softmax state (m, l, o[24] per lane) so the loop has no
 // barrier. The 4 wave states are merged once at the end through LDS.
+// direct = 1 (batched path with one split per (row, head)): the normalised head output goes
+// straight to the bf16 operand row xn, as the merge kernel would write it (o * (1 / l)), and the
+// merge kernel is skipped.
 template <typename TKV>
-__global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer, int ns_max) {
+__global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer, int ns_max, int direct) {
   __shared__ float wm_s[4], wl_s[4];
   __shared__ float wo_s[4][HD];
   const int sp = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
@@ -1173,6 +1176,10 @@ __global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer, 
       const float f = (wm_s[w] == -INFINITY) ? 0.f : expf(wm_s[w] - M);
       ov += f * wo_s[w][tid];
       lv += f * wl_s[w];
+    }
+    if (direct) {
+      st.xn[(size_t)b * D + head * HD + tid] = f32_to_bf16(ov * (1.0f / lv));
+      return;
     }
     st.part_o[((size_t)(b * N_HEAD + head) * NSPLIT + sp) * HD + tid] = ov;
     if (tid == 0) {
@@ -1820,20 +1827,23 @@ static void launch_bt(const GemvArgs& a, int ns_max, hipStream_t s) {
   else hipLaunchKernelGGL((ar_bt_kernel<K, 4, IN, OUT>), grid, block, 0, s, a, ns_max);
 }
 
-int g_opt_attn_blocks = 512;  // split count target: ns * 8 heads * B <= this (batched paths); measured
-// (tools/step_sweep.py, us/step): B = 32 at t < 256: 1024 -> 164, 512 -> 155, 256 -> 152; B = 8: 144 / 135
+int g_opt_attn_blocks = 256;  // split count target: ns * 8 heads * B <= this (batched paths); measured
+// (tools/step_sweep.py, us/step at t = 256-511): B = 32: 1024 -> 164, 512 -> 169, 256 (one split:
+// the attention writes xn directly, no merge kernel) -> 155.5; B = 16: 138 / 136 / 131 (128 blocks);
+// B = 8: 144 / 133 / 130
 static int attn_ns_max(int B) {  // enough splits to fill the chip, no more (early-exit blocks cost)
   int ns = NSPLIT;
   while (ns > 1 && ns * N_HEAD * B > g_opt_attn_blocks) ns >>= 1;
   return ns;
 }
 
-static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_t s, int ns_max = NSPLIT) {
-  if (g_opt_attn_v2 || kvdtype == LVX_DTYPE_FP8) {
+static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_t s, int ns_max = NSPLIT,
+                        int direct = 0) {
+  if (g_opt_attn_v2 || kvdtype == LVX_DTYPE_FP8 || direct) {
     dim3 grid(ns_max, N_HEAD, B);
-    if (kvdtype == LVX_DTYPE_BF16) hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t>), grid, dim3(256), 0, s, st, l, ns_max);
-    else if (kvdtype == LVX_DTYPE_FP8) hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t>), grid, dim3(256), 0, s, st, l, ns_max);
-    else hipLaunchKernelGGL((ar_attn_v2_kernel<float>), grid, dim3(256), 0, s, st, l, ns_max);
+    if (kvdtype == LVX_DTYPE_BF16) hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t>), grid, dim3(256), 0, s, st, l, ns_max, direct);
+    else if (kvdtype == LVX_DTYPE_FP8) hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t>), grid, dim3(256), 0, s, st, l, ns_max, direct);
+    else hipLaunchKernelGGL((ar_attn_v2_kernel<float>), grid, dim3(256), 0, s, st, l, ns_max, direct);
   } else {
     dim3 grid(NSPLIT, N_HEAD, B);
     if (kvdtype == LVX_DTYPE_BF16) hipLaunchKernelGGL((ar_attn_kernel<bf16_t>), grid, dim3(256), 0, s, st, l);
@@ -1926,12 +1936,12 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
         launch_gemv<TW, 768, 1, 2, 0, 0>(a, s);
       }
       break;
-    case 1: launch_attn(a.st, kvdtype, B, l, s, nsm); break;
+    case 1: launch_attn(a.st, kvdtype, B, l, s, nsm, mf && nsm == 1); break;
     case 2:
       a.W = w.w_aproj[l]; a.N = D;
       if (mf) {
         if (B > g_opt_mfma_ln) a.add_y = 0;  // ar_rows_kernel<4> of this layer's c_attn folded them
-        launch_merge_bf16(a.st, B, nsm, s);
+        if (nsm > 1) launch_merge_bf16(a.st, B, nsm, s);  // nsm == 1: the attention wrote xn itself
         if (B > g_opt_mfma_ln && g_opt_ln_stats) launch_mfma2<768, 7>(a, s);  // + bf16 x and row stats
         else launch_mfma2<768, 1>(a, s);
       } else {

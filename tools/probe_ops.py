@@ -19,4 +19,4 @@ for spec in sys.argv[3:] or [""]:
     tot = sum(v["share_us_per_step"] for v in r.values() if "share_us_per_step" in v)
     print(f"B={S} P={P} [{spec}] step~{tot:.1f} us: " + ", ".join(f"{v['name'].split(' ')[1] if ' ' in v['name'] else v['name']} {v['avg_us']:.2f}" for v in r.values()), flush=True)
     for k, v in opts:
-        e.set_option(k, {"bt": 1, "bt_rows": 16, "bt_merge": 0, "mfma_ln": 8, "attn_blocks": 512}.get(k, 0))
+        e.set_option(k, {"bt": 1, "bt_rows": 16, "bt_merge": 0, "mfma_ln": 8, "attn_blocks": 256}.get(k, 0))
