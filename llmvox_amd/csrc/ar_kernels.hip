@@ -1522,7 +1522,8 @@ template <int K, int OUT, int XM = 0>
 static void launch_mfma2(const GemvArgs& a, hipStream_t s) {
   dim3 grid((a.N + 15) / 16), block((K / 192) * 64);
   if (a.B <= 16) hipLaunchKernelGGL((ar_mfma2_kernel<K, 1, OUT, K, XM>), grid, block, 0, s, a);
-  else hipLaunchKernelGGL((ar_mfma2_kernel<K, 2, OUT, K, XM>), grid, block, 0, s, a);
+  else if (a.B <= 32) hipLaunchKernelGGL((ar_mfma2_kernel<K, 2, OUT, K, XM>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((ar_mfma2_kernel<K, 4, OUT, K, XM>), grid, block, 0, s, a);
 }
 int g_opt_ln_stats = 1;  // batched v2: c_fc normalises from c_proj's row statistics (no rows kernel)
 
@@ -1533,7 +1534,8 @@ static void launch_mproj_split(const GemvArgs& a, hipStream_t s) {
   static_assert(DFF == YCOPIES * 768, "one pending copy per K slice");
   dim3 grid((a.N + 15) / 16, YCOPIES), block(256);
   if (a.B <= 16) hipLaunchKernelGGL((ar_mfma2_kernel<768, 1, 6, DFF>), grid, block, 0, s, a);
-  else hipLaunchKernelGGL((ar_mfma2_kernel<768, 2, 6, DFF>), grid, block, 0, s, a);
+  else if (a.B <= 32) hipLaunchKernelGGL((ar_mfma2_kernel<768, 2, 6, DFF>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((ar_mfma2_kernel<768, 4, 6, DFF>), grid, block, 0, s, a);
 }
 
 // Batched GEMM with the per-row prologue fused (K = 768; small B): every block builds the
@@ -1862,7 +1864,7 @@ static bool use_bt(int B) {
 
 template <typename TW>
 static bool use_mfma(int B) {
-  return sizeof(TW) == 2 && g_opt_mfma_batch && B >= g_opt_mfma_batch && (B <= 32 || use_bt<TW>(B));
+  return sizeof(TW) == 2 && g_opt_mfma_batch && B >= g_opt_mfma_batch && B <= 64;
 }
 
 // batched path v3: one kernel per op (plus the attention), final x rows at every boundary

@@ -85,7 +85,7 @@ def test_rows_are_independent_of_batch_position(eng, B):
     np.testing.assert_array_equal(lg_a, lg_b)
 
 
-@pytest.mark.parametrize("B", [8, 32])
+@pytest.mark.parametrize("B", [8, 32, 48])
 def test_v3_close_to_v2_batched_path(eng, B):
     """Same v3 prefix (ragged, multi-split attention), then one step on v3 vs on the v2 path."""
     texts = _texts(B, 80, seed=3)
