@@ -12,6 +12,7 @@ reference checkout):
 * streaming policy:   configs/inference_config.py:30-41.
 """
 from dataclasses import dataclass, field
+from typing import Optional
 
 # ---- speech-token GPT (src/model.py:135-146, configs/train_config.py:70-75) ----
 N_LAYER = 4
@@ -65,6 +66,7 @@ class InferenceConfig:
       weights        "synthetic" (seeded, reference init scales) or "checkpoint".
       weight_dtype   "fp32" (parity mode, the reference runs fp32) or "bf16".
       kv_dtype       "fp32" | "bf16" | "fp8" (OCP e4m3fn KV cache).
+      codec_dtype    None (the weight dtype) | "fp8" (e4m3fn codec weights, per-row scales; bf16 mode).
       max_streams    KV slots per device.
       max_positions  KV capacity per slot (<= block_size 8192).
       seed           seed of the synthetic weights.
@@ -86,6 +88,7 @@ class InferenceConfig:
     weights: str = "synthetic"
     weight_dtype: str = "fp32"
     kv_dtype: str = "fp32"
+    codec_dtype: Optional[str] = None
     max_streams: int = 8
     max_positions: int = BLOCK_SIZE
     max_codec_frames: int = MAX_DUMP_SIZE

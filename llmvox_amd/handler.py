@@ -161,7 +161,7 @@ class ModelHandler:
     """``ModelHandler(config, device_id)`` (inference/model_handler.py:48-63).
 
     ``config`` is the reference's dict plus: weights "synthetic" | "checkpoint",
-    weight_dtype "fp32" | "bf16", kv_dtype, max_streams, max_positions, seed."""
+    weight_dtype "fp32" | "bf16", kv_dtype, codec_dtype (None | "fp8"), max_streams, max_positions, seed."""
 
     def __init__(self, config, device_id: Optional[int] = None):
         self.config = config
@@ -171,7 +171,7 @@ class ModelHandler:
         get = config.get if hasattr(config, "get") else (lambda k, d=None: getattr(config, k, d))
         self.engine = Engine(dev, get("weight_dtype", "fp32"), get("kv_dtype", "fp32"),
                              int(get("max_streams", 8)), int(get("max_positions", C.BLOCK_SIZE)),
-                             int(get("max_codec_frames", C.MAX_DUMP_SIZE)))
+                             int(get("max_codec_frames", C.MAX_DUMP_SIZE)), get("codec_dtype", None))
         self.device = self.engine.device
         src = get("weights", "synthetic")
         if src == "synthetic":
