@@ -268,7 +268,7 @@ static void gemm_launch(GemmArgs g, int batch, hipStream_t s) {
 // or implicit-Conv1d. TC = output type of the plain epilogue (bf16 for the GELU output that only
 // feeds the next GEMM). Rows of every tile are whole 128-B runs: coalesced loads and stores.
 // ---------------------------------------------------------------------------------
-constexpr int G2_BM = 128, G2_BN = 128, G2_BK = 64, G2_LDK = G2_BK + 8;  // bf16 row stride 144 B
+constexpr int G2_BN = 128, G2_BK = 64, G2_LDK = G2_BK + 8;  // bf16 row stride 144 B
 
 template <typename TB> struct BLoad;
 template <> struct BLoad<bf16_t> {  // 4 x 8 bf16 per thread per tile
@@ -302,9 +302,13 @@ template <> struct ALoad<float> {  // 8 x 16 B per thread per tile
 };
 
 
-template <typename TA, typename TB, int AMODE, int EPI, typename TC>
-__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) bf16_t As[2][G2_BM * G2_LDK];
+// BMt = 128: 4 waves of 64 x 64 (2 x 2 MFMA tiles), 2 blocks per CU. BMt = 256: 4 waves of 128 x 64
+// (4 x 2), one block per CU: 0.75 LDS fragment reads per MFMA instead of 1 (the LDS read rate of a
+// 64 x 64 wave tile equals the MFMA rate).
+template <typename TA, typename TB, int AMODE, int EPI, typename TC, int BMt>
+__global__ __launch_bounds__(256, BMt == 128 ? 2 : 1) void gemm_bf16_kernel(GemmArgs g) {
+  constexpr int WMt = BMt / 2, MI = WMt / 32;  // rows per wave, 32-row MFMA tiles per wave
+  __shared__ __attribute__((aligned(16))) bf16_t As[2][BMt * G2_LDK];
   __shared__ __attribute__((aligned(16))) bf16_t Bs[2][G2_BN * G2_LDK];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 1, wn = wave & 1;
@@ -320,7 +324,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
   const int gsz = G2_GM * ntn, grp = q / gsz, within = q - grp * gsz;
   const int gm = min(G2_GM, ntm - grp * G2_GM);
   const int tm = grp * G2_GM + within % gm, tn = within / gm;
-  const int m0 = tm * G2_BM, n0 = tn * G2_BN;
+  const int m0 = tm * BMt, n0 = tn * G2_BN;
   const int ks = blockIdx.z;
   const TA* __restrict__ A = reinterpret_cast<const TA*>(g.A);
   const TB* __restrict__ W = reinterpret_cast<const TB*>(g.W);
@@ -329,7 +333,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
   const int kt0 = ks * kt_per, kt1 = min(nkt, kt0 + kt_per);
   // loader geometry: chunk c = tid + 256 i covers row c / ACH, 16-B segment c % ACH
   constexpr int ACH = sizeof(TA) == 2 ? 8 : 16;  // 16-B chunks per A row of the tile
-  constexpr int AN = G2_BM * ACH / 256;           // chunks per thread (4 bf16 / 8 fp32)
+  constexpr int AN = BMt * ACH / 256;             // chunks per thread
   constexpr int AROWS = 256 / ACH;                // rows covered per i step
   const int arow0 = tid / ACH, aseg = (tid % ACH) * (16 / (int)sizeof(TA));
   // implicit conv: (stream, frame) of this thread's first row; later rows are +AROWS frames
@@ -378,9 +382,9 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
     }                                                                                                      \
   }
 
-  f32x16 acc[2][2];
+  f32x16 acc[MI][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -392,12 +396,12 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
     const bf16_t* as = As[buf];                                                                            \
     const bf16_t* bs = Bs[buf];                                                                            \
     _Pragma("unroll") for (int kk = 0; kk < G2_BK; kk += 16) {                                             \
-      bf16x8 fa[2], fb[2];                                                                                 \
-      _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                                      \
-        fa[i] = *reinterpret_cast<const bf16x8*>(as + (wm * 64 + i * 32 + (lane & 31)) * G2_LDK + kk + 8 * (lane >> 5)); \
-        fb[i] = *reinterpret_cast<const bf16x8*>(bs + (wn * 64 + i * 32 + (lane & 31)) * G2_LDK + kk + 8 * (lane >> 5)); \
-      }                                                                                                    \
+      bf16x8 fa[MI], fb[2];                                                                                \
+      _Pragma("unroll") for (int i = 0; i < MI; ++i)                                                       \
+        fa[i] = *reinterpret_cast<const bf16x8*>(as + (wm * WMt + i * 32 + (lane & 31)) * G2_LDK + kk + 8 * (lane >> 5)); \
       _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                        \
+        fb[i] = *reinterpret_cast<const bf16x8*>(bs + (wn * 64 + i * 32 + (lane & 31)) * G2_LDK + kk + 8 * (lane >> 5)); \
+      _Pragma("unroll") for (int i = 0; i < MI; ++i)                                                       \
       _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                        \
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);              \
     }                                                                                                      \
@@ -438,17 +442,17 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
     if constexpr (sizeof(TB) == 1) {  // fp8 weights: per-row dequantisation scale
       const float sc = g.wscale[col];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] *= sc;
     }
     if (g.ksplit > 1) {
       float* P = g.ws + (size_t)ks * g.M * g.N;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const int row = m0 + wm * WMt + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
           if (row < g.M) P[(size_t)row * g.N + col] = acc[i][j][r];
         }
       continue;
@@ -457,19 +461,19 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
     const float bias = (EPI != E_SCALE && g.bias) ? g.bias[col] : 0.f;
     const float gam = (EPI == E_BIAS_GAMMA_RES) ? g.gamma[col] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < MI; ++i) {
       // residual operands first, all 16 in flight (rows clamped: loads never sit under a branch)
       float rv[16];
       if constexpr (EPI == E_BIAS_GAMMA_RES || EPI == E_BIAS_RES) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = min(m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), g.M - 1);
+          const int row = min(m0 + wm * WMt + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), g.M - 1);
           rv[r] = g.res[(size_t)row * g.ldr + col];
         }
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int row = m0 + wm * WMt + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         const float v = acc[i][j][r] + bias;
         float o;
         if constexpr (EPI == E_BIAS) o = v;
@@ -501,22 +505,30 @@ int g_opt_codec_g2 = 1;       // large-M bf16 GEMM (gemm_bf16_kernel) on/off
 int g_opt_codec_xcd = 1;      // its XCD-aware tile order
 int g_opt_codec_g2_min = 128;  // smallest M that takes it (measured: M = 256 0.86 vs 1.04 ms, M = 10 0.64 vs 0.59)
 
+// 256-row tiles when (M/256) x (N/128) tiles >= this (one block per CU); 0: off. Measured slower
+// (tools/codec_sweep.py, 32 x 256 frames: 3.51 vs 2.99 ms; 64 x 256: 7.04 vs 5.16 ms): one resident
+// block per CU exposes the load latency that two 128-row blocks hide for each other.
+int g_opt_codec_bm256 = 0;
+
 template <typename TA, typename TB, int AMODE, int EPI, typename TC>
 static void gemm2_launch(GemmArgs g, hipStream_t s) {
-  const int tiles = ((g.N + G2_BN - 1) / G2_BN) * ((g.M + G2_BM - 1) / G2_BM);
+  // 256-row tiles when there are enough of them to keep every CU busy (one block per CU)
+  const bool big = g_opt_codec_bm256 > 0 && (size_t)((g.M + 255) / 256) * ((g.N + G2_BN - 1) / G2_BN) >= (size_t)g_opt_codec_bm256;
+  const int BMr = big ? 256 : 128;
+  const int tiles = ((g.N + G2_BN - 1) / G2_BN) * ((g.M + BMr - 1) / BMr);
   const int nkt = g.K / G2_BK;
   int ks = 1;
   while (tiles * ks * 2 <= 512 && nkt / (ks * 2) >= 4 && (size_t)(ks * 2) * g.M * g.N <= g_ws_floats) ks *= 2;
   g.ksplit = ks;
   g.xcd_remap = g_opt_codec_xcd;
-  dim3 grid((g.N + G2_BN - 1) / G2_BN, (g.M + G2_BM - 1) / G2_BM, ks);
-  hipLaunchKernelGGL((gemm_bf16_kernel<TA, TB, AMODE, EPI, TC>), grid, dim3(256), 0, s, g);
+  dim3 grid((g.N + G2_BN - 1) / G2_BN, (g.M + BMr - 1) / BMr, ks);
+  if (big) hipLaunchKernelGGL((gemm_bf16_kernel<TA, TB, AMODE, EPI, TC, 256>), grid, dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((gemm_bf16_kernel<TA, TB, AMODE, EPI, TC, 128>), grid, dim3(256), 0, s, g);
   if (ks > 1) {
     const int blocks = (int)std::min<size_t>(((size_t)g.M * g.N + 255) / 256, 2048);
     hipLaunchKernelGGL((gemm2_splitk_reduce<EPI, TC>), dim3(blocks), dim3(256), 0, s, g);
   }
 }
-
 
 // weight GEMMs: bf16 weights -> bf16 MFMA (gemm_bf16_kernel for large M); fp32 weights -> exact
 // fp32 MFMA (parity mode). TA / TC: activation types of the operand / output (bf16 only in bf16 mode)
