@@ -1525,7 +1525,11 @@ static void launch_mfma2(const GemvArgs& a, hipStream_t s) {
   else if (a.B <= 32) hipLaunchKernelGGL((ar_mfma2_kernel<K, 2, OUT, K, XM>), grid, block, 0, s, a);
   else hipLaunchKernelGGL((ar_mfma2_kernel<K, 4, OUT, K, XM>), grid, block, 0, s, a);
 }
-int g_opt_ln_stats = 1;  // batched v2: c_fc normalises from c_proj's row statistics (no rows kernel)
+// batched v2: 1 = c_fc normalises from c_proj's row statistics (no rows kernel before c_fc);
+// 2 = also c_attn / lm_head from an unsplit mlp c_proj's statistics (no rows kernels at all):
+// measured slower (B = 32: 178 vs 156 us/step, B = 16: 144 vs 134): the unsplit K = 3072 GEMM (48
+// blocks of 16 waves) costs more than the two rows kernels it removes
+int g_opt_ln_stats = 1;
 
 // mlp c_proj (K = 3072) split into YCOPIES K slices of 768: 4x the blocks of the unsplit GEMM;
 // each slice's partial goes to its pending copy (plain stores, deterministic), folded into x by
@@ -1926,6 +1930,8 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       if (mf && B <= g_opt_mfma_ln) {
         if (l == 0) launch_mfma_ln<0, 3>(a, s);
         else launch_mfma_ln<0, 4>(a, s);
+      } else if (mf && l > 0 && g_opt_ln_stats == 2) {
+        launch_mfma2<768, 0, 1>(a, s);  // LN1 from the previous mlp c_proj's statistics
       } else if (mf) {
         if (l == 0) hipLaunchKernelGGL((ar_rows_kernel<3>), dim3(B), dim3(64), 0, s, a);
         else hipLaunchKernelGGL((ar_rows_kernel<4>), dim3(B), dim3(64), 0, s, a);
@@ -1976,13 +1982,16 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
     case 4:
       a.W = w.w_mproj[l]; a.N = D;
       if (fm) return false;
-      if (mf) launch_mproj_split(a, s);
+      if (mf && B > g_opt_mfma_ln && g_opt_ln_stats == 2) launch_mfma2<DFF, 7>(a, s);  // final x + stats
+      else if (mf) launch_mproj_split(a, s);
       else launch_gemv<TW, 3072, 4, 2, 1, 1>(a, s);
       break;
     case 5:
       a.W = w.w_lm; a.N = VOCAB; a.ln_w = w.lnf;
       if (mf && B <= g_opt_mfma_ln) {
         launch_mfma_ln<3, 4>(a, s);
+      } else if (mf && g_opt_ln_stats == 2) {
+        launch_mfma2<768, 3, 1>(a, s);  // ln_f from the last mlp c_proj's statistics
       } else if (mf) {
         hipLaunchKernelGGL((ar_rows_kernel<4>), dim3(B), dim3(64), 0, s, a);
         launch_mfma2<768, 3>(a, s);
