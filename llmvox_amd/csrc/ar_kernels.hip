@@ -1399,7 +1399,7 @@ template <int K, int NT, int OUT, int KTOT = K, int XM = 0>
 __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   constexpr int NW = K / 192;  // waves per block, each a 192-wide K slice (6 MFMA k-steps)
   __shared__ float red[NW][NT * 256];
-  __shared__ float xo[OUT == 7 ? 16 * NT * 16 : 1];
+  __shared__ float xo[(OUT == 7 || OUT == 8) ? 16 * NT * 16 : 1];
   __shared__ float2 rs[XM == 1 ? NT * 16 : 1];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int n0 = blockIdx.x * 16;
@@ -1496,11 +1496,45 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
       a.st.x[(size_t)b * D + n] = xn;
       a.st.xb[(size_t)b * D + n] = f32_to_bf16(xn);
       xo[e] = xn;
+    } else if (OUT == 8) {  // K-slice slab of the split mlp c_proj (reduced by the tile's last arriver)
+      a.yacc[((size_t)blockIdx.y * a.st.max_streams + b) * D + n] = v;
     } else {
       gemv_store<OUT>(a, n, b, v);
     }
   }
-  if constexpr (OUT == 7) {  // (mean, M2) of this block's 16 columns for every batch row
+  if constexpr (OUT == 8) {
+    // In-launch split-K combine (cdna_hip_programming.md, "Projection GEMM at M = 256" item 2, the
+    // Guideline 16 counter form): slabs drained, agent release, ticket; the tile's last arriving
+    // slice acquires, sums the slabs in slice order (deterministic), adds the residual and leaves
+    // final x + its bf16 copy + the column statistics, so the next LayerNorm needs no rows kernel.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned tk = __hip_atomic_fetch_add(a.st.tick + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool last = tk == gridDim.y - 1;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(a.st.tick + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      red[0][0] = last ? 1.f : 0.f;
+    }
+    __syncthreads();
+    if (red[0][0] == 0.f) return;
+    for (int e = tid; e < 16 * NT * 16; e += NW * 64) {
+      const int r = e / (NT * 16), b = e - r * (NT * 16), n = n0 + r;
+      if (b >= B) continue;
+      float t = a.st.x[(size_t)b * D + n];
+#pragma unroll
+      for (int c = 0; c < YCOPIES; ++c) t += a.yacc[((size_t)c * a.st.max_streams + b) * D + n];
+      a.st.x[(size_t)b * D + n] = t;
+      a.st.xb[(size_t)b * D + n] = f32_to_bf16(t);
+      xo[e] = t;
+    }
+  }
+  if constexpr (OUT == 7 || OUT == 8) {  // (mean, M2) of this block's 16 columns for every batch row
     __syncthreads();
     if (tid < NT * 16 && tid < B) {
       float mean = 0.f;
@@ -1528,18 +1562,21 @@ static void launch_mfma2(const GemvArgs& a, hipStream_t s) {
 // batched v2: 1 = c_fc normalises from c_proj's row statistics (no rows kernel before c_fc);
 // 2 = also c_attn / lm_head from an unsplit mlp c_proj's statistics (no rows kernels at all):
 // measured slower (B = 32: 178 vs 156 us/step, B = 16: 144 vs 134): the unsplit K = 3072 GEMM (48
-// blocks of 16 waves) costs more than the two rows kernels it removes
+// blocks of 16 waves) costs more than the two rows kernels it removes; 3 = the split mlp c_proj
+// with an in-launch combine by each column tile's last arriving slice (agent release / ticket /
+// acquire) leaving the statistics: also slower (B = 32: 182 vs 157, B = 16: 146 vs 137)
 int g_opt_ln_stats = 1;
 
 // mlp c_proj (K = 3072) split into YCOPIES K slices of 768: 4x the blocks of the unsplit GEMM;
 // each slice's partial goes to its pending copy (plain stores, deterministic), folded into x by
 // the next c_proj and read as x + sum of copies by the next c_attn / lm_head prologue
+template <int OUT>
 static void launch_mproj_split(const GemvArgs& a, hipStream_t s) {
   static_assert(DFF == YCOPIES * 768, "one pending copy per K slice");
   dim3 grid((a.N + 15) / 16, YCOPIES), block(256);
-  if (a.B <= 16) hipLaunchKernelGGL((ar_mfma2_kernel<768, 1, 6, DFF>), grid, block, 0, s, a);
-  else if (a.B <= 32) hipLaunchKernelGGL((ar_mfma2_kernel<768, 2, 6, DFF>), grid, block, 0, s, a);
-  else hipLaunchKernelGGL((ar_mfma2_kernel<768, 4, 6, DFF>), grid, block, 0, s, a);
+  if (a.B <= 16) hipLaunchKernelGGL((ar_mfma2_kernel<768, 1, OUT, DFF>), grid, block, 0, s, a);
+  else if (a.B <= 32) hipLaunchKernelGGL((ar_mfma2_kernel<768, 2, OUT, DFF>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((ar_mfma2_kernel<768, 4, OUT, DFF>), grid, block, 0, s, a);
 }
 
 // Batched GEMM with the per-row prologue fused (K = 768; small B): every block builds the
@@ -1930,7 +1967,7 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       if (mf && B <= g_opt_mfma_ln) {
         if (l == 0) launch_mfma_ln<0, 3>(a, s);
         else launch_mfma_ln<0, 4>(a, s);
-      } else if (mf && l > 0 && g_opt_ln_stats == 2) {
+      } else if (mf && l > 0 && g_opt_ln_stats >= 2) {
         launch_mfma2<768, 0, 1>(a, s);  // LN1 from the previous mlp c_proj's statistics
       } else if (mf) {
         if (l == 0) hipLaunchKernelGGL((ar_rows_kernel<3>), dim3(B), dim3(64), 0, s, a);
@@ -1983,14 +2020,15 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       a.W = w.w_mproj[l]; a.N = D;
       if (fm) return false;
       if (mf && B > g_opt_mfma_ln && g_opt_ln_stats == 2) launch_mfma2<DFF, 7>(a, s);  // final x + stats
-      else if (mf) launch_mproj_split(a, s);
+      else if (mf && B > g_opt_mfma_ln && g_opt_ln_stats == 3) launch_mproj_split<8>(a, s);  // + in-launch combine
+      else if (mf) launch_mproj_split<6>(a, s);
       else launch_gemv<TW, 3072, 4, 2, 1, 1>(a, s);
       break;
     case 5:
       a.W = w.w_lm; a.N = VOCAB; a.ln_w = w.lnf;
       if (mf && B <= g_opt_mfma_ln) {
         launch_mfma_ln<3, 4>(a, s);
-      } else if (mf && g_opt_ln_stats == 2) {
+      } else if (mf && g_opt_ln_stats >= 2) {
         launch_mfma2<768, 3, 1>(a, s);  // ln_f from the last mlp c_proj's statistics
       } else if (mf) {
         hipLaunchKernelGGL((ar_rows_kernel<4>), dim3(B), dim3(64), 0, s, a);

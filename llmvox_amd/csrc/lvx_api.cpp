@@ -414,11 +414,13 @@ int lvx_finalize(lvx_ctx* c) {
       (r = c->dalloc(&st.logits, (size_t)S * VOCAB)) || (r = c->dalloc(&st.rowinfo, S)) ||
       (r = c->dalloc(&st.xn, (size_t)S * D)) || (r = c->dalloc(&st.hb, (size_t)S * DFF)) ||
       (r = c->dalloc(&st.xb, (size_t)S * D)) || (r = c->dalloc(&st.xstat, (size_t)(D / 16) * S * 2)) ||
+      (r = c->dalloc(&st.tick, (size_t)(D / 16))) ||
       (r = c->dalloc(&st.lmbest, (size_t)LM_MAX_BLOCKS * 4 * 2)) || (r = c->dalloc(&st.ticket, 4)) ||
       (r = c->dalloc(&st.yacc, (size_t)YCOPIES * S * D)))
     return r;
   HIP_TRY(hipMemset(st.yacc, 0, (size_t)YCOPIES * S * D * 4));
   HIP_TRY(hipMemset(st.ticket, 0, 16));
+  HIP_TRY(hipMemset(st.tick, 0, (D / 16) * 4));
   HIP_TRY(hipMemset(st.part_o, 0, (size_t)S * N_HEAD * NSPLIT * HD * 4));
   HIP_TRY(hipMemset(st.part_ml, 0, (size_t)S * N_HEAD * NSPLIT * 2 * 4));
   HIP_TRY(hipMemset(st.pos, 0, S * 4));

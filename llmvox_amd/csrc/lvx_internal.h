@@ -58,6 +58,7 @@ struct ArState {
   bf16_t* hb = nullptr;         // [B][3072] bf16 h (batched path)
   bf16_t* xb = nullptr;         // [B][768] bf16 copy of x after c_proj (batched path, option ln_stats)
   float* xstat = nullptr;       // [max_streams][48 column blocks][2] (mean, M2) of x over 16 columns
+  uint32_t* tick = nullptr;     // [48] arrival tickets of the split mlp c_proj's in-launch combine (reset by the last arriver)
   float* logits = nullptr;      // [B][4096]
   uint64_t* lmbest = nullptr;   // [LM_MAX_BLOCKS][4][2] per-block top1/top2 granules (fused lm_head + argmax)
   uint32_t* ticket = nullptr;   // [4] arrival counter of the fused lm_head (reset by its last block)
