@@ -131,3 +131,27 @@ def test_merge_kernel_option_agrees(eng):
         eng.set_option("bt_merge", 0)
         eng.set_option("bt", eng.bt_mode)
     assert np.abs(lg_a - lg_b).max() < 0.01 * np.abs(lg_b).max()
+
+
+@pytest.mark.parametrize("opts", [{"ln_stats": 0}, {"ln_stats": 2}, {"ln_stats": 3}, {"attn_blocks": 1024},
+                                  {"codec_g2": 0}])
+def test_alternative_batched_options_agree(eng, opts):
+    """The A/B options of the batched path (kept for measurement) compute the same step: one step
+    after a shared ragged prefix, against the default path, within bf16 rounding."""
+    B = 32
+    texts = _texts(B, 80, seed=13)
+    order = list(range(B))
+    pre = set(range(0, B, 2))
+    eng.set_option("bt", 1)
+    _, ref = _run(eng, order, texts, pre, 40, 1)
+
+    def switch():
+        for k, v in opts.items():
+            eng.set_option(k, v)
+    try:
+        _, got = _run(eng, order, texts, pre, 40, 1, between=switch)
+    finally:
+        for k in opts:
+            eng.set_option(k, {"ln_stats": 1, "attn_blocks": 256, "codec_g2": 1}[k])
+        eng.set_option("bt", eng.bt_mode)
+    assert np.abs(got - ref).max() < 0.02 * np.abs(ref).max()
