@@ -703,7 +703,7 @@ __global__ __launch_bounds__(256) void ar_gemv_reg_kernel(GemvArgs a) {
 // (head, split) table BEFORE the weight rows; the per-head max / denominator are reduced over
 // the 16 lanes of each head with shuffles, the coefficients go through LDS once.
 // ---------------------------------------------------------------------------------
-template <typename TW, int RPW>
+template <typename TW, int RPW, int NS>
 __global__ __launch_bounds__(256) void ar_cproj_b1_kernel(GemvArgs a) {
   __shared__ float cf[N_HEAD * NSPLIT];
   __shared__ __attribute__((aligned(16))) float xs[D];
@@ -712,13 +712,13 @@ __global__ __launch_bounds__(256) void ar_cproj_b1_kernel(GemvArgs a) {
   // (m, l) of (head = tid / 16, split = tid % 16) and the 48 partials of this thread's 3 elements
   float2 ml = make_float2(-INFINITY, 0.f);
   if (tid < N_HEAD * NSPLIT) ml = reinterpret_cast<const float2*>(a.st.part_ml)[tid];
-  float pv[3][NSPLIT];
+  float pv[3][NS];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int e = tid + 256 * j, head = e / HD, d = e - head * HD;
     const float* po = a.st.part_o + ((size_t)head * NSPLIT) * HD + d;
 #pragma unroll
-    for (int i = 0; i < NSPLIT; ++i) pv[j][i] = po[(size_t)i * HD];
+    for (int i = 0; i < NS; ++i) pv[j][i] = po[(size_t)i * HD];
   }
   const int row0 = (blockIdx.x * 4 + wave) * RPW;
   // residual epilogue operands of lane r < RPW (row row0 + r): x and the fused MLP's accumulators
@@ -738,7 +738,7 @@ __global__ __launch_bounds__(256) void ar_cproj_b1_kernel(GemvArgs a) {
       wr[r][i] = (row0 + r < a.N) ? WReg<TW>::load(W + (size_t)(row0 + r) * D + i * 256 + lane * 4) : WReg<TW>::zero();
   if (tid < N_HEAD * NSPLIT) {
     const int t = ri.y + 1;
-    const int ns = ri.x < 0 ? 0 : min(NSPLIT, (t + 63) / 64);
+    const int ns = ri.x < 0 ? 0 : min(NS, (t + 63) / 64);
     const int sp = tid & (NSPLIT - 1);
     const bool on = sp < ns && ml.x != -INFINITY;
     float M = on ? ml.x : -INFINITY;
@@ -756,7 +756,7 @@ __global__ __launch_bounds__(256) void ar_cproj_b1_kernel(GemvArgs a) {
     const int e = tid + 256 * j, head = e / HD;
     float y = 0.f;
 #pragma unroll
-    for (int i = 0; i < NSPLIT; ++i) y += cf[head * NSPLIT + i] * pv[j][i];
+    for (int i = 0; i < NS; ++i) y += cf[head * NSPLIT + i] * pv[j][i];
     xs[e] = y;
   }
   __syncthreads();
@@ -1230,6 +1230,8 @@ __global__ __launch_bounds__(256) void ar_argmax_kernel(ArState st) {
 // host launchers
 // ---------------------------------------------------------------------------------
 int g_opt_gemv_reg = 0;  // runtime A/B switches (lvx_set_option); measured: LDS path faster at B=1
+int g_opt_b1_splits = 16;  // B = 1 attention splits per head (8 or 16; c_proj merges that many);
+// measured (us/step at t < 256 / t = 768-1023): 16: 86.9 / 89.3, 8: 85.1 / 90.3 -- a wash over an utterance
 int g_opt_attn_v2 = 1;
 int g_opt_cproj_b1 = 1;
 int g_opt_prefetch_in = 1;
@@ -1248,7 +1250,11 @@ static void launch_gemv(const GemvArgs& a, hipStream_t s) {
     return;
   }
   if constexpr (IN == 2 && OUT == 1 && K == 768 && KW == 1) {
-    if (g_opt_cproj_b1 && a.B == 1) { hipLaunchKernelGGL((ar_cproj_b1_kernel<TW, RPW>), grid, dim3(256), 0, s, a); return; }
+    if (g_opt_cproj_b1 && a.B == 1) {
+      if (g_opt_b1_splits <= 8) hipLaunchKernelGGL((ar_cproj_b1_kernel<TW, RPW, 8>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((ar_cproj_b1_kernel<TW, RPW, NSPLIT>), grid, dim3(256), 0, s, a);
+      return;
+    }
   }
   if constexpr (IN != 2) {
     if (g_opt_gemv_reg && a.B <= 1) { hipLaunchKernelGGL((ar_gemv_reg_kernel<TW, K, KW, RPW, 1, IN, OUT>), grid, dim3(256), 0, s, a); return; }
@@ -1957,7 +1963,7 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
   }
   const bool mf = use_mfma<TW>(B);
   const bool fm = fused_mlp<TW>(B);
-  const int nsm = mf ? attn_ns_max(B) : NSPLIT;
+  const int nsm = mf ? attn_ns_max(B) : (B == 1 && g_opt_cproj_b1 && g_opt_b1_splits <= 8 ? 8 : NSPLIT);
   a.layer = l;
   a.yacc = (fm || mf) ? a.st.yacc : nullptr;
   a.add_y = l > 0;

@@ -534,6 +534,7 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   else if (n == "attn_blocks") g_opt_attn_blocks = value;
   else if (n == "ln_stats") g_opt_ln_stats = value;
   else if (n == "codec_bm256") g_opt_codec_bm256 = value;
+  else if (n == "b1_splits") g_opt_b1_splits = value;
   else return fail(LVX_E_NAME, "unknown option " + n);
   for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);  // captured kernels change
   c->graphs.clear();
