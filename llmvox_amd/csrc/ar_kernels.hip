@@ -60,6 +60,8 @@ struct GemvArgs {
   // fused MLP (ar_mlp_fused_kernel): its output sits in YCOPIES accumulators until c_proj folds it in
   float* yacc;           // non-null when the step runs the fused MLP
   int add_y;             // c_proj: fold the accumulators into x (layers >= 1; 0 at layer 0 = just clear)
+  int defer_sel;         // deferred greedy select (B <= 2 GEMV step, option "defer_select"): lm_head
+                         // publishes per-block granules, the next step's c_attn layer 0 reduces them
 };
 
 // ---------------------------------------------------------------------------------
@@ -81,6 +83,12 @@ __device__ __forceinline__ Best best_merge(Best a, Best c) {
 
 __device__ __forceinline__ int4 make_rowinfo(const ArState& st, int b, int s, int p, int j, int prev);
 
+// text id of row b at plan step j (-1: past the end of the plan; PAD when no plan is bound)
+__device__ __forceinline__ int plan_tok(const ArState& st, int b, int j) {
+  if (!st.text_plan) return 384;
+  return (j < st.plan_stride) ? min(max(st.text_plan[(size_t)b * st.plan_stride + j], 0), TEXT_VOCAB - 1) : -1;
+}
+
 __device__ __forceinline__ void argmax_commit(const ArState& st, int b, int4 ri, Best r) {
   if (!st.rowstep) return;  // measurement probe: no plan bound, state is not advanced
   const int s = ri.x;
@@ -97,6 +105,33 @@ __device__ __forceinline__ void argmax_commit(const ArState& st, int b, int4 ri,
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
+typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
+
+// Deferred select: lm_head (OUT 9) leaves one 16-byte granule {index << 32 | top1 bits, top2 bits}
+// per (block, row) in st.lmbest; the next step's c_attn layer 0 (IN 5) or ar_select_final_kernel
+// reduces a row's 512 granules with one wave: every load in flight at once, then a shuffle tree.
+constexpr int LM_SEL_BLOCKS = VOCAB / 8;  // lm_head blocks on the B <= 2 GEMV path (8 rows each)
+struct LmGran {
+  u64x2_t g[LM_SEL_BLOCKS / 64];
+};
+__device__ __forceinline__ void lmg_issue(const ArState& st, int b, int lane, LmGran& q) {
+  const u64x2_t* base = reinterpret_cast<const u64x2_t*>(st.lmbest);
+#pragma unroll
+  for (int k = 0; k < LM_SEL_BLOCKS / 64; ++k) q.g[k] = base[(size_t)(lane + 64 * k) * 4 + b];
+}
+__device__ __forceinline__ Best lmg_reduce(const LmGran& q) {
+  Best r{-INFINITY, -INFINITY, 0x7fffffff};
+#pragma unroll
+  for (int k = 0; k < LM_SEL_BLOCKS / 64; ++k)
+    r = best_merge(r, Best{__uint_as_float((unsigned)q.g[k].x), __uint_as_float((unsigned)q.g[k].y),
+                           (int)(q.g[k].x >> 32)});
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Best c{__shfl_xor(r.v, o, 64), __shfl_xor(r.v2, o, 64), __shfl_xor(r.i, o, 64)};
+    r = best_merge(r, c);
+  }
+  return r;
+}
 
 // one K (which 0) or V (which 1) element of the KV cache in its dtype
 __device__ __forceinline__ void store_kv(const GemvArgs& a, int which, size_t idx, float v) {
@@ -184,7 +219,7 @@ template <int K, int IN>
 __device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, float* aux, int g0, int bg,
                                                  const XRow<IN == 4 ? 4 : 0>& xpre, int4 ripre, bool prefetched) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  if (IN == 0 || IN == 3 || IN == 4) {
+  if (IN == 0 || IN == 3 || IN == 4 || IN == 5) {
     for (int bb = wave; bb < bg; bb += 4) {  // one wave per row
       const int b = g0 + bb;
       const bool pre = prefetched && g0 == 0 && bb == wave;  // this row was prefetched before the weights
@@ -305,6 +340,7 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
   __shared__ __attribute__((aligned(16))) float xs[BG * K];
   __shared__ float part[4][RPW][BG];
   __shared__ float aux[IN == 2 ? BG * N_HEAD * NSPLIT : 1];
+  __shared__ int4 ri_s[IN == 5 ? BG : 1];  // IN 5: the rows' new control records for the KV epilogue
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int rg = wave / KW, kp = wave % KW;
   const int row0 = (blockIdx.x * WROWS + rg) * RPW;
@@ -316,7 +352,7 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
   // control record of this lane's epilogue row in the first batch group (bb = lane % BG): the
   // KV append needs (slot, pos); loading it here keeps it off the epilogue's critical path
   int4 riep = make_int4(-1, 0, 0, 0);
-  if (OUT == 0) riep = a.st.rowinfo[min(lane % BG, a.B - 1)];
+  if (OUT == 0 && IN != 5) riep = a.st.rowinfo[min(lane % BG, a.B - 1)];
   // residual epilogue (OUT 1): this lane's (row, batch row) of the first group is (row0 + lane / BG,
   // lane % BG); its x element (and, for c_proj after a fused MLP, the pending accumulators) is
   // loaded now instead of behind the dot products
@@ -337,6 +373,18 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
       ripre = a.st.rowinfo[wave];
     }
   }
+  // IN 5 (deferred select, every row prefetched by its own wave): the previous step's lm_head
+  // granules, the pending flag and the row's {step, next text id} come in the same round trip
+  // as the control record
+  LmGran lmg;
+  int2 rxp = make_int2(0, 0);
+  unsigned selpend = 0u;
+  if (IN == 5 && prefetched) {
+    ripre = a.st.rowinfo[wave];
+    rxp = a.st.rowx[wave];
+    selpend = *a.st.selp;
+    lmg_issue(a.st, wave, lane, lmg);
+  }
   const TW* __restrict__ W = reinterpret_cast<const TW*>(a.W);
   typename WReg<TW>::T wr[RPW][NI];
 #pragma unroll
@@ -345,6 +393,34 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
 #pragma unroll
     for (int it = 0; it < NI; ++it)
       wr[r][it] = (n < a.N) ? WReg<TW>::load(W + (size_t)n * K + kp * KC + it * 256 + lane * 4) : WReg<TW>::zero();
+  }
+  if constexpr (IN == 5) {
+    // commit the previous step's greedy select (argmax_commit's state advance; block 0 writes
+    // the shadow records, attention layer 0 copies them back) and build this step's record
+    if (prefetched) {
+      const int b = wave, s = ripre.x;
+      if (selpend && s >= 0) {
+        const Best r = lmg_reduce(lmg);
+        const int j = rxp.x, p = ripre.y + 1;
+        const int4 rn = make_int4(s, min(p, a.st.max_pos - 1), rxp.y, min(max(r.i, 0), VOCAB - 1));
+        if (blockIdx.x == 0 && lane == 0) {
+          if (p >= a.st.max_pos) atomicOr(a.st.err, 1);
+          if (j < a.st.plan_stride) {
+            a.st.tok_plan[(size_t)b * a.st.plan_stride + j] = r.i;
+            if (a.st.margin_plan) a.st.margin_plan[(size_t)b * a.st.plan_stride + j] = r.v - r.v2;
+          }
+          a.st.prev[s] = r.i;
+          a.st.pos[s] = p;
+          a.st.rowinfo_n[b] = rn;
+          a.st.rowx_n[b] = make_int2(j + 1, plan_tok(a.st, b, j + 2));
+        }
+        ripre = rn;
+      } else if (blockIdx.x == 0 && lane == 0) {
+        a.st.rowinfo_n[b] = ripre;
+        a.st.rowx_n[b] = rxp;
+      }
+      if (lane == 0) ri_s[b] = ripre;
+    }
   }
   for (int g0 = 0; g0 < a.B; g0 += BG) {
     const int bg = min(BG, a.B - g0);
@@ -412,7 +488,7 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
           } else {
             const int c = (n - D) % D, which = (n - D) / D;
             const int head = c / HD, d = c - head * HD;
-            const int4 ri = g0 == 0 ? riep : a.st.rowinfo[b];
+            const int4 ri = IN == 5 ? ri_s[bb] : g0 == 0 ? riep : a.st.rowinfo[b];
             const int s = ri.x, p = ri.y;
             if (s < 0) continue;
             const size_t idx =
@@ -435,10 +511,30 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
           a.st.h[(size_t)b * DFF + n] = gelu_tanh(v);
         } else {
           a.dst[(size_t)b * a.N + n] = v;
-          if (OUT == 4) part[wave][r][bb] = v;
+          if (OUT == 4 || OUT == 9) part[wave][r][bb] = v;
         }
       }
     }
+  }
+  if constexpr (OUT == 9) {
+    // deferred select: this block's top1/top2 per row as one granule (plain store; the next
+    // kernel boundary publishes it) and the pending flag
+    __syncthreads();
+    if (tid < a.B) {
+      Best r{-INFINITY, -INFINITY, 0x7fffffff};
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+#pragma unroll
+        for (int rr = 0; rr < RPW; ++rr) {
+          const int n = (blockIdx.x * 4 + w) * RPW + rr;
+          if (n < a.N) r = best_merge(r, Best{part[w][rr][tid], -INFINITY, n});
+        }
+      u64x2_t g;
+      g.x = ((unsigned long long)(unsigned)r.i << 32) | __float_as_uint(r.v);
+      g.y = (unsigned long long)__float_as_uint(r.v2);
+      reinterpret_cast<u64x2_t*>(a.st.lmbest)[(size_t)blockIdx.x * 4 + tid] = g;
+    }
+    if (blockIdx.x == 0 && tid == 0) *a.st.selp = 1u;
   }
   if constexpr (OUT == 4) {
     // fused greedy select (B <= BG: one batch group). Each block publishes its top1/top2 per row
@@ -888,10 +984,7 @@ __device__ __forceinline__ int4 make_rowinfo(const ArState& st, int b, int s, in
     atomicOr(st.err, 1);
     p = st.max_pos - 1;
   }
-  int tok = 384;  // no plan bound (measurement probes): PAD
-  if (st.text_plan)
-    tok = (j < st.plan_stride) ? min(max(st.text_plan[(size_t)b * st.plan_stride + j], 0), TEXT_VOCAB - 1) : -1;
-  return make_int4(s, p, tok, min(max(prev, 0), VOCAB - 1));
+  return make_int4(s, p, plan_tok(st, b, j), min(max(prev, 0), VOCAB - 1));
 }
 
 __global__ void ar_rowinfo_init_kernel(ArState st, int B) {
@@ -900,6 +993,8 @@ __global__ void ar_rowinfo_init_kernel(ArState st, int B) {
   const int s = st.slots[b];
   const int j = st.rowstep ? st.rowstep[b] : 0;
   st.rowinfo[b] = s < 0 ? make_int4(-1, 0, 0, 0) : make_rowinfo(st, b, s, st.pos[s], j, st.prev[s]);
+  st.rowx[b] = make_int2(j, plan_tok(st, b, j + 1));  // deferred select: step and next text id
+  if (b == 0) *st.selp = 0u;
 }
 
 // drop-in row mode: publish (slot, pos) for the kernels of the step
@@ -1079,12 +1174,20 @@ __global__ __launch_bounds__(256) void ar_attn_kernel(ArState st, int layer) {
 // straight to the bf16 operand row xn, as the merge kernel would write it (o * (1 / l)), and the
 // merge kernel is skipped.
 template <typename TKV>
-__global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer, int ns_max, int direct) {
+__global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer, int ns_max, int direct,
+                                                         int selcopy) {
   __shared__ float wm_s[4], wl_s[4];
   __shared__ float wo_s[4][HD];
   const int sp = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int4 ri = st.rowinfo[b];
+  // selcopy (layer 0 of a deferred-select step): the records c_attn just built are in the shadow
+  // arrays; one block per row copies them back for the rest of the step and clears the flag
+  const int4 ri = selcopy ? st.rowinfo_n[b] : st.rowinfo[b];
+  if (selcopy && sp == 0 && head == 0 && tid == 0) {
+    st.rowinfo[b] = ri;
+    st.rowx[b] = st.rowx_n[b];
+    if (b == 0) *st.selp = 0u;
+  }
   const int s = ri.x;
   if (s < 0) return;
   const int t = ri.y + 1;
@@ -1236,6 +1339,7 @@ int g_opt_attn_v2 = 1;
 int g_opt_cproj_b1 = 1;
 int g_opt_prefetch_in = 1;
 int g_opt_fuse_argmax = 0;  // measured at B = 1: the in-launch tail costs more than the boundary it saves
+int g_opt_defer_select = 1;  // B <= 2: greedy select in the next step's c_attn layer 0 (no argmax kernel)
 int g_opt_fuse_mlp = 1;
 
 template <typename TW, int K, int KW, int RPW, int IN, int OUT>
@@ -1243,28 +1347,28 @@ static void launch_gemv(const GemvArgs& a, hipStream_t s) {
   const int rows_per_block = (4 / KW) * RPW;
   dim3 grid((a.N + rows_per_block - 1) / rows_per_block);
   constexpr int BGMAX = (K == 768) ? 16 : 4;
-  if constexpr (OUT == 4) {  // fused select: one batch group of <= 4 rows, <= 512 blocks (launch_op checks)
+  if constexpr (OUT == 4 || OUT == 9 || IN == 5) {  // select variants: one batch group of <= 4 rows (launch_op checks)
     if (a.B <= 1) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 1, IN, OUT>), grid, dim3(256), 0, s, a);
     else if (a.B <= 2) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 2, IN, OUT>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 4, IN, OUT>), grid, dim3(256), 0, s, a);
-    return;
-  }
-  if constexpr (IN == 2 && OUT == 1 && K == 768 && KW == 1) {
-    if (g_opt_cproj_b1 && a.B == 1) {
-      if (g_opt_b1_splits <= 8) hipLaunchKernelGGL((ar_cproj_b1_kernel<TW, RPW, 8>), grid, dim3(256), 0, s, a);
-      else hipLaunchKernelGGL((ar_cproj_b1_kernel<TW, RPW, NSPLIT>), grid, dim3(256), 0, s, a);
-      return;
+  } else {
+    if constexpr (IN == 2 && OUT == 1 && K == 768 && KW == 1) {
+      if (g_opt_cproj_b1 && a.B == 1) {
+        if (g_opt_b1_splits <= 8) hipLaunchKernelGGL((ar_cproj_b1_kernel<TW, RPW, 8>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((ar_cproj_b1_kernel<TW, RPW, NSPLIT>), grid, dim3(256), 0, s, a);
+        return;
+      }
     }
+    if constexpr (IN != 2) {
+      if (g_opt_gemv_reg && a.B <= 1) { hipLaunchKernelGGL((ar_gemv_reg_kernel<TW, K, KW, RPW, 1, IN, OUT>), grid, dim3(256), 0, s, a); return; }
+      if (g_opt_gemv_reg && a.B <= 4) { hipLaunchKernelGGL((ar_gemv_reg_kernel<TW, K, KW, RPW, 4, IN, OUT>), grid, dim3(256), 0, s, a); return; }
+    }
+    if (a.B <= 1) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 1, IN, OUT>), grid, dim3(256), 0, s, a);
+    else if (a.B <= 2) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 2, IN, OUT>), grid, dim3(256), 0, s, a);
+    else if (a.B <= 4 || BGMAX == 4) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 4, IN, OUT>), grid, dim3(256), 0, s, a);
+    else if (a.B <= 8) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, (BGMAX >= 8 ? 8 : 4), IN, OUT>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, BGMAX, IN, OUT>), grid, dim3(256), 0, s, a);
   }
-  if constexpr (IN != 2) {
-    if (g_opt_gemv_reg && a.B <= 1) { hipLaunchKernelGGL((ar_gemv_reg_kernel<TW, K, KW, RPW, 1, IN, OUT>), grid, dim3(256), 0, s, a); return; }
-    if (g_opt_gemv_reg && a.B <= 4) { hipLaunchKernelGGL((ar_gemv_reg_kernel<TW, K, KW, RPW, 4, IN, OUT>), grid, dim3(256), 0, s, a); return; }
-  }
-  if (a.B <= 1) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 1, IN, OUT>), grid, dim3(256), 0, s, a);
-  else if (a.B <= 2) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 2, IN, OUT>), grid, dim3(256), 0, s, a);
-  else if (a.B <= 4 || BGMAX == 4) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 4, IN, OUT>), grid, dim3(256), 0, s, a);
-  else if (a.B <= 8) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, (BGMAX >= 8 ? 8 : 4), IN, OUT>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, BGMAX, IN, OUT>), grid, dim3(256), 0, s, a);
 }
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -1887,12 +1991,12 @@ static int attn_ns_max(int B) {  // enough splits to fill the chip, no more (ear
 }
 
 static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_t s, int ns_max = NSPLIT,
-                        int direct = 0) {
-  if (g_opt_attn_v2 || kvdtype == LVX_DTYPE_FP8 || direct) {
+                        int direct = 0, int selcopy = 0) {
+  if (g_opt_attn_v2 || kvdtype == LVX_DTYPE_FP8 || direct || selcopy) {
     dim3 grid(ns_max, N_HEAD, B);
-    if (kvdtype == LVX_DTYPE_BF16) hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t>), grid, dim3(256), 0, s, st, l, ns_max, direct);
-    else if (kvdtype == LVX_DTYPE_FP8) hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t>), grid, dim3(256), 0, s, st, l, ns_max, direct);
-    else hipLaunchKernelGGL((ar_attn_v2_kernel<float>), grid, dim3(256), 0, s, st, l, ns_max, direct);
+    if (kvdtype == LVX_DTYPE_BF16) hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
+    else if (kvdtype == LVX_DTYPE_FP8) hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
+    else hipLaunchKernelGGL((ar_attn_v2_kernel<float>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
   } else {
     dim3 grid(NSPLIT, N_HEAD, B);
     if (kvdtype == LVX_DTYPE_BF16) hipLaunchKernelGGL((ar_attn_kernel<bf16_t>), grid, dim3(256), 0, s, st, l);
@@ -1948,6 +2052,15 @@ static bool fused_select(int B) {
   return g_opt_fuse_argmax && B <= 4 && !use_mfma<TW>(B);
 }
 
+// deferred select: every row of the step is prefetched by its own wave of c_attn layer 0 (B <= 2,
+// one batch group) and lm_head runs LM_SEL_BLOCKS blocks of 8 rows
+template <typename TW>
+static bool defer_select(int B) {
+  static_assert(LM_SEL_BLOCKS <= LM_MAX_BLOCKS && LM_SEL_BLOCKS % 64 == 0, "deferred select granules");
+  return g_opt_defer_select && g_opt_prefetch_in && B <= 2 && !use_mfma<TW>(B) && !use_bt<TW>(B) &&
+         !fused_select<TW>(B);
+}
+
 template <typename TW>
 static bool fused_mlp(int B) {
   return sizeof(TW) == 2 && g_opt_fuse_mlp && B <= 2 && !use_mfma<TW>(B);
@@ -1979,6 +2092,8 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
         if (l == 0) hipLaunchKernelGGL((ar_rows_kernel<3>), dim3(B), dim3(64), 0, s, a);
         else hipLaunchKernelGGL((ar_rows_kernel<4>), dim3(B), dim3(64), 0, s, a);
         launch_mfma2<768, 0>(a, s);
+      } else if (l == 0 && a.defer_sel) {
+        launch_gemv<TW, 768, 1, 2, 5, 0>(a, s);  // + the previous step's select
       } else if (l == 0) {
         launch_gemv<TW, 768, 1, 2, 3, 0>(a, s);
       } else if (fm) {
@@ -1987,7 +2102,7 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
         launch_gemv<TW, 768, 1, 2, 0, 0>(a, s);
       }
       break;
-    case 1: launch_attn(a.st, kvdtype, B, l, s, nsm, mf && nsm == 1); break;
+    case 1: launch_attn(a.st, kvdtype, B, l, s, nsm, mf && nsm == 1, a.defer_sel && l == 0); break;
     case 2:
       a.W = w.w_aproj[l]; a.N = D;
       if (mf) {
@@ -2039,6 +2154,9 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       } else if (mf) {
         hipLaunchKernelGGL((ar_rows_kernel<4>), dim3(B), dim3(64), 0, s, a);
         launch_mfma2<768, 3>(a, s);
+      } else if (a.defer_sel) {
+        if (fm) launch_gemv<TW, 768, 1, 2, 4, 9>(a, s);
+        else launch_gemv<TW, 768, 1, 2, 0, 9>(a, s);
       } else if (select) {
         if (fm) launch_gemv<TW, 768, 1, 2, 4, 4>(a, s);
         else launch_gemv<TW, 768, 1, 2, 0, 4>(a, s);
@@ -2071,13 +2189,14 @@ template <typename TW>
 static bool ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B, const float* emb_row, int slot,
                       int pos, float* logits_dst, bool select, hipStream_t s) {
   GemvArgs a = make_args<TW>(w, st, kvdtype, B, emb_row);
+  a.defer_sel = select && !emb_row && defer_select<TW>(B);
   if (emb_row) hipLaunchKernelGGL(ar_row_state_kernel, dim3(1), dim3(1), 0, s, st, slot, pos);
   for (int l = 0; l < N_LAYER; ++l)
     for (int op = 0; op < 5; ++op) launch_op<TW>(op, a, w, l, kvdtype, B, s);
   a.dst = logits_dst;
   const bool fused = select && fused_select<TW>(B);
   launch_op<TW>(5, a, w, N_LAYER - 1, kvdtype, B, s, fused);
-  return fused;
+  return fused || a.defer_sel;
 }
 
 // Launch one op of the decode step `iters` times (bench.py times it with HIP events); layer 1.
@@ -2108,6 +2227,29 @@ void ar_launch_step(const ArWeights& w, const ArState& st, int wdtype, int kvdty
   const bool fused = wdtype == LVX_DTYPE_BF16 ? ar_layers<bf16_t>(w, st, kvdtype, B, er, slot, pos, dst, mode == 0, s)
                                              : ar_layers<float>(w, st, kvdtype, B, er, slot, pos, dst, mode == 0, s);
   if (mode == 0 && !fused) hipLaunchKernelGGL(ar_argmax_kernel, dim3(B), dim3(256), 0, s, st);
+}
+
+// deferred select: the last step's lm_head granules are committed here (argmax_commit), once per
+// lvx_ar_steps call, after the steps
+__global__ __launch_bounds__(64) void ar_select_final_kernel(ArState st) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int4 ri = st.rowinfo[b];
+  const int2 rx = st.rowx[b];
+  LmGran q;
+  lmg_issue(st, b, lane, q);
+  const Best r = lmg_reduce(q);
+  if (lane == 0) {
+    if (b == 0) *st.selp = 0u;
+    if (ri.x >= 0) {
+      st.rowstep[b] = rx.x;  // the step being committed (argmax_commit advances it)
+      argmax_commit(st, b, ri, r);
+    }
+  }
+}
+
+void ar_launch_steps_end(const ArState& st, int wdtype, int B, hipStream_t s) {
+  const bool d = wdtype == LVX_DTYPE_BF16 ? defer_select<bf16_t>(B) : defer_select<float>(B);
+  if (d) hipLaunchKernelGGL(ar_select_final_kernel, dim3(B), dim3(64), 0, s, st);
 }
 
 // ---------------------------------------------------------------------------------

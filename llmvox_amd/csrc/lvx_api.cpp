@@ -412,6 +412,8 @@ int lvx_finalize(lvx_ctx* c) {
       (r = c->dalloc(&st.part_o, (size_t)S * N_HEAD * NSPLIT * HD)) ||
       (r = c->dalloc(&st.part_ml, (size_t)S * N_HEAD * NSPLIT * 2)) || (r = c->dalloc(&st.h, (size_t)S * DFF)) ||
       (r = c->dalloc(&st.logits, (size_t)S * VOCAB)) || (r = c->dalloc(&st.rowinfo, S)) ||
+      (r = c->dalloc(&st.rowinfo_n, S)) || (r = c->dalloc(&st.rowx, S)) || (r = c->dalloc(&st.rowx_n, S)) ||
+      (r = c->dalloc(&st.selp, 4)) ||
       (r = c->dalloc(&st.xn, (size_t)S * D)) || (r = c->dalloc(&st.hb, (size_t)S * DFF)) ||
       (r = c->dalloc(&st.xb, (size_t)S * D)) || (r = c->dalloc(&st.xstat, (size_t)(D / 16) * S * 2)) ||
       (r = c->dalloc(&st.tick, (size_t)(D / 16))) ||
@@ -420,6 +422,7 @@ int lvx_finalize(lvx_ctx* c) {
     return r;
   HIP_TRY(hipMemset(st.yacc, 0, (size_t)YCOPIES * S * D * 4));
   HIP_TRY(hipMemset(st.ticket, 0, 16));
+  HIP_TRY(hipMemset(st.selp, 0, 16));
   HIP_TRY(hipMemset(st.tick, 0, (D / 16) * 4));
   HIP_TRY(hipMemset(st.part_o, 0, (size_t)S * N_HEAD * NSPLIT * HD * 4));
   HIP_TRY(hipMemset(st.part_ml, 0, (size_t)S * N_HEAD * NSPLIT * 2 * 4));
@@ -523,6 +526,7 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   else if (n == "prefetch_in") g_opt_prefetch_in = value;
   else if (n == "mfma_batch") g_opt_mfma_batch = value;
   else if (n == "fuse_argmax") g_opt_fuse_argmax = value;
+  else if (n == "defer_select") g_opt_defer_select = value;
   else if (n == "fuse_mlp") g_opt_fuse_mlp = value;
   else if (n == "mfma_ln") g_opt_mfma_ln = value;
   else if (n == "bt") g_opt_bt = value;
@@ -610,6 +614,7 @@ static int ar_step_impl(lvx_ctx* c, int n_steps, int B, const int32_t* slots, co
   if (!c->use_graphs || s == nullptr) {
     for (int i = 0; i < n_steps; ++i)
       ar_launch_step(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, 0, nullptr, 0, 0, nullptr, s);
+    ar_launch_steps_end(st, c->cfg.weight_dtype, B, s);
     HIP_TRY(hipGetLastError());
     return LVX_OK;
   }
@@ -645,6 +650,8 @@ static int ar_step_impl(lvx_ctx* c, int n_steps, int B, const int32_t* slots, co
     if (int r = get_graph(1, &g1)) return r;
     for (; left > 0; --left) HIP_TRY(hipGraphLaunch(g1, s));
   }
+  ar_launch_steps_end(st, c->cfg.weight_dtype, B, s);
+  HIP_TRY(hipGetLastError());
   return LVX_OK;
 }
 

@@ -17,7 +17,7 @@ constexpr int NSPLIT = 16;  // max KV splits per (stream, head) in decode attent
 #endif
 constexpr int YCOPIES = LVX_YCOPIES;  // accumulator copies of the fused MLP (spreads atomic contention)
 constexpr int LM_MAX_BLOCKS = 1024;  // lm_head blocks of the fused argmax tail (4096 rows / 8 per block = 512)
-extern int g_opt_gemv_reg, g_opt_attn_v2, g_opt_cproj_b1, g_opt_prefetch_in, g_opt_mfma_batch, g_opt_fuse_argmax,
+extern int g_opt_gemv_reg, g_opt_attn_v2, g_opt_cproj_b1, g_opt_prefetch_in, g_opt_mfma_batch, g_opt_fuse_argmax, g_opt_defer_select,
     g_opt_fuse_mlp, g_opt_mfma_ln, g_opt_bt, g_opt_bt_rows, g_opt_bt_merge, g_opt_codec_g2, g_opt_codec_g2_min, g_opt_codec_xcd, g_opt_attn_blocks, g_opt_ln_stats, g_opt_codec_bm256, g_opt_b1_splits;  // A/B switches (lvx_set_option)
 
 // Device-resident AR weights. Matrices are [out][in] row-major (torch Linear layout),
@@ -46,6 +46,10 @@ struct ArState {
   float* margin_plan = nullptr;  // [B][plan_stride] top1-top2 logit margin (optional)
   int plan_stride = 1;
   int4* rowinfo = nullptr;       // [B] {slot, pos, text id, prev token} of the step in flight
+  int4* rowinfo_n = nullptr;     // [B] deferred select: records built by c_attn layer 0 (copied back by attention)
+  int2* rowx = nullptr;          // [B] deferred select: {plan step j of the step in flight, text id of step j + 1}
+  int2* rowx_n = nullptr;        // [B] its shadow (as rowinfo_n)
+  uint32_t* selp = nullptr;      // [1] deferred select pending: lm_head granules not yet committed
   int32_t* pos = nullptr;       // [max_streams] per-slot next position
   int32_t* prev = nullptr;      // [max_streams] per-slot previous token
   int32_t* err = nullptr;       // [1] capacity overflow flag
@@ -77,6 +81,7 @@ void ar_launch_step(const ArWeights& w, const ArState& st, int wdtype, int kvdty
 int ar_probe(const ArWeights& w, const ArState& st, int wdtype, int kvdtype, int B, int which, int iters,
              hipStream_t s);
 void ar_launch_rowinfo_init(const ArState& st, int B, hipStream_t s);
+void ar_launch_steps_end(const ArState& st, int wdtype, int B, hipStream_t s);  // deferred select: commit the last step
 void launch_set_slot(int32_t* pos, int32_t* prev, int slot, int p, int tok, hipStream_t s);
 void launch_text_embed(const float* table, const int64_t* ids, int n, float* out, hipStream_t s);
 void launch_codes_to_features(const float* codebook, const int64_t* codes, int B, int L, float* feats,

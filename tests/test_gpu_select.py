@@ -1,0 +1,88 @@
+"""Deferred greedy select (option "defer_select", B <= 2 GEMV step): lm_head leaves per-block
+top1/top2 granules and the next step's c_attn layer 0 commits them (ar_select_final_kernel commits
+the last step of each lvx_ar_steps call). The state it produces must be bit-identical to the
+separate ar_argmax_kernel path (option off): tokens, margins, plan steps, slot positions and the
+last logits, across graph replays (16-step graphs + 1-step graphs), eager launches, an idle row and
+several calls in a row (the pending select never leaks across calls). The bf16 B <= 2 fused MLP
+adds its partial sums in arrival order (fp32 atomics), so with it on two runs of the same path
+differ in the last bits: bit-equality is checked with it off, and with it on tokens must agree
+wherever the top1-top2 margin exceeds that noise.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", params=["bf16", "fp32"])
+def eng(request):
+    from llmvox_amd.engine import build_engine
+    e = build_engine(0, request.param, request.param, max_streams=4, max_positions=256, max_codec_frames=64)
+    yield e
+    e.close()
+
+
+def _run(e, B, slots, calls, graphs):
+    dev = e.device
+    rng = np.random.default_rng(B * 31 + len(calls))
+    n = sum(calls)
+    plan = torch.from_numpy(rng.integers(3, 384, size=(B, n)).astype(np.int32)).to(dev)
+    for s in range(4):
+        e.reset_slot(s)
+    st = torch.tensor(slots, dtype=torch.int32, device=dev)
+    rowstep = torch.zeros(B, dtype=torch.int32, device=dev)
+    tok = torch.full((B, n), -7, dtype=torch.int32, device=dev)
+    margin = torch.zeros(B, n, dtype=torch.float32, device=dev)
+    e.set_graphs(graphs)
+    try:
+        for c in calls:
+            e.ar_steps(c, st, plan, rowstep, tok, margin)
+    finally:
+        e.set_graphs(True)
+    e.check_errors()
+    pos = [e.slot_position(s) for s in slots if s >= 0]
+    return tok.cpu().numpy(), margin.cpu().numpy(), rowstep.cpu().numpy(), pos, e.last_logits(B).cpu().numpy()
+
+
+@pytest.mark.parametrize("fuse_mlp", [0, 1], ids=["exact", "fused-mlp"])
+@pytest.mark.parametrize("graphs", [True, False], ids=["graphs", "eager"])
+@pytest.mark.parametrize("B,slots", [(1, [2]), (2, [0, 3]), (2, [1, -1])], ids=["B1", "B2", "B2-idle"])
+def test_deferred_select_matches_argmax_kernel(eng, B, slots, graphs, fuse_mlp):
+    calls = [3, 17, 1, 16]
+    eng.set_option("fuse_mlp", fuse_mlp)
+    try:
+        eng.set_option("defer_select", 0)
+        try:
+            ref = _run(eng, B, slots, calls, graphs)
+        finally:
+            eng.set_option("defer_select", 1)
+        got = _run(eng, B, slots, calls, graphs)
+    finally:
+        eng.set_option("fuse_mlp", 1)
+    if fuse_mlp == 0 or eng.weight_dtype == "fp32":  # no arrival-order sums on this path
+        for a, b, name in zip(got, ref, ["tokens", "margins", "rowstep", "positions", "logits"]):
+            np.testing.assert_array_equal(np.asarray(a), np.asarray(b), err_msg=name)
+    else:
+        # a near-tie may flip a token, and the stream diverges from there: compare up to the
+        # first step whose margin is within the noise, and the logits only if there is none
+        tied = False
+        for b, s in enumerate(slots):
+            if s < 0:
+                continue
+            close = np.nonzero(ref[1][b] < 1e-3)[0]
+            k = close[0] if len(close) else ref[0].shape[1]
+            tied |= bool(len(close))
+            np.testing.assert_array_equal(got[0][b, :k], ref[0][b, :k])
+        np.testing.assert_array_equal(got[2], ref[2])
+        assert got[3] == ref[3]
+        if not tied:
+            np.testing.assert_allclose(got[4], ref[4], atol=1e-3 * np.abs(ref[4]).max())
+    tok, _, rowstep, pos, _ = got
+    n = sum(calls)
+    for b, s in enumerate(slots):
+        if s >= 0:
+            assert rowstep[b] == n and (tok[b] >= 0).all()
+        else:
+            assert rowstep[b] == 0 and (tok[b] == -7).all()
+    assert pos == [n] * len(pos)
