@@ -83,6 +83,23 @@ __device__ __forceinline__ Best best_merge(Best a, Best c) {
 
 __device__ __forceinline__ int4 make_rowinfo(const ArState& st, int b, int s, int p, int j, int prev);
 
+// best_merge over the whole wave (exact: best_merge is commutative and associative), DPP within
+// rows then the four row results through SGPRs; wave-uniform result
+template <int CTRL>
+__device__ __forceinline__ Best best_dpp(Best r) {
+  return best_merge(r, Best{dpp_f32<CTRL>(r.v), dpp_f32<CTRL>(r.v2), dpp_i32<CTRL>(r.i)});
+}
+__device__ __forceinline__ Best best_lane(Best r, int lane) {
+  return Best{lane_f32(r.v, lane), lane_f32(r.v2, lane), __builtin_amdgcn_readlane(r.i, lane)};
+}
+__device__ __forceinline__ Best best_wave(Best r) {
+  r = best_dpp<0xB1>(r);
+  r = best_dpp<0x4E>(r);
+  r = best_dpp<0x128>(r);
+  r = best_dpp<0x124>(r);
+  return best_merge(best_merge(best_lane(r, 0), best_lane(r, 16)), best_merge(best_lane(r, 32), best_lane(r, 48)));
+}
+
 // text id of row b at plan step j (-1: past the end of the plan; PAD when no plan is bound)
 __device__ __forceinline__ int plan_tok(const ArState& st, int b, int j) {
   if (!st.text_plan) return 384;
@@ -110,6 +127,7 @@ typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
 // Deferred select: lm_head (OUT 9) leaves one 16-byte granule {index << 32 | top1 bits, top2 bits}
 // per (block, row) in st.lmbest; the next step's c_attn layer 0 (IN 5) or ar_select_final_kernel
 // reduces a row's 512 granules with one wave: every load in flight at once, then a shuffle tree.
+static_assert(NSPLIT == 16, "the split merges reduce one head's splits as one 16-lane DPP row");
 constexpr int LM_SEL_BLOCKS = VOCAB / 8;  // lm_head blocks on the B <= 2 GEMV path (8 rows each)
 struct LmGran {
   u64x2_t g[LM_SEL_BLOCKS / 64];
@@ -125,12 +143,7 @@ __device__ __forceinline__ Best lmg_reduce(const LmGran& q) {
   for (int k = 0; k < LM_SEL_BLOCKS / 64; ++k)
     r = best_merge(r, Best{__uint_as_float((unsigned)q.g[k].x), __uint_as_float((unsigned)q.g[k].y),
                            (int)(q.g[k].x >> 32)});
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    Best c{__shfl_xor(r.v, o, 64), __shfl_xor(r.v2, o, 64), __shfl_xor(r.i, o, 64)};
-    r = best_merge(r, c);
-  }
-  return r;
+  return best_wave(r);
 }
 
 // one K (which 0) or V (which 1) element of the KV cache in its dtype
@@ -583,11 +596,7 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
       for (int k = 0; k < 8; ++k)
         if (lane + 64 * k < (int)gridDim.x)
           r = best_merge(r, Best{__uint_as_float((unsigned)g0v[k]), __uint_as_float((unsigned)g1v[k]), (int)(g0v[k] >> 32)});
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        Best c{__shfl_xor(r.v, o, 64), __shfl_xor(r.v2, o, 64), __shfl_xor(r.i, o, 64)};
-        r = best_merge(r, c);
-      }
+      r = best_wave(r);
       if (lane == 0) argmax_commit(a.st, wave, a.st.rowinfo[wave], r);
     }
     if (tid == 0) __hip_atomic_store(((gu32*)a.st.ticket), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -838,12 +847,10 @@ __global__ __launch_bounds__(256) void ar_cproj_b1_kernel(GemvArgs a) {
     const int sp = tid & (NSPLIT - 1);
     const bool on = sp < ns && ml.x != -INFINITY;
     float M = on ? ml.x : -INFINITY;
-#pragma unroll
-    for (int o = 1; o < NSPLIT; o <<= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
+    M = row16_max(M);  // the NSPLIT == 16 splits of a head are one DPP row
     const float f = on ? expf(ml.x - M) : 0.f;
     float den = f * ml.y;
-#pragma unroll
-    for (int o = 1; o < NSPLIT; o <<= 1) den += __shfl_xor(den, o, 64);
+    den = row16_sum(den);
     cf[tid] = (ns > 0) ? f / den : 0.f;
   }
   __syncthreads();
@@ -1173,11 +1180,11 @@ __global__ __launch_bounds__(256) void ar_attn_kernel(ArState st, int layer) {
 // direct = 1 (batched path with one split per (row, head)): the normalised head output goes
 // straight to the bf16 operand row xn, as the merge kernel would write it (o * (1 / l)), and the
 // merge kernel is skipped.
-template <typename TKV>
+template <typename TKV, int DEPTH>
 __global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer, int ns_max, int direct,
                                                          int selcopy) {
   __shared__ float wm_s[4], wl_s[4];
-  __shared__ float wo_s[4][HD];
+  __shared__ float wo_s[4][4][HD];  // [wave][16-lane row][part * 24 + i]
   const int sp = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   // selcopy (layer 0 of a deferred-select step): the records c_attn just built are in the shadow
@@ -1212,12 +1219,13 @@ __global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer, 
   float m = -INFINITY, l = 0.f, o[24];
 #pragma unroll
   for (int i = 0; i < 24; ++i) o[i] = 0.f;
-  // Two tiles in flight: tile kb+128 is loaded into one register set while tile kb (in that set,
-  // issued two tiles ago) is consumed and tile kb+64 is landing in the other. Loads are
+  // DEPTH tiles in flight: the register set of tile kb is refilled with tile kb + DEPTH * 64 right
+  // after it is consumed, while the other sets are landing (DEPTH * 24 KB per block in flight: a
+  // block streams at bytes-in-flight / latency, so the depth sets the per-CU rate). Loads are
   // unconditional (key clamped to the last valid one, invalid lanes masked after) so that no load
-  // sits under a branch: the compiler's vmcnt for "this set has landed" then leaves the other set
+  // sits under a branch: the compiler's vmcnt for "this set has landed" then leaves the other sets
   // in flight instead of draining every outstanding load.
-  KvPiece<TKV> kp0[3], vp0[3], kp1[3], vp1[3];
+  KvPiece<TKV> kpr[DEPTH][3], vpr[DEPTH][3];
   auto issue = [&](int kb, KvPiece<TKV>(&kp)[3], KvPiece<TKV>(&vp)[3]) {
     const int key = min(kb + kq, k1 - 1);
 #pragma unroll
@@ -1234,11 +1242,10 @@ __global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer, 
     float sc = 0.f;
 #pragma unroll
     for (int i = 0; i < 24; ++i) sc = fmaf(q[i], kf[i], sc);
-    sc += __shfl_xor(sc, 1, 64);
-    sc += __shfl_xor(sc, 2, 64);
+    sc = quad_sum(sc);
     if (!valid) sc = -INFINITY;
-    const float mn = fmaxf(m, wave_max(sc));
-    if (mn == -INFINITY) return;  // this wave has no key in this tile yet (wave-uniform)
+    const float mn = fmaxf(m, wave_max(sc));  // -inf while this wave has seen no key: alpha = p = 0
+    if (DEPTH == 2 && mn == -INFINITY) return;  // (wave-uniform) skip the no-op update
     const float alpha = (m == -INFINITY) ? 0.f : expf(m - mn);
     const float p = valid ? expf(sc - mn) : 0.f;
     l = l * alpha + wave_sum(part == 0 ? p : 0.f);
@@ -1246,28 +1253,33 @@ __global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer, 
     for (int i = 0; i < 24; ++i) o[i] = fmaf(valid ? p : 0.f, valid ? vf[i] : 0.f, o[i] * alpha);
     m = mn;
   };
-  issue(k0, kp0, vp0);
-  issue(k0 + ATK, kp1, vp1);
-  for (int kb = k0; kb < k1; kb += 2 * ATK) {
-    tile(kb, kp0, vp0);
-    issue(kb + 2 * ATK, kp0, vp0);
-    if (kb + ATK >= k1) break;
-    tile(kb + ATK, kp1, vp1);
-    issue(kb + 3 * ATK, kp1, vp1);
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d) issue(k0 + d * ATK, kpr[d], vpr[d]);
+  // DEPTH 2 (few tiles per block, the B <= 2 step): leave after the last valid tile. DEPTH >= 4
+  // (long splits, batched steps): whole groups of DEPTH tiles with no exit inside a group (a tile
+  // past k1 is all-invalid: alpha = 1, p = 0), which keeps the compiler from draining every
+  // outstanding load at the group boundary
+  for (int kb = k0; kb < k1; kb += DEPTH * ATK) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      if (DEPTH == 2 && d > 0 && kb + d * ATK >= k1) break;
+      tile(kb + d * ATK, kpr[d], vpr[d]);
+      issue(kb + (d + DEPTH) * ATK, kpr[d], vpr[d]);
+      if (DEPTH > 2) __builtin_amdgcn_sched_barrier(0);  // keep the refill right behind its tile
+    }
   }
-  // sum o over the 16 key slots of the wave (lanes with equal part)
+  // sum o over the 16 key slots of the wave (lanes with equal part): within each 16-lane row by
+  // DPP (row_ror 8, 4), the four rows through LDS
 #pragma unroll
   for (int i = 0; i < 24; ++i) {
     float v = o[i];
-    v += __shfl_xor(v, 4, 64);
-    v += __shfl_xor(v, 8, 64);
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
+    v += dpp_f32<0x128>(v);
+    v += dpp_f32<0x124>(v);
     o[i] = v;
   }
-  if (lane < 4) {
+  if ((lane & 15) < 4) {
 #pragma unroll
-    for (int i = 0; i < 24; ++i) wo_s[wave][lane * 24 + i] = o[i];
+    for (int i = 0; i < 24; ++i) wo_s[wave][lane >> 4][(lane & 3) * 24 + i] = o[i];
   }
   if (lane == 0) { wm_s[wave] = m; wl_s[wave] = l; }
   __syncthreads();
@@ -1277,7 +1289,7 @@ __global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer, 
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
       const float f = (wm_s[w] == -INFINITY) ? 0.f : expf(wm_s[w] - M);
-      ov += f * wo_s[w][tid];
+      ov += f * ((wo_s[w][0][tid] + wo_s[w][1][tid]) + (wo_s[w][2][tid] + wo_s[w][3][tid]));
       lv += f * wl_s[w];
     }
     if (direct) {
@@ -1315,11 +1327,7 @@ __global__ __launch_bounds__(256) void ar_argmax_kernel(ArState st) {
     bt = best_merge(bt, Best{v.z, -INFINITY, i0 + 2});
     bt = best_merge(bt, Best{v.w, -INFINITY, i0 + 3});
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    Best c{__shfl_xor(bt.v, o, 64), __shfl_xor(bt.v2, o, 64), __shfl_xor(bt.i, o, 64)};
-    bt = best_merge(bt, c);
-  }
+  bt = best_wave(bt);
   if (lane == 0) { sv[wave] = bt.v; sv2[wave] = bt.v2; si[wave] = bt.i; }
   __syncthreads();
   if (tid == 0) {
@@ -1473,12 +1481,10 @@ __global__ __launch_bounds__(256) void ar_merge_bf16_kernel(ArState st, int ns_m
     const int ns = ri.x < 0 ? 0 : min(ns_max, (ri.y + 1 + 63) / 64);
     const bool on = (tid & (NSPLIT - 1)) < ns && ml.x != -INFINITY;
     float M = on ? ml.x : -INFINITY;
-#pragma unroll
-    for (int o = 1; o < NSPLIT; o <<= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
+    M = row16_max(M);  // the NSPLIT == 16 splits of a head are one DPP row
     const float f = on ? expf(ml.x - M) : 0.f;
     float den = f * ml.y;
-#pragma unroll
-    for (int o = 1; o < NSPLIT; o <<= 1) den += __shfl_xor(den, o, 64);
+    den = row16_sum(den);
     cf[tid] = ns > 0 ? f / den : 0.f;
   }
   __syncthreads();
@@ -1980,6 +1986,10 @@ static void launch_bt(const GemvArgs& a, int ns_max, hipStream_t s) {
   else hipLaunchKernelGGL((ar_bt_kernel<K, 4, IN, OUT>), grid, block, 0, s, a, ns_max);
 }
 
+int g_opt_attn_depth = 2;  // KV tiles in flight per attention block for B > 2 (2, or 4 / 8 for whole
+                           // groups of tiles). us/step (tools/step_sweep.py) depth 2 / 4, after the DPP
+                           // reductions: B = 32, t = 256+: 152.0 / 157.9; B = 64: 216.3 / 234.2 (with
+                           // the ds_bpermute reductions depth 4 had won: 173.5 / 167.9, 248.8 / 242.4)
 int g_opt_attn_blocks = 256;  // split count target: ns * 8 heads * B <= this (batched paths); measured
 // (tools/step_sweep.py, us/step at t = 256-511): B = 32: 1024 -> 164, 512 -> 169, 256 (one split:
 // the attention writes xn directly, no merge kernel) -> 155.5; B = 16: 138 / 136 / 131 (128 blocks);
@@ -1994,9 +2004,18 @@ static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_
                         int direct = 0, int selcopy = 0) {
   if (g_opt_attn_v2 || kvdtype == LVX_DTYPE_FP8 || direct || selcopy) {
     dim3 grid(ns_max, N_HEAD, B);
-    if (kvdtype == LVX_DTYPE_BF16) hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
-    else if (kvdtype == LVX_DTYPE_FP8) hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
-    else hipLaunchKernelGGL((ar_attn_v2_kernel<float>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
+    const bool deep = g_opt_attn_depth >= 4 && B > 2;  // B <= 2: ~1 tile per split at t <= 1024
+    if (kvdtype == LVX_DTYPE_BF16) {
+      if (deep && g_opt_attn_depth >= 8) hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 8>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
+      else if (deep) hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 4>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
+      else hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
+    } else if (kvdtype == LVX_DTYPE_FP8) {
+      if (deep) hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t, 4>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
+      else hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t, 2>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
+    } else {
+      if (deep) hipLaunchKernelGGL((ar_attn_v2_kernel<float, 4>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
+      else hipLaunchKernelGGL((ar_attn_v2_kernel<float, 2>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
+    }
   } else {
     dim3 grid(NSPLIT, N_HEAD, B);
     if (kvdtype == LVX_DTYPE_BF16) hipLaunchKernelGGL((ar_attn_kernel<bf16_t>), grid, dim3(256), 0, s, st, l);

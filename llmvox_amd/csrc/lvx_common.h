@@ -55,15 +55,48 @@ template <> struct Ld<bf16_t> {
 };
 
 // ---- wave / block reductions ---------------------------------------------
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// Full-wave reductions (every lane active): DPP within each 16-lane row (quad_perm xor 1 / xor 2,
+// then row_ror 8 / row_ror 4: VALU-latency steps), then the four row results read into SGPRs
+// (v_readlane) and combined in a fixed order, so the result is wave-uniform. Rotating by 8 before
+// 4 adds the same two pair sums on every lane of a row (only operand order differs), so row16_sum
+// is bit-identical across the row, like a butterfly. A ds_bpermute butterfly (__shfl_xor) costs an
+// LDS round trip per step, six in a chain.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ float lane_f32(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+__device__ __forceinline__ float quad_sum(float v) {  // sum over the 4 lanes of a quad (xor 1, 2)
+  v += dpp_f32<0xB1>(v);  // quad_perm [1,0,3,2]
+  v += dpp_f32<0x4E>(v);  // quad_perm [2,3,0,1]
   return v;
 }
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+__device__ __forceinline__ float row16_sum(float v) {
+  v = quad_sum(v);
+  v += dpp_f32<0x128>(v);  // row_ror 8
+  v += dpp_f32<0x124>(v);  // row_ror 4
   return v;
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp_f32<0xB1>(v));
+  v = fmaxf(v, dpp_f32<0x4E>(v));
+  v = fmaxf(v, dpp_f32<0x128>(v));
+  v = fmaxf(v, dpp_f32<0x124>(v));
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+  v = row16_sum(v);
+  return (lane_f32(v, 0) + lane_f32(v, 16)) + (lane_f32(v, 32) + lane_f32(v, 48));
+}
+__device__ __forceinline__ float wave_max(float v) {
+  v = row16_max(v);
+  return fmaxf(fmaxf(lane_f32(v, 0), lane_f32(v, 16)), fmaxf(lane_f32(v, 32), lane_f32(v, 48)));
 }
 
 // block of NT threads; scratch must hold NT/64 floats; result broadcast to all threads
