@@ -1556,7 +1556,9 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
       }
 #pragma unroll
       for (int o = 1; o < 4; o <<= 1) {  // pairs of equal counts n: M2 += (mb - ma)^2 n / 2
-        const float mb = __shfl_xor(mean, o, 64), m2b = __shfl_xor(m2, o, 64);
+        // (whole waves: tid < NT * 64) partner lane xor o within the quad by DPP quad_perm
+        const float mb = o == 1 ? dpp_f32<0xB1>(mean) : dpp_f32<0x4E>(mean);
+        const float m2b = o == 1 ? dpp_f32<0xB1>(m2) : dpp_f32<0x4E>(m2);
         const float d = mb - mean;
         const float n = 192.0f * o;
         m2 = m2 + m2b + d * d * (n * 0.5f);

@@ -1,6 +1,8 @@
 """Per-kernel duration and inter-kernel gap from a rocprofv3 kernel_trace.csv (last N kernels)."""
 import csv, sys, collections
 rows = list(csv.DictReader(open(sys.argv[1])))
+if len(sys.argv) > 3:  # only kernels whose name contains this substring (e.g. "ar_")
+    rows = [r for r in rows if sys.argv[3] in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 200
 rows = rows[-n:]
