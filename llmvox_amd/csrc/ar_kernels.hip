@@ -60,8 +60,9 @@ struct GemvArgs {
   // fused MLP (ar_mlp_fused_kernel): its output sits in YCOPIES accumulators until c_proj folds it in
   float* yacc;           // non-null when the step runs the fused MLP
   int add_y;             // c_proj: fold the accumulators into x (layers >= 1; 0 at layer 0 = just clear)
-  int defer_sel;         // deferred greedy select (B <= 2 GEMV step, option "defer_select"): lm_head
-                         // publishes per-block granules, the next step's c_attn layer 0 reduces them
+  int defer_sel;         // deferred greedy select (option "defer_select"). 1: B <= 2 GEMV step, lm_head
+                         // publishes per-block granules, the next step's c_attn layer 0 reduces them;
+                         // 2: batched step, the next step's embedding rows kernel reduces the logits
 };
 
 // ---------------------------------------------------------------------------------
@@ -1001,6 +1002,7 @@ __global__ void ar_rowinfo_init_kernel(ArState st, int B) {
   const int j = st.rowstep ? st.rowstep[b] : 0;
   st.rowinfo[b] = s < 0 ? make_int4(-1, 0, 0, 0) : make_rowinfo(st, b, s, st.pos[s], j, st.prev[s]);
   st.rowx[b] = make_int2(j, plan_tok(st, b, j + 1));  // deferred select: step and next text id
+  st.selrow[b] = 0u;
   if (b == 0) *st.selp = 0u;
 }
 
@@ -1449,10 +1451,74 @@ __global__ __launch_bounds__(256) void ar_rows_kernel(GemvArgs a) {
 #pragma unroll      // then adds its output to a final x instead of re-reading the copies
       for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = v[j];
   } else {
-    embed_row(a, a.st.rowinfo[b], lane, v);
+    const int4 ri = a.st.rowinfo[b];
+    embed_row(a, ri, lane, v);
 #pragma unroll
     for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = v[j];
   }
+  wave_ln_regs(v, g);
+  uint2* dst = reinterpret_cast<uint2*>(a.st.xn + (size_t)b * D);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) dst[j * 64 + lane] = pack4_bf16(v[j]);
+}
+
+// Batched deferred select (defer_sel 2): the previous step's greedy select of row b (the
+// ar_argmax_kernel commit, streaming_server.py:342-347) and then the embedding + LayerNorm of the
+// token it picked (ar_rows_kernel<3>). Four waves split the 4096 logits (one round trip with the
+// row's control records), wave 0 commits and builds the operand row.
+__global__ __launch_bounds__(256) void ar_embed_select_kernel(GemvArgs a) {
+  __shared__ float sv[4], sv2[4];
+  __shared__ int si[4];
+  const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  int4 ri = a.st.rowinfo[b];
+  const int2 rx = a.st.rowx[b];  // {plan step j, text id of step j + 1}
+  const unsigned pend = a.st.selrow[b];
+  const float4* lg = reinterpret_cast<const float4*>(a.st.logits + (size_t)b * VOCAB);
+  float4 lv[VOCAB / 1024];
+#pragma unroll
+  for (int k = 0; k < VOCAB / 1024; ++k) lv[k] = lg[k * 256 + tid];
+  float4 g[3];
+  if (wave == 0)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) g[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
+  Best bt{-INFINITY, -INFINITY, 0x7fffffff};
+#pragma unroll
+  for (int k = 0; k < VOCAB / 1024; ++k) {
+    const int i0 = (k * 256 + tid) * 4;
+    bt = best_merge(bt, Best{lv[k].x, -INFINITY, i0});
+    bt = best_merge(bt, Best{lv[k].y, -INFINITY, i0 + 1});
+    bt = best_merge(bt, Best{lv[k].z, -INFINITY, i0 + 2});
+    bt = best_merge(bt, Best{lv[k].w, -INFINITY, i0 + 3});
+  }
+  bt = best_wave(bt);
+  if (lane == 0) { sv[wave] = bt.v; sv2[wave] = bt.v2; si[wave] = bt.i; }
+  __syncthreads();
+  if (wave != 0) return;
+  if (pend && ri.x >= 0) {
+    Best r{sv[0], sv2[0], si[0]};
+#pragma unroll
+    for (int w = 1; w < 4; ++w) r = best_merge(r, Best{sv[w], sv2[w], si[w]});
+    const int s = ri.x, p = ri.y + 1, j = rx.x;
+    const int4 rn = make_int4(s, min(p, a.st.max_pos - 1), rx.y, min(max(r.i, 0), VOCAB - 1));
+    if (lane == 0) {  // argmax_commit
+      if (p >= a.st.max_pos) atomicOr(a.st.err, 1);
+      if (j < a.st.plan_stride) {
+        a.st.tok_plan[(size_t)b * a.st.plan_stride + j] = r.i;
+        if (a.st.margin_plan) a.st.margin_plan[(size_t)b * a.st.plan_stride + j] = r.v - r.v2;
+      }
+      a.st.prev[s] = r.i;
+      a.st.pos[s] = p;
+      a.st.rowstep[b] = j + 1;
+      a.st.rowinfo[b] = rn;
+      a.st.rowx[b] = make_int2(j + 1, plan_tok(a.st, b, j + 2));
+    }
+    ri = rn;
+  }
+  if (lane == 0) a.st.selrow[b] = 1u;  // this step's lm_head leaves the next pending select
+  float4 v[3];
+  embed_row(a, ri, lane, v);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = v[j];
   wave_ln_regs(v, g);
   uint2* dst = reinterpret_cast<uint2*>(a.st.xn + (size_t)b * D);
 #pragma unroll
@@ -2048,8 +2114,14 @@ static void launch_op_bt(int op, GemvArgs& a, const ArWeights& w, int l, int kvd
   switch (op) {
     case 0:
       a.W = w.w_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
-      if (l == 0) launch_bt<768, 3, 0>(a, 0, s);
-      else launch_bt<768, 0, 0>(a, 0, s);
+      if (l == 0 && a.defer_sel == 2) {  // embedding + the previous step's select, then c_attn
+        hipLaunchKernelGGL(ar_embed_select_kernel, dim3(B), dim3(256), 0, s, a);
+        launch_bt<768, 1, 0>(a, 0, s);
+      } else if (l == 0) {
+        launch_bt<768, 3, 0>(a, 0, s);
+      } else {
+        launch_bt<768, 0, 0>(a, 0, s);
+      }
       break;
     case 1: launch_attn(a.st, kvdtype, B, l, s, nsm); break;
     case 2:
@@ -2081,6 +2153,10 @@ static bool defer_select(int B) {
   return g_opt_defer_select && g_opt_prefetch_in && B <= 2 && !use_mfma<TW>(B) && !use_bt<TW>(B) &&
          !fused_select<TW>(B);
 }
+template <typename TW>
+static bool defer_select_batched(int B) {  // not for B <= mfma_ln (embedding inside the MFMA c_attn)
+  return g_opt_defer_select && ((use_mfma<TW>(B) && B > g_opt_mfma_ln) || use_bt<TW>(B));
+}
 
 template <typename TW>
 static bool fused_mlp(int B) {
@@ -2104,7 +2180,10 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
   switch (op) {
     case 0:
       a.W = w.w_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
-      if (mf && B <= g_opt_mfma_ln) {
+      if (mf && l == 0 && a.defer_sel == 2) {  // embedding + the previous step's select, then c_attn
+        hipLaunchKernelGGL(ar_embed_select_kernel, dim3(B), dim3(256), 0, s, a);
+        launch_mfma2<768, 0>(a, s);
+      } else if (mf && B <= g_opt_mfma_ln) {
         if (l == 0) launch_mfma_ln<0, 3>(a, s);
         else launch_mfma_ln<0, 4>(a, s);
       } else if (mf && l > 0 && g_opt_ln_stats >= 2) {
@@ -2123,7 +2202,7 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
         launch_gemv<TW, 768, 1, 2, 0, 0>(a, s);
       }
       break;
-    case 1: launch_attn(a.st, kvdtype, B, l, s, nsm, mf && nsm == 1, a.defer_sel && l == 0); break;
+    case 1: launch_attn(a.st, kvdtype, B, l, s, nsm, mf && nsm == 1, a.defer_sel == 1 && l == 0); break;
     case 2:
       a.W = w.w_aproj[l]; a.N = D;
       if (mf) {
@@ -2210,7 +2289,7 @@ template <typename TW>
 static bool ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B, const float* emb_row, int slot,
                       int pos, float* logits_dst, bool select, hipStream_t s) {
   GemvArgs a = make_args<TW>(w, st, kvdtype, B, emb_row);
-  a.defer_sel = select && !emb_row && defer_select<TW>(B);
+  a.defer_sel = (select && !emb_row) ? (defer_select<TW>(B) ? 1 : defer_select_batched<TW>(B) ? 2 : 0) : 0;
   if (emb_row) hipLaunchKernelGGL(ar_row_state_kernel, dim3(1), dim3(1), 0, s, st, slot, pos);
   for (int l = 0; l < N_LAYER; ++l)
     for (int op = 0; op < 5; ++op) launch_op<TW>(op, a, w, l, kvdtype, B, s);
@@ -2270,7 +2349,9 @@ __global__ __launch_bounds__(64) void ar_select_final_kernel(ArState st) {
 
 void ar_launch_steps_end(const ArState& st, int wdtype, int B, hipStream_t s) {
   const bool d = wdtype == LVX_DTYPE_BF16 ? defer_select<bf16_t>(B) : defer_select<float>(B);
+  const bool db = wdtype == LVX_DTYPE_BF16 ? defer_select_batched<bf16_t>(B) : defer_select_batched<float>(B);
   if (d) hipLaunchKernelGGL(ar_select_final_kernel, dim3(B), dim3(64), 0, s, st);
+  else if (db) hipLaunchKernelGGL(ar_argmax_kernel, dim3(B), dim3(256), 0, s, st);
 }
 
 // ---------------------------------------------------------------------------------

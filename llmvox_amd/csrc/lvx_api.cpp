@@ -413,7 +413,7 @@ int lvx_finalize(lvx_ctx* c) {
       (r = c->dalloc(&st.part_ml, (size_t)S * N_HEAD * NSPLIT * 2)) || (r = c->dalloc(&st.h, (size_t)S * DFF)) ||
       (r = c->dalloc(&st.logits, (size_t)S * VOCAB)) || (r = c->dalloc(&st.rowinfo, S)) ||
       (r = c->dalloc(&st.rowinfo_n, S)) || (r = c->dalloc(&st.rowx, S)) || (r = c->dalloc(&st.rowx_n, S)) ||
-      (r = c->dalloc(&st.selp, 4)) ||
+      (r = c->dalloc(&st.selp, 4)) || (r = c->dalloc(&st.selrow, S)) ||
       (r = c->dalloc(&st.xn, (size_t)S * D)) || (r = c->dalloc(&st.hb, (size_t)S * DFF)) ||
       (r = c->dalloc(&st.xb, (size_t)S * D)) || (r = c->dalloc(&st.xstat, (size_t)(D / 16) * S * 2)) ||
       (r = c->dalloc(&st.tick, (size_t)(D / 16))) ||

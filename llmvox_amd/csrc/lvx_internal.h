@@ -50,6 +50,7 @@ struct ArState {
   int2* rowx = nullptr;          // [B] deferred select: {plan step j of the step in flight, text id of step j + 1}
   int2* rowx_n = nullptr;        // [B] its shadow (as rowinfo_n)
   uint32_t* selp = nullptr;      // [1] deferred select pending: lm_head granules not yet committed
+  uint32_t* selrow = nullptr;    // [B] batched deferred select: row b's logits not yet committed
   int32_t* pos = nullptr;       // [max_streams] per-slot next position
   int32_t* prev = nullptr;      // [max_streams] per-slot previous token
   int32_t* err = nullptr;       // [1] capacity overflow flag

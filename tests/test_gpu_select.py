@@ -86,3 +86,51 @@ def test_deferred_select_matches_argmax_kernel(eng, B, slots, graphs, fuse_mlp):
         else:
             assert rowstep[b] == 0 and (tok[b] == -7).all()
     assert pos == [n] * len(pos)
+
+
+@pytest.fixture(scope="module")
+def eng_batched():
+    from llmvox_amd.engine import build_engine
+    e = build_engine(0, "bf16", "bf16", max_streams=48, max_positions=256, max_codec_frames=64)
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("B", [3, 8, 32, 48])
+def test_batched_deferred_select_matches_argmax_kernel(eng_batched, B):
+    """Batched steps (MFMA / v3 paths): the select runs in the next step's embedding rows kernel
+    (ar_argmax_kernel after the last step). These paths have no arrival-order sums: bit-equal,
+    with one idle row."""
+    e = eng_batched
+    slots = list(range(B))
+    slots[B // 2] = -1
+    calls = [3, 17, 1, 16]
+
+    def run():
+        dev = e.device
+        rng = np.random.default_rng(B)
+        n = sum(calls)
+        plan = torch.from_numpy(rng.integers(3, 384, size=(B, n)).astype(np.int32)).to(dev)
+        for s in range(48):
+            e.reset_slot(s)
+        st = torch.tensor(slots, dtype=torch.int32, device=dev)
+        rowstep = torch.zeros(B, dtype=torch.int32, device=dev)
+        tok = torch.full((B, n), -7, dtype=torch.int32, device=dev)
+        margin = torch.zeros(B, n, dtype=torch.float32, device=dev)
+        for c in calls:
+            e.ar_steps(c, st, plan, rowstep, tok, margin)
+        e.check_errors()
+        pos = [e.slot_position(s) for s in slots if s >= 0]
+        return tok.cpu().numpy(), margin.cpu().numpy(), rowstep.cpu().numpy(), pos, e.last_logits(B).cpu().numpy()
+
+    e.set_option("defer_select", 0)
+    try:
+        ref = run()
+    finally:
+        e.set_option("defer_select", 1)
+    got = run()
+    for a, b, name in zip(got, ref, ["tokens", "margins", "rowstep", "positions", "logits"]):
+        np.testing.assert_array_equal(np.asarray(a), np.asarray(b), err_msg=name)
+    n = sum(calls)
+    assert got[2][B // 2] == 0 and (got[0][B // 2] == -7).all()
+    assert all(got[2][b] == n for b in range(B) if b != B // 2)
