@@ -2154,8 +2154,11 @@ static bool defer_select(int B) {
          !fused_select<TW>(B);
 }
 template <typename TW>
-static bool defer_select_batched(int B) {  // not for B <= mfma_ln (embedding inside the MFMA c_attn)
-  return g_opt_defer_select && ((use_mfma<TW>(B) && B > g_opt_mfma_ln) || use_bt<TW>(B));
+static bool defer_select_batched(int B) {
+  // us/step (tools/step_sweep.py, t = 256+) argmax kernel / deferred: B = 3: 112.9 / 114.7 (left on
+  // the argmax kernel unless defer_select = 2), B = 4: 106.0 / 104.9, 8: 120.7 / 118.3,
+  // 12: 123.0 / 120.5, 16: 128.4 / 125.5, 32: 150.3 / 147.3, 64: 213.4 / 206.8
+  return g_opt_defer_select && ((use_mfma<TW>(B) && (B >= 4 || g_opt_defer_select >= 2)) || use_bt<TW>(B));
 }
 
 template <typename TW>

@@ -1,0 +1,9 @@
+set -o pipefail
+mkdir -p gpurun_out
+export PYTHONPATH=.
+timeout -k 10 200 python -u tools/step_sweep.py 4 256 defer_select=1 defer_select=2 > gpurun_out/sweep.log 2>&1 \
+ && timeout -k 10 200 python -u tools/step_sweep.py 8 256 defer_select=1 defer_select=2 >> gpurun_out/sweep.log 2>&1 \
+ && timeout -k 10 200 python -u tools/step_sweep.py 3 256 defer_select=1 defer_select=2 >> gpurun_out/sweep.log 2>&1
+rc=$?
+cat gpurun_out/sweep.log | grep -v amdgpu.ids
+exit $rc
