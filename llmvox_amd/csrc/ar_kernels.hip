@@ -926,13 +926,12 @@ __global__ __launch_bounds__(256) void ar_mlp_fused_kernel(GemvArgs a, const bf1
 #pragma unroll
     for (int i = 0; i < 3; ++i)
       wf[r][i] = *reinterpret_cast<const uint2*>(Wfc + (size_t)(n0 + wave * RW + r) * D + i * 256 + lane * 4);
-  uint4 wp[RB / 16][6];  // pack of 16 columns g: 96 contiguous bytes per thread
+  uint2 wp[RB / 4][3];  // column group g4 (4 columns), output third jj: 4 bf16 (pack_mproj layout)
 #pragma unroll
-  for (int g = 0; g < RB / 16; ++g) {
-    const uint4* pk = reinterpret_cast<const uint4*>(Wpk + (((size_t)blockIdx.x * (RB / 16) + g) * 256 + tid) * 48);
+  for (int g = 0; g < RB / 4; ++g)
 #pragma unroll
-    for (int i = 0; i < 6; ++i) wp[g][i] = pk[i];
-  }
+    for (int jj = 0; jj < 3; ++jj)
+      wp[g][jj] = reinterpret_cast<const uint2*>(Wpk)[(((size_t)blockIdx.x * (RB / 4) + g) * 3 + jj) * 256 + tid];
   if (wave < BG) wave_ln_to_lds(xv, a.ln_w, xs[wave], lane);
   __syncthreads();
   float acc[RW][BG];
@@ -967,16 +966,13 @@ __global__ __launch_bounds__(256) void ar_mlp_fused_kernel(GemvArgs a, const bf1
     for (int jj = 0; jj < 3; ++jj) {
       float t = 0.f;
 #pragma unroll
-      for (int g = 0; g < RB / 16; ++g)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const uint4 u = wp[g][jj * 2 + q];
-          const uint32_t wv[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-          for (int m = 0; m < 4; ++m)
-            t = fmaf(__uint_as_float(wv[m] & 0xffff0000u), hs[bb][16 * g + q * 8 + 2 * m + 1],
-                     fmaf(__uint_as_float(wv[m] << 16), hs[bb][16 * g + q * 8 + 2 * m], t));
-        }
+      for (int g = 0; g < RB / 4; ++g) {
+        const uint2 u = wp[g][jj];
+        t = fmaf(__uint_as_float(u.x << 16), hs[bb][4 * g], t);
+        t = fmaf(__uint_as_float(u.x & 0xffff0000u), hs[bb][4 * g + 1], t);
+        t = fmaf(__uint_as_float(u.y << 16), hs[bb][4 * g + 2], t);
+        t = fmaf(__uint_as_float(u.y & 0xffff0000u), hs[bb][4 * g + 3], t);
+      }
       atomicAdd(y + (size_t)bb * D + tid + 256 * jj, t);
     }
   }
@@ -2225,6 +2221,9 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
         if (g_opt_fuse_mlp == 2) {  // 32 h rows per block (96 blocks)
           if (B <= 1) hipLaunchKernelGGL((ar_mlp_fused_kernel<1, 32>), dim3(DFF / 32), dim3(256), 0, s, a, wfc, wpk);
           else hipLaunchKernelGGL((ar_mlp_fused_kernel<2, 32>), dim3(DFF / 32), dim3(256), 0, s, a, wfc, wpk);
+        } else if (g_opt_fuse_mlp == 3) {  // 12 h rows per block (256 blocks: one per CU)
+          if (B <= 1) hipLaunchKernelGGL((ar_mlp_fused_kernel<1, 12>), dim3(DFF / 12), dim3(256), 0, s, a, wfc, wpk);
+          else hipLaunchKernelGGL((ar_mlp_fused_kernel<2, 12>), dim3(DFF / 12), dim3(256), 0, s, a, wfc, wpk);
         } else {  // 16 h rows per block (192 blocks)
           if (B <= 1) hipLaunchKernelGGL((ar_mlp_fused_kernel<1, 16>), dim3(DFF / 16), dim3(256), 0, s, a, wfc, wpk);
           else hipLaunchKernelGGL((ar_mlp_fused_kernel<2, 16>), dim3(DFF / 16), dim3(256), 0, s, a, wfc, wpk);

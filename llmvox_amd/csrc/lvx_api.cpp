@@ -221,13 +221,15 @@ static std::vector<float> repack_conv(const std::vector<float>& w, int N, int C,
 
 // mlp.c_proj [768][3072] -> [3072/16 blocks][256 threads][3][16]: block k's thread t holds
 // W[t + 256 jj][16 k + j] as 96 contiguous bytes (bf16), the operand order of ar_mlp_fused_kernel
+// mlp.c_proj [768][3072] for ar_mlp_fused_kernel: groups of 4 columns k4, then the output row's
+// third jj (e = t + 256 jj), then thread t, 4 values: a wave's 8-byte load covers 512 contiguous bytes
 static std::vector<float> pack_mproj(const std::vector<float>& w) {
   std::vector<float> o((size_t)D * DFF);
   size_t q = 0;
-  for (int k = 0; k < DFF / 16; ++k)
-    for (int t = 0; t < 256; ++t)
-      for (int jj = 0; jj < 3; ++jj)
-        for (int j = 0; j < 16; ++j) o[q++] = w[(size_t)(t + 256 * jj) * DFF + 16 * k + j];
+  for (int k4 = 0; k4 < DFF / 4; ++k4)
+    for (int jj = 0; jj < 3; ++jj)
+      for (int t = 0; t < 256; ++t)
+        for (int j = 0; j < 4; ++j) o[q++] = w[(size_t)(t + 256 * jj) * DFF + 4 * k4 + j];
   return o;
 }
 
