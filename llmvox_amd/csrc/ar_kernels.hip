@@ -1178,11 +1178,14 @@ __global__ __launch_bounds__(256) void ar_attn_kernel(ArState st, int layer) {
 // direct = 1 (batched path with one split per (row, head)): the normalised head output goes
 // straight to the bf16 operand row xn, as the merge kernel would write it (o * (1 / l)), and the
 // merge kernel is skipped.
-template <typename TKV, int DEPTH>
-__global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer, int ns_max, int direct,
+template <typename TKV, int DEPTH, int NW>
+__global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int layer, int ns_max, int direct,
                                                          int selcopy) {
-  __shared__ float wm_s[4], wl_s[4];
-  __shared__ float wo_s[4][4][HD];  // [wave][16-lane row][part * 24 + i]
+  // NW waves: a tile is NW x 16 keys (4 lanes per key); NW = 8 doubles the bytes in flight per
+  // block for long splits (batched steps)
+  constexpr int TK = NW * 16;
+  __shared__ float wm_s[NW], wl_s[NW];
+  __shared__ float wo_s[NW][4][HD];  // [wave][16-lane row][part * 24 + i]
   const int sp = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   // selcopy (layer 0 of a deferred-select step): the records c_attn just built are in the shadow
@@ -1203,7 +1206,7 @@ __global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer, 
   const size_t base = (((size_t)layer * st.max_streams + s) * N_HEAD + head) * st.max_pos;
   const TKV* __restrict__ Kg = reinterpret_cast<const TKV*>(st.kc) + base * HD;
   const TKV* __restrict__ Vg = reinterpret_cast<const TKV*>(st.vc) + base * HD;
-  const int part = tid & 3, kq = tid >> 2;  // key slot within the 64-key tile
+  const int part = tid & 3, kq = tid >> 2;  // key slot within the TK-key tile
   float q[24];
   {
     const float* qg = st.q + (size_t)b * D + head * HD + part * 24;
@@ -1252,17 +1255,17 @@ __global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer, 
     m = mn;
   };
 #pragma unroll
-  for (int d = 0; d < DEPTH; ++d) issue(k0 + d * ATK, kpr[d], vpr[d]);
+  for (int d = 0; d < DEPTH; ++d) issue(k0 + d * TK, kpr[d], vpr[d]);
   // DEPTH 2 (few tiles per block, the B <= 2 step): leave after the last valid tile. DEPTH >= 4
   // (long splits, batched steps): whole groups of DEPTH tiles with no exit inside a group (a tile
   // past k1 is all-invalid: alpha = 1, p = 0), which keeps the compiler from draining every
   // outstanding load at the group boundary
-  for (int kb = k0; kb < k1; kb += DEPTH * ATK) {
+  for (int kb = k0; kb < k1; kb += DEPTH * TK) {
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d) {
-      if (DEPTH == 2 && d > 0 && kb + d * ATK >= k1) break;
-      tile(kb + d * ATK, kpr[d], vpr[d]);
-      issue(kb + (d + DEPTH) * ATK, kpr[d], vpr[d]);
+      if (DEPTH == 2 && d > 0 && kb + d * TK >= k1) break;
+      tile(kb + d * TK, kpr[d], vpr[d]);
+      issue(kb + (d + DEPTH) * TK, kpr[d], vpr[d]);
       if (DEPTH > 2) __builtin_amdgcn_sched_barrier(0);  // keep the refill right behind its tile
     }
   }
@@ -1282,10 +1285,12 @@ __global__ __launch_bounds__(256) void ar_attn_v2_kernel(ArState st, int layer, 
   if (lane == 0) { wm_s[wave] = m; wl_s[wave] = l; }
   __syncthreads();
   if (tid < HD) {
-    const float M = fmaxf(fmaxf(wm_s[0], wm_s[1]), fmaxf(wm_s[2], wm_s[3]));
+    float M = wm_s[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) M = fmaxf(M, wm_s[w]);
     float ov = 0.f, lv = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NW; ++w) {
       const float f = (wm_s[w] == -INFINITY) ? 0.f : expf(wm_s[w] - M);
       ov += f * ((wo_s[w][0][tid] + wo_s[w][1][tid]) + (wo_s[w][2][tid] + wo_s[w][3][tid]));
       lv += f * wl_s[w];
@@ -2050,7 +2055,10 @@ static void launch_bt(const GemvArgs& a, int ns_max, hipStream_t s) {
   else hipLaunchKernelGGL((ar_bt_kernel<K, 4, IN, OUT>), grid, block, 0, s, a, ns_max);
 }
 
-int g_opt_attn_depth = 2;  // KV tiles in flight per attention block for B > 2 (2, or 4 / 8 for whole
+int g_opt_attn_waves = 4;  // waves per attention block for B > 2 (4, or 8: 128-key tiles). us/step
+                           // 4 / 8 waves: B = 32 t = 256+ 149.4 / 153.7; B = 64 209.0 / 211.1;
+                           // B = 16 t = 1024+ 152.4 / 156.4; B = 8 t = 512+ 121.9 / 123.9
+int g_opt_attn_depth = 2;  // KV tiles in flight per attention block for B > 2 (2, or 4 for whole
                            // groups of tiles). us/step (tools/step_sweep.py) depth 2 / 4, after the DPP
                            // reductions: B = 32, t = 256+: 152.0 / 157.9; B = 64: 216.3 / 234.2 (with
                            // the ds_bpermute reductions depth 4 had won: 173.5 / 167.9, 248.8 / 242.4)
@@ -2069,17 +2077,18 @@ static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_
   if (g_opt_attn_v2 || kvdtype == LVX_DTYPE_FP8 || direct || selcopy) {
     dim3 grid(ns_max, N_HEAD, B);
     const bool deep = g_opt_attn_depth >= 4 && B > 2;  // B <= 2: ~1 tile per split at t <= 1024
-    if (kvdtype == LVX_DTYPE_BF16) {
-      if (deep && g_opt_attn_depth >= 8) hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 8>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
-      else if (deep) hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 4>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
-      else hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
-    } else if (kvdtype == LVX_DTYPE_FP8) {
-      if (deep) hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t, 4>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
-      else hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t, 2>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
-    } else {
-      if (deep) hipLaunchKernelGGL((ar_attn_v2_kernel<float, 4>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
-      else hipLaunchKernelGGL((ar_attn_v2_kernel<float, 2>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
-    }
+    const bool wide = g_opt_attn_waves >= 8 && B > 2;   // 8 waves (128-key tiles) per block
+    const dim3 blk(wide ? 512 : 256);
+#define LVX_ATTN(T)                                                                                       \
+    do {                                                                                                  \
+      if (wide) hipLaunchKernelGGL((ar_attn_v2_kernel<T, 2, 8>), grid, blk, 0, s, st, l, ns_max, direct, selcopy); \
+      else if (deep) hipLaunchKernelGGL((ar_attn_v2_kernel<T, 4, 4>), grid, blk, 0, s, st, l, ns_max, direct, selcopy); \
+      else hipLaunchKernelGGL((ar_attn_v2_kernel<T, 2, 4>), grid, blk, 0, s, st, l, ns_max, direct, selcopy); \
+    } while (0)
+    if (kvdtype == LVX_DTYPE_BF16) LVX_ATTN(bf16_t);
+    else if (kvdtype == LVX_DTYPE_FP8) LVX_ATTN(fp8_t);
+    else LVX_ATTN(float);
+#undef LVX_ATTN
   } else {
     dim3 grid(NSPLIT, N_HEAD, B);
     if (kvdtype == LVX_DTYPE_BF16) hipLaunchKernelGGL((ar_attn_kernel<bf16_t>), grid, dim3(256), 0, s, st, l);

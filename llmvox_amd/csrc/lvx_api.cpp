@@ -374,7 +374,13 @@ int lvx_finalize(lvx_ctx* c) {
   UP_F("backbone.pos_net.5.bias", cw.pn_b);
   for (int i = 0; i < 12; ++i) {
     std::string p = "backbone.convnext." + std::to_string(i) + ".";
-    UP_F(p + "dwconv.weight", cw.dw_w[i]);
+    {  // depthwise conv [768][1][7] -> tap-major [7][768] (16-byte weight loads in dwconv_adaln)
+      const std::vector<float>& dwv = c->H(p + "dwconv.weight");
+      std::vector<float> t(dwv.size());
+      for (int ch = 0; ch < 768; ++ch)
+        for (int k = 0; k < 7; ++k) t[(size_t)k * 768 + ch] = dwv[(size_t)ch * 7 + k];
+      if ((r = c->upload_f32(t, &cw.dw_w[i]))) return r;
+    }
     UP_F(p + "dwconv.bias", cw.dw_b[i]);
     UP_F(p + "norm.scale.weight", cw.cn_scale[i]);
     UP_F(p + "norm.shift.weight", cw.cn_shift[i]);
@@ -539,6 +545,7 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   else if (n == "codec_xcd") g_opt_codec_xcd = value;
   else if (n == "attn_blocks") g_opt_attn_blocks = value;
   else if (n == "attn_depth") g_opt_attn_depth = value;
+  else if (n == "attn_waves") g_opt_attn_waves = value;
   else if (n == "ln_stats") g_opt_ln_stats = value;
   else if (n == "codec_bm256") g_opt_codec_bm256 = value;
   else if (n == "b1_splits") g_opt_b1_splits = value;
