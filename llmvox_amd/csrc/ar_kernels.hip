@@ -406,7 +406,10 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
     const int n = row0 + r;
 #pragma unroll
     for (int it = 0; it < NI; ++it)
-      wr[r][it] = (n < a.N) ? WReg<TW>::load(W + (size_t)n * K + kp * KC + it * 256 + lane * 4) : WReg<TW>::zero();
+      // clamped row, unconditional load: a load under a branch makes the compiler drain every
+      // outstanding load (the prefetched inputs) before the weights are even issued; rows past N
+      // are never stored
+      wr[r][it] = WReg<TW>::load(W + (size_t)min(n, a.N - 1) * K + kp * KC + it * 256 + lane * 4);
   }
   if constexpr (IN == 5) {
     // commit the previous step's greedy select (argmax_commit's state advance; block 0 writes
@@ -697,7 +700,7 @@ __global__ __launch_bounds__(256) void ar_gemv_reg_kernel(GemvArgs a) {
     const int n = row0 + r;
 #pragma unroll
     for (int i = 0; i < NI; ++i)
-      wr[r][i] = (n < a.N) ? WReg<TW>::load(W + (size_t)n * K + kp * KC + i * 256 + lane * 4) : WReg<TW>::zero();
+      wr[r][i] = WReg<TW>::load(W + (size_t)min(n, a.N - 1) * K + kp * KC + i * 256 + lane * 4);  // clamped, unconditional
   }
   // 3. prologue math in registers
   if (IN == 3) {
@@ -841,7 +844,7 @@ __global__ __launch_bounds__(256) void ar_cproj_b1_kernel(GemvArgs a) {
   for (int r = 0; r < RPW; ++r)
 #pragma unroll
     for (int i = 0; i < 3; ++i)
-      wr[r][i] = (row0 + r < a.N) ? WReg<TW>::load(W + (size_t)(row0 + r) * D + i * 256 + lane * 4) : WReg<TW>::zero();
+      wr[r][i] = WReg<TW>::load(W + (size_t)min(row0 + r, a.N - 1) * D + i * 256 + lane * 4);  // clamped, unconditional
   if (tid < N_HEAD * NSPLIT) {
     const int t = ri.y + 1;
     const int ns = ri.x < 0 ? 0 : min(NS, (t + 63) / 64);
@@ -1591,6 +1594,17 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   const bf16_t* __restrict__ X = XM == 1 ? a.st.xb : ((KTOT == 768) ? a.st.xn : a.st.hb);
   const int wrow = min(n0 + (lane & 15), a.N - 1);
   const int k0 = blockIdx.y * K + wave * 192 + 8 * (lane >> 4);
+  // XM 1: the row statistics partials first (vmcnt retires in issue order, so the Chan combine
+  // waits for them alone while the weights and operand rows stream), by every thread (clamped
+  // row: no load under a branch), used by the first NT * 64
+  float2 sp[XM == 1 ? 12 : 1];
+  if constexpr (XM == 1) {
+    const int rr = min(tid >> 2, NT * 16 - 1), q = tid & 3;
+    const float2* xs = reinterpret_cast<const float2*>(a.st.xstat) + (size_t)min(rr, B - 1) * (D / 16) + q * 12;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) sp[j] = xs[j];
+    __builtin_amdgcn_sched_barrier(0);  // keep them ahead of the weight / operand loads
+  }
   uint4 wf[6], xf[NT][6];
 #pragma unroll
   for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(W + (size_t)wrow * KTOT + k0 + kk * 32);
@@ -1607,13 +1621,9 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
       g[kk][0] = *reinterpret_cast<const float4*>(a.ln_w + k0 + kk * 32);
       g[kk][1] = *reinterpret_cast<const float4*>(a.ln_w + k0 + kk * 32 + 4);
     }
-    if (tid < NT * 16 * 4) {  // 4 lanes per row, 12 column blocks each, all loads issued at once
+    if (tid < NT * 16 * 4) {  // 4 lanes per row, 12 column blocks each (loaded above)
       const int rr = tid >> 2, q = tid & 3;
-      const int b = min(rr, B - 1);
-      const float2* xs = reinterpret_cast<const float2*>(a.st.xstat) + (size_t)b * (D / 16) + q * 12;
-      float2 p[12];
-#pragma unroll
-      for (int j = 0; j < 12; ++j) p[j] = xs[j];
+      const float2 (&p)[12] = sp;
       float mean = 0.f, m2 = 0.f;  // Chan's combine of equal-count (16) groups, in a fixed order
 #pragma unroll
       for (int j = 0; j < 12; ++j) {
