@@ -173,7 +173,10 @@ template <> struct WReg<bf16_t> {
 };
 
 // LayerNorm of one 768-row held as 3 float4 per lane (one wave), written to xs
-__device__ __forceinline__ void wave_ln_to_lds(float4 (&v)[3], const float* __restrict__ lnw, float* xs_row, int lane) {
+// gamma (3 float4 per lane, k = j * 256 + lane * 4) is loaded by the caller ahead of the weight
+// stream: loaded here, after x, it was the last load issued, so waiting for it waited for every
+// weight load in flight as well
+__device__ __forceinline__ void wave_ln_to_lds(float4 (&v)[3], const float4 (&gam)[3], float* xs_row, int lane) {
   float s = 0.f;
 #pragma unroll
   for (int j = 0; j < 3; ++j) s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
@@ -189,7 +192,7 @@ __device__ __forceinline__ void wave_ln_to_lds(float4 (&v)[3], const float* __re
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int k = j * 256 + lane * 4;
-    const float4 g = *reinterpret_cast<const float4*>(lnw + k);
+    const float4 g = gam[j];
     *reinterpret_cast<float4*>(xs_row + k) =
         make_float4((v[j].x - mean) * rstd * g.x, (v[j].y - mean) * rstd * g.y, (v[j].z - mean) * rstd * g.z,
                     (v[j].w - mean) * rstd * g.w);
@@ -230,7 +233,7 @@ __device__ __forceinline__ void xrow_sum(const XRow<IN>& r, float4 (&v)[3]) {
 }
 
 template <int K, int IN>
-__device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, float* aux, int g0, int bg,
+__device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, float* aux, const float4 (&gam)[3], int g0, int bg,
                                                  const XRow<IN == 4 ? 4 : 0>& xpre, int4 ripre, bool prefetched) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   if (IN == 0 || IN == 3 || IN == 4 || IN == 5) {
@@ -294,7 +297,7 @@ __device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, f
 #pragma unroll
           for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = v[j];
       }
-      wave_ln_to_lds(v, a.ln_w, xs + bb * K, lane);
+      wave_ln_to_lds(v, gam, xs + bb * K, lane);
     }
   } else if (IN == 1) {
     for (int e = tid * 4; e < bg * K; e += 256 * 4)
@@ -393,11 +396,17 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
   LmGran lmg;
   int2 rxp = make_int2(0, 0);
   unsigned selpend = 0u;
-  if (IN == 5 && prefetched) {
-    ripre = a.st.rowinfo[wave];
-    rxp = a.st.rowx[wave];
+  if constexpr (IN == 5) {  // every wave, clamped row (no loads under a branch); used by waves < B
+    const int rb = min(wave, a.B - 1);
+    ripre = a.st.rowinfo[rb];
+    rxp = a.st.rowx[rb];
     selpend = *a.st.selp;
-    lmg_issue(a.st, wave, lane, lmg);
+    lmg_issue(a.st, rb, lane, lmg);
+  }
+  float4 gam[3];  // LayerNorm gamma of the LN input modes, ahead of the weights
+  if constexpr (IN == 0 || IN == 3 || IN == 4 || IN == 5) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) gam[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
   }
   const TW* __restrict__ W = reinterpret_cast<const TW*>(a.W);
   typename WReg<TW>::T wr[RPW][NI];
@@ -413,36 +422,36 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
   }
   if constexpr (IN == 5) {
     // commit the previous step's greedy select (argmax_commit's state advance; block 0 writes
-    // the shadow records, attention layer 0 copies them back) and build this step's record
-    if (prefetched) {
-      const int b = wave, s = ripre.x;
-      if (selpend && s >= 0) {
-        const Best r = lmg_reduce(lmg);
-        const int j = rxp.x, p = ripre.y + 1;
-        const int4 rn = make_int4(s, min(p, a.st.max_pos - 1), rxp.y, min(max(r.i, 0), VOCAB - 1));
-        if (blockIdx.x == 0 && lane == 0) {
-          if (p >= a.st.max_pos) atomicOr(a.st.err, 1);
-          if (j < a.st.plan_stride) {
-            a.st.tok_plan[(size_t)b * a.st.plan_stride + j] = r.i;
-            if (a.st.margin_plan) a.st.margin_plan[(size_t)b * a.st.plan_stride + j] = r.v - r.v2;
-          }
-          a.st.prev[s] = r.i;
-          a.st.pos[s] = p;
-          a.st.rowinfo_n[b] = rn;
-          a.st.rowx_n[b] = make_int2(j + 1, plan_tok(a.st, b, j + 2));
+    // the shadow records, attention layer 0 copies them back) and build this step's record. The
+    // reduction and the record select run unconditionally so that the granule loads stay in the
+    // prologue (used only under a branch, the compiler sinks them into it: one more round trip).
+    const Best r = lmg_reduce(lmg);
+    const int s = ripre.x, j = rxp.x, p = ripre.y + 1;
+    const bool take = selpend && s >= 0;
+    const int4 rn = take ? make_int4(s, min(p, a.st.max_pos - 1), rxp.y, min(max(r.i, 0), VOCAB - 1)) : ripre;
+    if (prefetched && blockIdx.x == 0 && lane == 0) {
+      const int b = wave;
+      if (take) {
+        if (p >= a.st.max_pos) atomicOr(a.st.err, 1);
+        if (j < a.st.plan_stride) {
+          a.st.tok_plan[(size_t)b * a.st.plan_stride + j] = r.i;
+          if (a.st.margin_plan) a.st.margin_plan[(size_t)b * a.st.plan_stride + j] = r.v - r.v2;
         }
-        ripre = rn;
-      } else if (blockIdx.x == 0 && lane == 0) {
-        a.st.rowinfo_n[b] = ripre;
-        a.st.rowx_n[b] = rxp;
+        a.st.prev[s] = r.i;
+        a.st.pos[s] = p;
       }
-      if (lane == 0) ri_s[b] = ripre;
+      // the next text id is looked up by attention layer 0's copier (a dependent load here would
+      // hold this block until its weight loads landed: vmcnt retires in order)
+      a.st.rowx_n[b] = make_int2(take ? j + 1 : j, 0);
+      a.st.rowinfo_n[b] = rn;
     }
+    ripre = rn;
+    if (prefetched && lane == 0) ri_s[wave] = rn;
   }
   for (int g0 = 0; g0 < a.B; g0 += BG) {
     const int bg = min(BG, a.B - g0);
     if (g0) __syncthreads();
-    gemv_stage_input<K, IN>(a, xs, aux, g0, bg, xpre, ripre, prefetched);
+    gemv_stage_input<K, IN>(a, xs, aux, gam, g0, bg, xpre, ripre, prefetched);
     __syncthreads();
     float acc[RPW][BG];
 #pragma unroll
@@ -918,10 +927,12 @@ __global__ __launch_bounds__(256) void ar_mlp_fused_kernel(GemvArgs a, const bf1
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int n0 = blockIdx.x * RB;
   // issue order: x rows (LayerNorm input), c_fc rows, packed c_proj columns
-  float4 xv[3];
+  float4 xv[3], gam[3];
   if (wave < BG) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) xv[j] = *reinterpret_cast<const float4*>(a.st.x + (size_t)wave * D + j * 256 + lane * 4);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) gam[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
   }
   uint2 wf[RW][3];
 #pragma unroll
@@ -935,7 +946,7 @@ __global__ __launch_bounds__(256) void ar_mlp_fused_kernel(GemvArgs a, const bf1
 #pragma unroll
     for (int jj = 0; jj < 3; ++jj)
       wp[g][jj] = reinterpret_cast<const uint2*>(Wpk)[(((size_t)blockIdx.x * (RB / 4) + g) * 3 + jj) * 256 + tid];
-  if (wave < BG) wave_ln_to_lds(xv, a.ln_w, xs[wave], lane);
+  if (wave < BG) wave_ln_to_lds(xv, gam, xs[wave], lane);
   __syncthreads();
   float acc[RW][BG];
 #pragma unroll
@@ -1193,14 +1204,24 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   // selcopy (layer 0 of a deferred-select step): the records c_attn just built are in the shadow
   // arrays; one block per row copies them back for the rest of the step and clears the flag
+  // (the next text id, a dependent plan load, is looked up at the end of the block, when every
+  // other load has landed)
   const int4 ri = selcopy ? st.rowinfo_n[b] : st.rowinfo[b];
-  if (selcopy && sp == 0 && head == 0 && tid == 0) {
+  const bool cp = selcopy && sp == 0 && head == 0 && tid == 0;
+  int jn = 0;
+  if (cp) {
+    jn = st.rowx_n[b].x;
     st.rowinfo[b] = ri;
-    st.rowx[b] = st.rowx_n[b];
     if (b == 0) *st.selp = 0u;
   }
+  auto copy_tail = [&]() {
+    if (cp) st.rowx[b] = make_int2(jn, plan_tok(st, b, jn + 1));
+  };
   const int s = ri.x;
-  if (s < 0) return;
+  if (s < 0) {
+    copy_tail();
+    return;
+  }
   const int t = ri.y + 1;
   const int ns = min(ns_max, (t + ATK - 1) / ATK);
   if (sp >= ns) return;
@@ -1287,6 +1308,7 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
   }
   if (lane == 0) { wm_s[wave] = m; wl_s[wave] = l; }
   __syncthreads();
+  copy_tail();
   if (tid < HD) {
     float M = wm_s[0];
 #pragma unroll
