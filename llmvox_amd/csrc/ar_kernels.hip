@@ -1499,14 +1499,13 @@ __global__ __launch_bounds__(256) void ar_embed_select_kernel(GemvArgs a) {
   int4 ri = a.st.rowinfo[b];
   const int2 rx = a.st.rowx[b];  // {plan step j, text id of step j + 1}
   const unsigned pend = a.st.selrow[b];
+  float4 g[3];  // LN gamma first: the reduction's wait for the logits then covers it too
+#pragma unroll
+  for (int j = 0; j < 3; ++j) g[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
   const float4* lg = reinterpret_cast<const float4*>(a.st.logits + (size_t)b * VOCAB);
   float4 lv[VOCAB / 1024];
 #pragma unroll
   for (int k = 0; k < VOCAB / 1024; ++k) lv[k] = lg[k * 256 + tid];
-  float4 g[3];
-  if (wave == 0)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) g[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
   Best bt{-INFINITY, -INFINITY, 0x7fffffff};
 #pragma unroll
   for (int k = 0; k < VOCAB / 1024; ++k) {
@@ -1520,7 +1519,8 @@ __global__ __launch_bounds__(256) void ar_embed_select_kernel(GemvArgs a) {
   if (lane == 0) { sv[wave] = bt.v; sv2[wave] = bt.v2; si[wave] = bt.i; }
   __syncthreads();
   if (wave != 0) return;
-  if (pend && ri.x >= 0) {
+  const bool take = pend && ri.x >= 0;
+  if (take) {
     Best r{sv[0], sv2[0], si[0]};
 #pragma unroll
     for (int w = 1; w < 4; ++w) r = best_merge(r, Best{sv[w], sv2[w], si[w]});
@@ -1536,7 +1536,6 @@ __global__ __launch_bounds__(256) void ar_embed_select_kernel(GemvArgs a) {
       a.st.pos[s] = p;
       a.st.rowstep[b] = j + 1;
       a.st.rowinfo[b] = rn;
-      a.st.rowx[b] = make_int2(j + 1, plan_tok(a.st, b, j + 2));
     }
     ri = rn;
   }
@@ -1549,6 +1548,8 @@ __global__ __launch_bounds__(256) void ar_embed_select_kernel(GemvArgs a) {
   uint2* dst = reinterpret_cast<uint2*>(a.st.xn + (size_t)b * D);
 #pragma unroll
   for (int j = 0; j < 3; ++j) dst[j * 64 + lane] = pack4_bf16(v[j]);
+  // the plan load for the next text id last: waiting for it earlier held the embedding loads
+  if (take && lane == 0) a.st.rowx[b] = make_int2(rx.x + 1, plan_tok(a.st, b, rx.x + 2));
 }
 
 // split-KV merge for the batched path: y[b] (bf16) into st.xn. NS = ns_max (the attention's split
