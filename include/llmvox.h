@@ -123,10 +123,16 @@ int lvx_stream_set(lvx_ctx* ctx, int slot, int pos, int prev_token, void* stream
 int lvx_probe_kernel(lvx_ctx* ctx, int which, int B, const int32_t* slots_dev, int iters, void* stream);
 /* Host-side view of a slot's position (synchronises the stream). */
 int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
-/* Kernel-variant switches for in-process A/B timing: "gemv_reg" (register-path GEMV, B <= 4),
- * "attn_v2", "cproj_b1", "prefetch_in", "mfma_batch" (smallest B of the bf16 MFMA path, up to 32; 0 off),
- * "fuse_mlp" (bf16 fused MLP, B <= 2), "fuse_argmax" (greedy select inside lm_head, B <= 4),
- * "mfma_ln" (largest B whose batched GEMMs normalise their rows in the prologue, default 16). */
+/* Kernel-variant switches for in-process A/B timing (defaults and measurements: DESIGN.md §4 and
+ * the comments at their definitions in ar_kernels.hip / codec_kernels.hip): "gemv_reg"
+ * (register-path GEMV, B <= 4), "attn_v2", "cproj_b1", "prefetch_in", "mfma_batch" (smallest B of
+ * the bf16 MFMA path; 0 off), "fuse_mlp" (bf16 fused MLP, B <= 2: 1 = 16 h rows per block, 2 = 32,
+ * 3 = 12; 0 off), "fuse_argmax" (greedy select inside lm_head, B <= 4), "defer_select" (greedy
+ * select in the next step's first kernel: 1 = B <= 2 and B >= 4, 2 = also B = 3, 0 = separate
+ * argmax kernel), "mfma_ln" (largest B whose batched GEMMs normalise their rows in the prologue),
+ * "bt" / "bt_rows" / "bt_merge" (batched v3 path), "ln_stats", "attn_blocks", "attn_depth",
+ * "attn_waves", "b1_splits", "codec_g2", "codec_g2_min", "codec_xcd", "codec_bm256".
+ * Every option yields the same tokens (tested); changing one drops the captured graphs. */
 int lvx_set_option(lvx_ctx* ctx, const char* name, int value);
 /* Enable/disable HIP-graph replay of lvx_ar_step for a given B (default on). */
 int lvx_set_graphs(lvx_ctx* ctx, int enable);
