@@ -132,7 +132,8 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
  * argmax kernel), "mfma_ln" (largest B whose batched GEMMs normalise their rows in the prologue),
  * "bt" / "bt_rows" / "bt_merge" (batched v3 path), "ln_stats", "attn_blocks", "attn_depth",
  * "attn_waves", "b1_splits", "codec_g2", "codec_g2_min", "codec_xcd", "codec_bm256".
- * Every option yields the same tokens (tested); changing one drops the captured graphs. */
+ * The variants compute the same step (bit-equal or within bf16 rounding: tests/test_gpu_select.py,
+ * tests/test_gpu_batched.py); changing an option drops the captured graphs. */
 int lvx_set_option(lvx_ctx* ctx, const char* name, int value);
 /* Enable/disable HIP-graph replay of lvx_ar_step for a given B (default on). */
 int lvx_set_graphs(lvx_ctx* ctx, int enable);
