@@ -1637,6 +1637,9 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
 #pragma unroll
     for (int kk = 0; kk < 6; ++kk) xf[t][kk] = *reinterpret_cast<const uint4*>(X + (size_t)b * KTOT + k0 + kk * 32);
   }
+  // every operand load in flight before the first MFMA (left to itself the scheduler interleaves
+  // them with the MFMAs: ~7 KB in flight per wave instead of (6 + 6 NT) KB)
+  __builtin_amdgcn_sched_barrier(0);
   if constexpr (XM == 1) {
     float4 g[6][2];
 #pragma unroll
