@@ -99,7 +99,9 @@ int lvx_ar_forward_row(lvx_ctx* ctx, int slot, int pos, const float* emb_row_dev
  * (and margin_plan[b][j] = top1 - top2 logit, optional), stores the token as the slot's
  * prev_token, advances the slot's position and rowstep[b]. text_plan / tok_plan /
  * margin_plan are [B][plan_stride] device arrays, so a whole chunk of steps can be enqueued
- * back to back (replayed as a HIP graph) and read back once. */
+ * back to back (replayed as a HIP graph) and read back once. Inside a call the select of step i
+ * is committed by the first kernel of step i + 1 (option "defer_select"); the last one by a
+ * closing kernel of the call, so every output is in place when the call's work on `stream` is. */
 int lvx_ar_step(lvx_ctx* ctx, int B, const int32_t* slots_dev, const int32_t* text_plan_dev,
                 int plan_stride, int32_t* rowstep_dev, int32_t* tok_plan_dev, float* margin_plan_dev,
                 void* stream);
