@@ -1617,6 +1617,21 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   const bf16_t* __restrict__ X = XM == 1 ? a.st.xb : ((KTOT == 768) ? a.st.xn : a.st.hb);
   const int wrow = min(n0 + (lane & 15), a.N - 1);
   const int k0 = blockIdx.y * K + wave * 192 + 8 * (lane >> 4);
+  // epilogue operands first (a load in the epilogue is one more dependent round trip): thread tid
+  // stores elements e = tid + k * NW * 64, all of batch row tid % (NT * 16) (NW * 64 is a multiple
+  // of NT * 16): its control record (OUT 0, KV append) or its x values (OUT 7, residual)
+  constexpr int EPT = (16 * NT * 16 + NW * 64 - 1) / (NW * 64);
+  static_assert((NW * 64) % (NT * 16) == 0, "one batch row per thread in the epilogue");
+  int4 ripre = make_int4(-1, 0, 0, 0);
+  float xpre[OUT == 7 ? EPT : 1];
+  if constexpr (OUT == 0) ripre = a.st.rowinfo[min(tid % (NT * 16), B - 1)];
+  if constexpr (OUT == 7) {
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+      const int e = min(tid + k * NW * 64, 16 * NT * 16 - 1), r = e / (NT * 16), b = e - r * (NT * 16);
+      xpre[k] = a.st.x[(size_t)min(b, B - 1) * D + min(n0 + r, a.N - 1)];
+    }
+  }
   // XM 1: the row statistics partials first (vmcnt retires in issue order, so the Chan combine
   // waits for them alone while the weights and operand rows stream), by every thread (clamped
   // row: no load under a branch), used by the first NT * 64
@@ -1704,16 +1719,25 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) red[wave][(4 * (lane >> 4) + i) * (NT * 16) + t * 16 + (lane & 15)] = acc[t][i];
   __syncthreads();
-  for (int e = tid; e < 16 * NT * 16; e += NW * 64) {
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int e = tid + k * NW * 64;
+    if (e >= 16 * NT * 16) break;
     const int r = e / (NT * 16), b = e - r * (NT * 16), n = n0 + r;
     if (b >= B || n >= a.N) continue;
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) v += red[w][e];
-    if (OUT == 5) {
+    if (OUT == 0 && n >= D) {  // K / V append at the row's (slot, pos), record prefetched
+      const int c = (n - D) % D, which = (n - D) / D;
+      const int head = c / HD, d = c - head * HD;
+      if (ripre.x < 0) continue;
+      const size_t idx = ((((size_t)a.layer * a.st.max_streams + ripre.x) * N_HEAD + head) * a.st.max_pos + ripre.y) * HD + d;
+      store_kv(a, which, idx, v);
+    } else if (OUT == 5) {
       a.st.hb[(size_t)b * DFF + n] = f32_to_bf16(gelu_tanh(v));
     } else if (OUT == 7) {
-      const float xn = a.st.x[(size_t)b * D + n] + v;
+      const float xn = xpre[k] + v;
       a.st.x[(size_t)b * D + n] = xn;
       a.st.xb[(size_t)b * D + n] = f32_to_bf16(xn);
       xo[e] = xn;
