@@ -1840,29 +1840,37 @@ __global__ __launch_bounds__(256) void ar_mfma_ln_kernel(GemvArgs a) {
   const int n0 = blockIdx.x * 16;
   const int B = a.B;
   // 1. row inputs (x rows or control records) first, then the weight fragments
-  float4 xv[RW][3];
+  // (clamped rows, unconditional loads: a load under a branch drains everything in flight; the
+  // pending copies of the first YR rows come with them, the rest are loaded in step 2)
+  constexpr int YR = MODE == 4 ? (RW < 2 ? RW : 2) : 0;
+  float4 xv[RW][3], ya[YR > 0 ? YR : 1][YCOPIES][3];
   int4 ri[RW];
 #pragma unroll
   for (int i = 0; i < RW; ++i) {
-    const int b = wave + NW * i;
-    if (b < B) {
-      if (MODE == 0 || MODE == 4) {
+    const int b = min(wave + NW * i, B - 1);
+    if (MODE == 0 || MODE == 4) {
 #pragma unroll
-        for (int j = 0; j < 3; ++j) xv[i][j] = *reinterpret_cast<const float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4);
-      } else {
-        ri[i] = a.st.rowinfo[b];
-      }
+      for (int j = 0; j < 3; ++j) xv[i][j] = *reinterpret_cast<const float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4);
+    } else {
+      ri[i] = a.st.rowinfo[b];
     }
+    if (i < YR)
+#pragma unroll
+      for (int c = 0; c < YCOPIES; ++c)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          ya[i < YR ? i : 0][c][j] = *reinterpret_cast<const float4*>(a.yacc + ((size_t)c * a.st.max_streams + b) * D + j * 256 + lane * 4);
   }
   const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(a.W);
   const int wrow = min(n0 + (lane & 15), a.N - 1);
   const int k0 = wave * 192 + 8 * (lane >> 4);
+  float4 g[3];  // gamma ahead of the weights (the first LayerNorm waits for it)
+#pragma unroll
+  for (int j = 0; j < 3; ++j) g[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
+  __builtin_amdgcn_sched_barrier(0);  // (the scheduler otherwise moves them behind the weights)
   uint4 wf[6];
 #pragma unroll
   for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(W + (size_t)wrow * K + k0 + kk * 32);
-  float4 g[3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) g[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
   // 2. rows -> LayerNorm -> bf16 tile (rows >= B are zero: padded columns, never stored)
 #pragma unroll
   for (int i = 0; i < RW; ++i) {
@@ -1879,7 +1887,8 @@ __global__ __launch_bounds__(256) void ar_mfma_ln_kernel(GemvArgs a) {
         for (int c = 0; c < YCOPIES; ++c)
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
-            const float4 y = *reinterpret_cast<const float4*>(a.yacc + ((size_t)c * a.st.max_streams + b) * D + j * 256 + lane * 4);
+            const float4 y = i < YR ? ya[i < YR ? i : 0][c][j]
+                                    : *reinterpret_cast<const float4*>(a.yacc + ((size_t)c * a.st.max_streams + b) * D + j * 256 + lane * 4);
             xv[i][j].x += y.x; xv[i][j].y += y.y; xv[i][j].z += y.z; xv[i][j].w += y.w;
           }
       }
@@ -1965,22 +1974,21 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_bt_kernel(GemvArgs a, int ns_
       float4 xv[4][3];
       int4 ri[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int b = r0 + wave * RPW + gi + i;
-        if (b < B) {
-          if (IN == 0) {
+      for (int i = 0; i < 4; ++i) {  // clamped row, unconditional loads (rows past B are not stored)
+        const int b = min(r0 + wave * RPW + gi + i, B - 1);
+        if (IN == 0) {
 #pragma unroll
-            for (int j = 0; j < 3; ++j) xv[i][j] = *reinterpret_cast<const float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4);
-          } else {
-            ri[i] = a.st.rowinfo[b];
-          }
+          for (int j = 0; j < 3; ++j) xv[i][j] = *reinterpret_cast<const float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4);
+        } else {
+          ri[i] = a.st.rowinfo[b];
         }
       }
-      if (gi == 0) {  // weights behind the first row group's inputs (vmcnt retires in issue order)
-#pragma unroll
-        for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(W + (size_t)wrow * K + k0 + kk * 32);
+      if (gi == 0) {  // gamma, then the weights, behind the first row group's inputs (vmcnt retires in issue order)
 #pragma unroll
         for (int j = 0; j < 3; ++j) g[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
+        __builtin_amdgcn_sched_barrier(0);  // (the scheduler otherwise moves them behind the weights)
+#pragma unroll
+        for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(W + (size_t)wrow * K + k0 + kk * 32);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
