@@ -115,7 +115,7 @@ __device__ __forceinline__ void store_out(TC* p, float v);
 template <> __device__ __forceinline__ void store_out<float>(float* p, float v) { *p = v; }
 template <> __device__ __forceinline__ void store_out<bf16_t>(bf16_t* p, float v) { *p = f32_to_bf16(v); }
 
-template <bool BF, typename TA, typename TB, int AMODE, int EPI, typename TC>
+template <bool BF, typename TA, typename TB, int AMODE, int EPI, typename TC, bool KF>
 __global__ __launch_bounds__(256) void gemm_mfma_kernel(GemmArgs g) {
   constexpr int LDSZ = BF ? (BM * LDH / 2) : (BM * LDF);  // in floats
   __shared__ __attribute__((aligned(16))) float As_[LDSZ];
@@ -134,7 +134,34 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(GemmArgs g) {
   const int kt_per = (nkt + g.ksplit - 1) / g.ksplit;
   const int kt0 = ks * kt_per, kt1 = min(nkt, kt0 + kt_per);
 
+  // KF (K a multiple of BK: every weight GEMM): branch-free loads — clamped row / tap, the load
+  // always issued, zeros selected afterwards (a load under a branch made the compiler wait for
+  // every outstanding load: the k-tile's loads ran one round trip each)
+  const int amc = min(am, g.M - 1), bnc = min(bn, g.N - 1);
+  auto load_tile_kf = [&](int kt, float* av, float* bv) {
+    const int k = kt * BK + lseg;
+    bool aok = am < g.M;
+    if (AMODE == A_PLAIN) {
+      load8<TA>(A + (size_t)amc * g.lda + k, av);
+    } else {
+      const int tap = k / g.cin, c = k - tap * g.cin;
+      const int tt = at + tap - (g.taps - 1) / 2;
+      aok = aok && tt >= 0 && tt < g.L;
+      load8<TA>(A + ((size_t)ab * g.L + min(max(tt, 0), g.L - 1)) * g.cin + c, av);
+    }
+    load8<TB>(W + (size_t)bnc * g.ldw + k, bv);
+    const bool bok = bn < g.N;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      av[i] = aok ? av[i] : 0.f;
+      bv[i] = bok ? bv[i] : 0.f;
+    }
+  };
   auto load_tile = [&](int kt, float* av, float* bv) {
+    if constexpr (KF) {
+      load_tile_kf(kt, av, bv);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) { av[i] = 0.f; bv[i] = 0.f; }
     const int k = kt * BK + lseg;
@@ -165,9 +192,9 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(GemmArgs g) {
   f32x16 acc;
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-  float av[8], bv[8];
-  if (kt0 < kt1) load_tile(kt0, av, bv);
-  for (int kt = kt0; kt < kt1; ++kt) {
+  // stage a k-tile's registers into LDS, then its MFMAs (both waves of a pair of k-tiles share the
+  // LDS tiles: barrier before overwriting, barrier before reading)
+  auto stage = [&](const float* av, const float* bv) {
     __syncthreads();  // the previous tile's LDS reads are done
     if (BF) {
       bf16_t* As = reinterpret_cast<bf16_t*>(As_);
@@ -182,7 +209,8 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(GemmArgs g) {
       }
     }
     __syncthreads();
-    if (kt + 1 < kt1) load_tile(kt + 1, av, bv);  // in flight during the MFMAs below
+  };
+  auto mma = [&]() {
     if (BF) {
       const bf16_t* As = reinterpret_cast<const bf16_t*>(As_);
       const bf16_t* Bs = reinterpret_cast<const bf16_t*>(Bs_);
@@ -198,8 +226,46 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(GemmArgs g) {
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 2) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ar[kk], Br[kk], acc, 0, 0, 0);
     }
+  };
+  if (KF) {
+    // two k-tiles in flight: tile kt + 2 is loaded into the register set tile kt just left (its
+    // index clamped to the split's last tile: the load is always issued, no branch around it)
+    float av0[8], bv0[8], av1[8], bv1[8];
+    if (kt0 < kt1) {
+      load_tile(kt0, av0, bv0);
+      load_tile(min(kt0 + 1, kt1 - 1), av1, bv1);
+    }
+    for (int kt = kt0; kt < kt1; kt += 2) {
+      stage(av0, bv0);
+      load_tile(min(kt + 2, kt1 - 1), av0, bv0);
+      mma();
+      if (kt + 1 >= kt1) break;
+      stage(av1, bv1);
+      load_tile(min(kt + 3, kt1 - 1), av1, bv1);
+      mma();
+    }
+  } else {
+    float av[8], bv[8];
+    if (kt0 < kt1) load_tile(kt0, av, bv);
+    for (int kt = kt0; kt < kt1; ++kt) {
+      stage(av, bv);
+      if (kt + 1 < kt1) load_tile(kt + 1, av, bv);  // in flight during the MFMAs below
+      mma();
+    }
   }
-  const int col = n0 + wn * 32 + (lane & 31);
+  const int col = n0 + wn * 32 + (lane & 31), colc = min(col, g.N - 1);
+  // epilogue operands loaded unconditionally (clamped row / column) before any branch
+  const float* R = g.res ? g.res + zb * g.sR : nullptr;
+  const float bias = (EPI != E_SCALE && g.bias) ? g.bias[colc] : 0.f;
+  const float gam = (EPI == E_BIAS_GAMMA_RES) ? g.gamma[colc] : 0.f;
+  float rv[16];
+  if (EPI == E_BIAS_GAMMA_RES || EPI == E_BIAS_RES) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = min(m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), g.M - 1);
+      rv[r] = (g.ksplit > 1) ? 0.f : R[(size_t)row * g.ldr + colc];
+    }
+  }
   if (col >= g.N) return;
   if (g.ksplit > 1) {  // raw partial tile -> ws[ks][zb][M][N]
     float* P = g.ws + ((size_t)ks * gridDim.z / g.ksplit + zb) * (size_t)g.M * g.N;
@@ -211,13 +277,23 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(GemmArgs g) {
     return;
   }
   TC* C = reinterpret_cast<TC*>(g.C) + zb * g.sC;
-  const float* R = g.res ? g.res + zb * g.sR : nullptr;
-  const float bias = (EPI != E_SCALE && g.bias) ? g.bias[col] : 0.f;
-  const float gam = (EPI == E_BIAS_GAMMA_RES) ? g.gamma[col] : 0.f;
+  // outputs computed before any row guard: the empty asm takes them as inputs, so the waits for
+  // the epilogue loads happen once here. Computed inside each guarded store, every store block
+  // re-waited vmcnt(0) (the skip edge leaves the loads "pending") and the 16 stores ran one
+  // write acknowledgement apart.
+  float o[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if (row < g.M) store_out<TC>(C + (size_t)row * g.ldc + col, gemm_epi<EPI>(g, R, row, col, acc[r], bias, gam));
+    if (EPI == E_BIAS_GAMMA_RES) o[r] = rv[r] + gam * (acc[r] + bias);
+    else if (EPI == E_BIAS_RES) o[r] = rv[r] + (acc[r] + bias);
+    else o[r] = gemm_epi<EPI>(g, R, row, col, acc[r], bias, gam);
+    asm volatile("" : "+v"(o[r]));
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (row < g.M) store_out<TC>(C + (size_t)row * g.ldc + col, o[r]);
   }
 }
 
@@ -251,7 +327,8 @@ static void gemm_launch(GemmArgs g, int batch, hipStream_t s) {
   while (tiles * ks * 2 <= 320 && nkt / (ks * 2) >= 4 && (size_t)(ks * 2) * g.M * g.N * batch <= g_ws_floats) ks *= 2;
   g.ksplit = ks;
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, batch * ks);
-  hipLaunchKernelGGL((gemm_mfma_kernel<BF, TA, TB, AMODE, EPI, TC>), grid, dim3(256), 0, s, g);
+  if (g.K % BK == 0) hipLaunchKernelGGL((gemm_mfma_kernel<BF, TA, TB, AMODE, EPI, TC, true>), grid, dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((gemm_mfma_kernel<BF, TA, TB, AMODE, EPI, TC, false>), grid, dim3(256), 0, s, g);
   if (ks > 1) {
     const size_t total = (size_t)g.M * g.N * batch;
     const int blocks = (int)std::min<size_t>((total + 255) / 256, 2048);

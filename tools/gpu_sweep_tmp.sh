@@ -1,8 +1,10 @@
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONPATH=.
-rm -f gpurun_out/sweep.log
-for BP in "32 256" "32 512" "64 512" "16 1024"; do
-  timeout -k 10 200 python -u tools/probe_ops.py $BP attn_depth=2 attn_depth=4 attn_depth=2 attn_depth=4 >> gpurun_out/sweep.log 2>&1 || exit 1
-done
-grep -v amdgpu.ids gpurun_out/sweep.log
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_codec_bf16.py tests/test_gpu_fp8.py tests/test_gpu_streaming.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/tests.log 2>&1 \
+ && timeout -k 10 200 python -u tools/codec_sweep.py 1:10,1:30,1:90,2:90,1:160,8:90 "" > gpurun_out/sweep.log 2>&1 \
+ && LVX_LIB_PATH=$PWD/llmvox_amd/libllmvox_hip_ab.so timeout -k 10 200 python -u tools/codec_sweep.py 1:10,1:30,1:90,2:90,1:160,8:90 "" >> gpurun_out/sweep.log 2>&1
+rc=$?
+grep -E "passed|failed|Error" gpurun_out/tests.log | tail -5
+cat gpurun_out/sweep.log | grep -v amdgpu.ids
+exit $rc
