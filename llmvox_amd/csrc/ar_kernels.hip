@@ -1472,6 +1472,8 @@ __global__ __launch_bounds__(256) void ar_rows_kernel(GemvArgs a) {
   if (MODE == 0 || MODE == 4) {
     XRow<MODE> r;
     xrow_issue(a, b, lane, r);
+    __builtin_amdgcn_sched_barrier(0);  // gamma and the rows issued up front (the scheduler sank a
+                                        // gamma load behind the variance: one more round trip)
     xrow_sum(r, v);
     if (MODE == 4)  // fold the pending copies into x here (one wave owns the row): the next c_proj
 #pragma unroll      // then adds its output to a final x instead of re-reading the copies

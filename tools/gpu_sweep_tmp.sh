@@ -1,13 +1,10 @@
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONPATH=.
-timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/b1.jsonl 2> gpurun_out/b1.err \
- && timeout -k 10 200 python -u tools/step_sweep.py 1 1024 "" "" > gpurun_out/sweep.log 2>&1 \
- && timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/b2.jsonl 2> gpurun_out/b2.err
+timeout -k 10 400 python -u -m pytest tests/test_gpu_batched.py tests/test_gpu_select.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/tests.log 2>&1 \
+ && timeout -k 10 200 python -u tools/step_sweep.py 32 256 "" "" "" > gpurun_out/sweep.log 2>&1 \
+ && timeout -k 10 200 python -u tools/step_sweep.py 16 256 "" "" >> gpurun_out/sweep.log 2>&1
 rc=$?
-for f in gpurun_out/b1.jsonl gpurun_out/b2.jsonl; do python -c "
-import json
-d=json.loads(open('$f').read().strip().splitlines()[-1])
-print('$f', d['value'], d['ms_per_step'], d['roofline']['kernel'], d['roofline']['frac'], {k:v['avg_us'] for k,v in d['kernels'].items()})"; done
+grep -E "passed|failed|Error" gpurun_out/tests.log | tail -5
 cat gpurun_out/sweep.log | grep -v amdgpu.ids
 exit $rc
