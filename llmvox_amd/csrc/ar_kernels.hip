@@ -1614,6 +1614,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   __shared__ float2 rs[XM == 1 ? NT * 16 : 1];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int n0 = blockIdx.x * 16;
+  const int r0 = blockIdx.z * (NT * 16);  // first batch row of this block's tile (grid.z batch tiles)
   const int B = a.B;
   const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(a.W);
   const bf16_t* __restrict__ X = XM == 1 ? a.st.xb : ((KTOT == 768) ? a.st.xn : a.st.hb);
@@ -1626,12 +1627,12 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   static_assert((NW * 64) % (NT * 16) == 0, "one batch row per thread in the epilogue");
   int4 ripre = make_int4(-1, 0, 0, 0);
   float xpre[OUT == 7 ? EPT : 1];
-  if constexpr (OUT == 0) ripre = a.st.rowinfo[min(tid % (NT * 16), B - 1)];
+  if constexpr (OUT == 0) ripre = a.st.rowinfo[min(r0 + tid % (NT * 16), B - 1)];
   if constexpr (OUT == 7) {
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
       const int e = min(tid + k * NW * 64, 16 * NT * 16 - 1), r = e / (NT * 16), b = e - r * (NT * 16);
-      xpre[k] = a.st.x[(size_t)min(b, B - 1) * D + min(n0 + r, a.N - 1)];
+      xpre[k] = a.st.x[(size_t)min(r0 + b, B - 1) * D + min(n0 + r, a.N - 1)];
     }
   }
   // XM 1: the row statistics partials first (vmcnt retires in issue order, so the Chan combine
@@ -1640,7 +1641,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   float2 sp[XM == 1 ? 12 : 1];
   if constexpr (XM == 1) {
     const int rr = min(tid >> 2, NT * 16 - 1), q = tid & 3;
-    const float2* xs = reinterpret_cast<const float2*>(a.st.xstat) + (size_t)min(rr, B - 1) * (D / 16) + q * 12;
+    const float2* xs = reinterpret_cast<const float2*>(a.st.xstat) + (size_t)min(r0 + rr, B - 1) * (D / 16) + q * 12;
 #pragma unroll
     for (int j = 0; j < 12; ++j) sp[j] = xs[j];
     __builtin_amdgcn_sched_barrier(0);  // keep them ahead of the weight / operand loads
@@ -1650,7 +1651,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(W + (size_t)wrow * KTOT + k0 + kk * 32);
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    const int b = min(t * 16 + (lane & 15), B - 1);  // padded columns recompute row B-1, never stored
+    const int b = min(r0 + t * 16 + (lane & 15), B - 1);  // padded columns recompute row B-1, never stored
 #pragma unroll
     for (int kk = 0; kk < 6; ++kk) xf[t][kk] = *reinterpret_cast<const uint4*>(X + (size_t)b * KTOT + k0 + kk * 32);
   }
@@ -1725,7 +1726,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   for (int k = 0; k < EPT; ++k) {
     const int e = tid + k * NW * 64;
     if (e >= 16 * NT * 16) break;
-    const int r = e / (NT * 16), b = e - r * (NT * 16), n = n0 + r;
+    const int r = e / (NT * 16), b = r0 + e - r * (NT * 16), n = n0 + r;
     if (b >= B || n >= a.N) continue;
     float v = 0.f;
 #pragma unroll
@@ -1771,7 +1772,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
     __syncthreads();
     if (red[0][0] == 0.f) return;
     for (int e = tid; e < 16 * NT * 16; e += NW * 64) {
-      const int r = e / (NT * 16), b = e - r * (NT * 16), n = n0 + r;
+      const int r = e / (NT * 16), b = r0 + e - r * (NT * 16), n = n0 + r;
       if (b >= B) continue;
       float t = a.st.x[(size_t)b * D + n];
 #pragma unroll
@@ -1783,7 +1784,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   }
   if constexpr (OUT == 7 || OUT == 8) {  // (mean, M2) of this block's 16 columns for every batch row
     __syncthreads();
-    if (tid < NT * 16 && tid < B) {
+    if (tid < NT * 16 && r0 + tid < B) {
       float mean = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) mean += xo[r * (NT * 16) + tid];
@@ -1794,14 +1795,23 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
         const float d = xo[r * (NT * 16) + tid] - mean;
         m2 += d * d;
       }
-      reinterpret_cast<float2*>(a.st.xstat)[(size_t)tid * (D / 16) + blockIdx.x] = make_float2(mean, m2);
+      reinterpret_cast<float2*>(a.st.xstat)[(size_t)(r0 + tid) * (D / 16) + blockIdx.x] = make_float2(mean, m2);
     }
   }
 }
 
+int g_opt_mfma_btile = 0;  // B > 16: batch tiles of 16 rows in grid.z instead of NT = 2 / 4 per block;
+                           // measured slower (B = 32 t = 256+: 144.6 vs 142.2 us/step, B = 24: 132.4
+                           // vs 129.6): twice the blocks each re-read the weights
+
 template <int K, int OUT, int XM = 0>
 static void launch_mfma2(const GemvArgs& a, hipStream_t s) {
   dim3 grid((a.N + 15) / 16), block((K / 192) * 64);
+  if (g_opt_mfma_btile && a.B > 16 && OUT != 8) {  // 16-row batch tiles: half / quarter the bytes per block
+    grid.z = (a.B + 15) / 16;
+    hipLaunchKernelGGL((ar_mfma2_kernel<K, 1, OUT, K, XM>), grid, block, 0, s, a);
+    return;
+  }
   if (a.B <= 16) hipLaunchKernelGGL((ar_mfma2_kernel<K, 1, OUT, K, XM>), grid, block, 0, s, a);
   else if (a.B <= 32) hipLaunchKernelGGL((ar_mfma2_kernel<K, 2, OUT, K, XM>), grid, block, 0, s, a);
   else hipLaunchKernelGGL((ar_mfma2_kernel<K, 4, OUT, K, XM>), grid, block, 0, s, a);
@@ -1821,6 +1831,11 @@ template <int OUT>
 static void launch_mproj_split(const GemvArgs& a, hipStream_t s) {
   static_assert(DFF == YCOPIES * 768, "one pending copy per K slice");
   dim3 grid((a.N + 15) / 16, YCOPIES), block(256);
+  if (g_opt_mfma_btile && a.B > 16 && OUT != 8) {
+    grid.z = (a.B + 15) / 16;
+    hipLaunchKernelGGL((ar_mfma2_kernel<768, 1, OUT, DFF>), grid, block, 0, s, a);
+    return;
+  }
   if (a.B <= 16) hipLaunchKernelGGL((ar_mfma2_kernel<768, 1, OUT, DFF>), grid, block, 0, s, a);
   else if (a.B <= 32) hipLaunchKernelGGL((ar_mfma2_kernel<768, 2, OUT, DFF>), grid, block, 0, s, a);
   else hipLaunchKernelGGL((ar_mfma2_kernel<768, 4, OUT, DFF>), grid, block, 0, s, a);

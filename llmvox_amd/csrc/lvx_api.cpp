@@ -546,6 +546,7 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   else if (n == "attn_blocks") g_opt_attn_blocks = value;
   else if (n == "attn_depth") g_opt_attn_depth = value;
   else if (n == "attn_waves") g_opt_attn_waves = value;
+  else if (n == "mfma_btile") g_opt_mfma_btile = value;
   else if (n == "ln_stats") g_opt_ln_stats = value;
   else if (n == "codec_bm256") g_opt_codec_bm256 = value;
   else if (n == "b1_splits") g_opt_b1_splits = value;

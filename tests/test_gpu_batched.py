@@ -135,7 +135,7 @@ def test_merge_kernel_option_agrees(eng):
 
 @pytest.mark.parametrize("opts", [{"ln_stats": 0}, {"ln_stats": 2}, {"ln_stats": 3}, {"attn_blocks": 1024},
                                   {"codec_g2": 0}, {"attn_waves": 8}, {"attn_depth": 4},
-                                  {"attn_waves": 8, "attn_blocks": 1024}])
+                                  {"attn_waves": 8, "attn_blocks": 1024}, {"mfma_btile": 1}])
 def test_alternative_batched_options_agree(eng, opts):
     """The A/B options of the batched path (kept for measurement) compute the same step: one step
     after a shared ragged prefix, against the default path, within bf16 rounding."""
@@ -153,6 +153,6 @@ def test_alternative_batched_options_agree(eng, opts):
         _, got = _run(eng, order, texts, pre, 40, 1, between=switch)
     finally:
         for k in opts:
-            eng.set_option(k, {"ln_stats": 1, "attn_blocks": 256, "codec_g2": 1, "attn_waves": 4, "attn_depth": 2}[k])
+            eng.set_option(k, {"ln_stats": 1, "attn_blocks": 256, "codec_g2": 1, "attn_waves": 4, "attn_depth": 2, "mfma_btile": 0}[k])
         eng.set_option("bt", eng.bt_mode)
     assert np.abs(got - ref).max() < 0.02 * np.abs(ref).max()
