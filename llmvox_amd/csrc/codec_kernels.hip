@@ -548,9 +548,11 @@ __global__ __launch_bounds__(256, BMt == 128 ? 2 : 1) void gemm_bf16_kernel(Gemm
           rv[r] = g.res[(size_t)row * g.ldr + col];
         }
       }
+      // outputs in place, before the row guards (the empty asm keeps them here): computed inside
+      // a guarded store, each store block re-waited for the bias / residual loads, one write
+      // acknowledgement after the previous store
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * WMt + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         const float v = acc[i][j][r] + bias;
         float o;
         if constexpr (EPI == E_BIAS) o = v;
@@ -558,7 +560,13 @@ __global__ __launch_bounds__(256, BMt == 128 ? 2 : 1) void gemm_bf16_kernel(Gemm
         else if constexpr (EPI == E_BIAS_GAMMA_RES) o = rv[r] + gam * v;
         else if constexpr (EPI == E_BIAS_RES) o = rv[r] + v;
         else o = acc[i][j][r] * g.alpha;
-        if (row < g.M) store_out<TC>(C + (size_t)row * g.ldc + col, o);
+        acc[i][j][r] = o;
+        asm volatile("" : "+v"(acc[i][j][r]));
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * WMt + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row < g.M) store_out<TC>(C + (size_t)row * g.ldc + col, acc[i][j][r]);
       }
     }
   }
