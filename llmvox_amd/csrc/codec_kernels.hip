@@ -704,13 +704,21 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const float* __restrict__
   const int gi = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   constexpr int CG = CD / GN_G;  // 24 channels
   const size_t off = (size_t)b * L * CD + gi * CG;
+  // gamma / beta of this thread's apply elements, loaded up front (in the loop they were one
+  // dependent round trip per iteration): element e = tid + 256 k has chunk (tid + 4 k) mod 6, a
+  // cycle of three chunks
+  const int q0 = tid % 6, q1 = (q0 + 4) % 6, q2 = (q0 + 2) % 6;
+  const float4* gw4 = reinterpret_cast<const float4*>(gw + gi * CG);
+  const float4* gb4 = reinterpret_cast<const float4*>(gb + gi * CG);
+  const float4 wq0 = gw4[q0], wq1 = gw4[q1], wq2 = gw4[q2], bq0 = gb4[q0], bq1 = gb4[q1], bq2 = gb4[q2];
   float mean, rstd;
   gn_group_stats(x + off, L, red, cache, mean, rstd);
   const bool lds = L <= GN_LDS_FRAMES;
-  for (int e = tid; e < L * 6; e += 256) {
-    const int t = e / 6, q = e - t * 6, ch = gi * CG + q * 4;
+  int ph = 0;
+  for (int e = tid; e < L * 6; e += 256, ph = ph == 2 ? 0 : ph + 1) {
+    const int t = e / 6, q = e - t * 6;
     const float4 v = lds ? cache[e] : gn_ld(x + off, e);
-    const float4 w = *reinterpret_cast<const float4*>(gw + ch), bb = *reinterpret_cast<const float4*>(gb + ch);
+    const float4 w = ph == 0 ? wq0 : ph == 1 ? wq1 : wq2, bb = ph == 0 ? bq0 : ph == 1 ? bq1 : bq2;
     float4 o = make_float4((v.x - mean) * rstd * w.x + bb.x, (v.y - mean) * rstd * w.y + bb.y,
                            (v.z - mean) * rstd * w.z + bb.z, (v.w - mean) * rstd * w.w + bb.w);
     if (SWISH) o = make_float4(swishf(o.x), swishf(o.y), swishf(o.z), swishf(o.w));
@@ -755,17 +763,21 @@ __global__ __launch_bounds__(256) void gn_adaln_kernel(const float* __restrict__
                                                        float* __restrict__ y) {
   __shared__ float red[4];
   const int m = blockIdx.x, tid = threadIdx.x, b = m / L;
+  float sc[3], sh[3];  // the closing affine's operands with the inputs (not behind the reductions)
+#pragma unroll
+  for (int j = 0; j < 3; ++j) { sc[j] = scale[tid + 256 * j]; sh[j] = shift[tid + 256 * j]; }
   float v[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int c = tid + 256 * j, gi = c / (CD / GN_G);
     v[j] = (x[(size_t)m * CD + c] - stats[((size_t)b * GN_G + gi) * 2]) * stats[((size_t)b * GN_G + gi) * 2 + 1] * gw[c] + gb[c];
   }
+  __builtin_amdgcn_sched_barrier(0);
   row_ln(v, 1e-6f, red);
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int c = tid + 256 * j;
-    y[(size_t)m * CD + c] = v[j] * scale[c] + shift[c];
+    y[(size_t)m * CD + c] = v[j] * sc[j] + sh[j];
   }
 }
 
@@ -781,7 +793,14 @@ __global__ __launch_bounds__(256) void dwconv_adaln_kernel(const float* __restri
   // 8,192.)
   __shared__ float red[4];
   const int m = blockIdx.x, tid = threadIdx.x, b = m / L, t = m - b * L;
-  float xv[3][7], wv[3][7], v[3];
+  float xv[3][7], wv[3][7], v[3], bb[3], sc[3], sh[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {  // bias and the AdaLN affine with the taps, not behind the reductions
+    const int c = tid + 256 * j;
+    bb[j] = dwb[c];
+    sc[j] = scale[c];
+    sh[j] = shift[c];
+  }
 #pragma unroll
   for (int k = 0; k < 7; ++k) {
     const int tt = min(max(t + k - 3, 0), L - 1);
@@ -802,13 +821,14 @@ __global__ __launch_bounds__(256) void dwconv_adaln_kernel(const float* __restri
       const float na = a + wv[j][k] * xv[j][k];
       a = (tt >= 0 && tt < L) ? na : a;
     }
-    v[j] = a + dwb[c];
+    v[j] = a + bb[j];
+    (void)c;
   }
   row_ln(v, 1e-6f, red);  // AdaLayerNorm (modules.py:81-86): no affine, eps 1e-6, then scale / shift
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int c = tid + 256 * j;
-    store_out<TO>(y + (size_t)m * CD + c, v[j] * scale[c] + shift[c]);
+    store_out<TO>(y + (size_t)m * CD + c, v[j] * sc[j] + sh[j]);
   }
 }
 
@@ -818,14 +838,19 @@ __global__ __launch_bounds__(256) void ln_affine_kernel(const float* __restrict_
                                                         const float* __restrict__ bb, TO* __restrict__ y) {
   __shared__ float red[4];
   const int m = blockIdx.x, tid = threadIdx.x;
-  float v[3];
+  float v[3], wv[3], bv[3];
 #pragma unroll
-  for (int j = 0; j < 3; ++j) v[j] = x[(size_t)m * CD + tid + 256 * j];
+  for (int j = 0; j < 3; ++j) {
+    v[j] = x[(size_t)m * CD + tid + 256 * j];
+    wv[j] = w[tid + 256 * j];
+    bv[j] = bb[tid + 256 * j];
+  }
+  __builtin_amdgcn_sched_barrier(0);  // the affine's operands with the row, not behind the reductions
   row_ln(v, 1e-6f, red);
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int c = tid + 256 * j;
-    store_out<TO>(y + (size_t)m * CD + c, v[j] * w[c] + bb[c]);
+    store_out<TO>(y + (size_t)m * CD + c, v[j] * wv[j] + bv[j]);
   }
 }
 
