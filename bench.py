@@ -93,10 +93,25 @@ KNAMES = {0: "ar_gemv c_attn", 1: "ar_attn (split-KV decode)", 2: "ar_gemv c_pro
 KCALLS = {0: 4, 1: 4, 2: 4, 3: 4, 4: 4, 5: 1}
 
 
-def probe_kernels(eng, slots, t, wbytes, kvbytes, iters=200):
+def probe_kernels(eng, slots, t, wbytes, kvbytes, iters=200, rounds=2):
     """Average launch time of each op's kernel(s) at KV position t, HIP events on the stream the
-    kernels run on. An op fused into the previous one (mlp c_proj inside the fused MLP at small B)
-    has no kernel of its own: its bytes are charged to the fused kernel."""
+    kernels run on; the lower of `rounds` passes over all ops (the first op probed after the timed
+    run was at times caught in a clock ramp, 3.3-5.1 us for the same kernel). An op fused into the
+    previous one (mlp c_proj inside the fused MLP at small B) has no kernel of its own: its bytes
+    are charged to the fused kernel."""
+    best = None
+    for _ in range(rounds):
+        r = _probe_pass(eng, slots, t, wbytes, kvbytes, iters)
+        if best is None:
+            best = r
+        else:
+            for k, v in r.items():
+                if v["avg_us"] < best[k]["avg_us"]:
+                    best[k] = v
+    return best
+
+
+def _probe_pass(eng, slots, t, wbytes, kvbytes, iters):
     from llmvox_amd._lib import LvxError
     res = {}
     s = torch.cuda.current_stream(eng.device)
