@@ -3,7 +3,7 @@
 
 Workload (BASELINE.json configs[1]): "30M LLMVoX bf16, 1xMI355X, 1 stream, 256-token chunk,
 greedy". One bench STEP = one 256-token chunk of one utterance stream: 256 greedy AR decode
-steps of the speech-token GPT (fused HIP step, replayed as a HIP graph) + the WavTokenizer
+steps of the speech-token GPT (17 fused HIP kernels per step at B = 1) + the WavTokenizer
 decode of those 256 codes into 81,920 PCM samples at 24 kHz + the PCM copy to the host.
 Steps continue the same stream (positions 0..K*256-1). Synthetic input: the config's 64-char
 sentence (66 ByT5 ids, then PAD), seeded synthetic weights at the reference init scales
@@ -93,12 +93,31 @@ KNAMES = {0: "ar_gemv c_attn", 1: "ar_attn (split-KV decode)", 2: "ar_gemv c_pro
 KCALLS = {0: 4, 1: 4, 2: 4, 3: 4, 4: 4, 5: 1}
 
 
-def probe_kernels(eng, slots, t, wbytes, kvbytes, iters=200, rounds=2):
+def pmc_traffic(prefix, kernel):
+    """HBM bytes per launch of a probed kernel from the committed PMC passes
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py), or None if not collected."""
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        return json.load(open(pmc)).get(f"{prefix}:{kernel}")
+    except (OSError, ValueError):
+        return None
+
+
+def probe_kernels(eng, slots, t, wbytes, kvbytes, iters=200, rounds=3):
     """Average launch time of each op's kernel(s) at KV position t, HIP events on the stream the
-    kernels run on; the lower of `rounds` passes over all ops (the first op probed after the timed
-    run was at times caught in a clock ramp, 3.3-5.1 us for the same kernel). An op fused into the
-    previous one (mlp c_proj inside the fused MLP at small B) has no kernel of its own: its bytes
-    are charged to the fused kernel."""
+    kernels run on. The library replays each op's `iters` launches as one HIP graph, as the
+    decode step is replayed (launched one by one from the host, 3-5 us kernels measured the
+    host's launch rate too: the same kernel read 3.3-5.8 us from box to box). One untimed pass
+    captures the graphs and warms clocks and caches; the lowest of `rounds` timed passes is kept.
+    An op fused into the previous one (mlp c_proj inside the fused MLP at small B) has no kernel
+    of its own: its bytes are charged to the fused kernel."""
+    from llmvox_amd._lib import LvxError
+    for k in KNAMES:
+        try:
+            eng.probe_kernel(k, slots, iters)
+        except LvxError as e:
+            if e.code != -2:
+                raise
     best = None
     for _ in range(rounds):
         r = _probe_pass(eng, slots, t, wbytes, kvbytes, iters)
@@ -117,8 +136,10 @@ def _probe_pass(eng, slots, t, wbytes, kvbytes, iters):
     s = torch.cuda.current_stream(eng.device)
     B = slots.numel()
     for k in KNAMES:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
         try:
-            eng.probe_kernel(k, slots, 10)
+            eng.probe_kernel(k, slots, iters)
         except LvxError as e:
             if e.code != -2:  # LVX_E_STATE: fused into the previous op at this B
                 raise
@@ -126,9 +147,6 @@ def _probe_pass(eng, slots, t, wbytes, kvbytes, iters):
             res[k - 1]["bytes"] += kernel_bytes(k, B, t, wbytes, kvbytes)
             res[k - 1]["gbs"] = res[k - 1]["bytes"] / (res[k - 1]["avg_us"] * 1e-6) / 1e9
             continue
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(s)
-        eng.probe_kernel(k, slots, iters)
         e1.record(s)
         e1.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / iters
@@ -319,6 +337,7 @@ def run_config3(args, eng, world, rank, local, dist):
         rl = {"bound": "hbm", "kernel": dom["name"], "achieved": round(dom["gbs"], 1), "peak": HBM_PEAK_GBS,
               "unit": "GB/s", "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4), "traffic": None,
               "bytes_per_launch": dom["bytes"], "avg_us": round(dom["avg_us"], 3), "kv_positions": N}
+        rl["traffic"] = pmc_traffic(f"{args.dtype}/P{N}" + (f"/B{S}" if S > 1 else ""), dom["name"])
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(0, 0, schedule=dump_schedule(N, 10))
@@ -366,8 +385,10 @@ def main():
                     help="KV position of the roofline probe (default: steps * chunk, where the run ends)")
     ap.add_argument("--codec-overlap", action="store_true",
                     help="run the codec on a second HIP stream beside the next chunk's AR (measured slower)")
+    ap.add_argument("--graph-stream", action="store_true",
+                    help="run on a non-default stream so the decode steps replay as HIP graphs")
     ap.add_argument("--no-graphs", action="store_true",
-                    help="launch the decode step kernel by kernel (for rocprofv3 --pmc passes)")
+                    help="never replay graphs (steps and kernel probes launched kernel by kernel)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the multi-rank path on one GPU (collectives on host copies)")
     ap.add_argument("--config", type=int, default=1, choices=[1, 2, 3, 4],
@@ -412,6 +433,12 @@ def main():
     torch.cuda.set_device(dev)
     if args.no_graphs:
         eng.set_graphs(False)
+    if args.graph_stream:
+        # decode steps replayed as HIP graphs need a non-default stream (the legacy null stream,
+        # torch's default, cannot be captured; the library launches its steps one by one there).
+        # Measured no faster than the default (tools/ab_graphs.sh: configs[1] 13.04-13.06k vs
+        # 12.95-13.35k tok/s, configs[2] 210.9-211.9k vs 213.4k)
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     if args.config == 3:
         return run_config3(args, eng, world, rank, local, dist)
 
@@ -546,15 +573,7 @@ def main():
         rl = {"bound": "hbm", "kernel": dom["name"], "achieved": round(dom["gbs"], 1), "peak": HBM_PEAK_GBS,
               "unit": "GB/s", "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4), "traffic": None,
               "bytes_per_launch": dom["bytes"], "avg_us": round(dom["avg_us"], 3), "kv_positions": ppos}
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
-            try:
-                tr = json.load(open(pmc))
-                key = f"{pmc_prefix}:{dom['name']}"
-                if key in tr:
-                    rl["traffic"] = tr[key]
-            except Exception:
-                pass
+        rl["traffic"] = pmc_traffic(pmc_prefix, dom["name"])
 
     # ---- codec: one batched decode of a chunk (S streams x chunk frames), HIP events on the
     # stream it runs on; algorithmic FLOPs per SURVEY 8(d): 125,566,976 + 3,072 L per frame

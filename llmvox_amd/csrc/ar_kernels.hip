@@ -2401,6 +2401,7 @@ static int ar_probe_impl(const ArWeights& w, const ArState& st, int kvdtype, int
                          hipStream_t s) {
   if (which < 0 || which > 5) return -1;
   if (which == 4 && fused_mlp<TW>(B)) return 1;  // no kernel of its own at this B
+  if (iters == 0) return 0;                       // validation only
   GemvArgs a = make_args<TW>(w, st, kvdtype, B, nullptr);
   a.dst = st.logits;
   hipLaunchKernelGGL(ar_rowinfo_init_kernel, dim3((B + 63) / 64), dim3(64), 0, s, st, B);

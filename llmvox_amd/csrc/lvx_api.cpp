@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <algorithm>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <string>
@@ -158,6 +159,7 @@ struct lvx_ctx {
   std::map<GraphKey, hipGraphExec_t> graphs;
   std::vector<hipGraph_t> graph_defs;
   bool use_graphs = true;
+  hipStream_t capture_stream = nullptr;  // graphs of null-stream callers are captured here
   std::mutex mu;
 
   template <typename T>
@@ -266,6 +268,7 @@ void lvx_destroy(lvx_ctx* c) {
   (void)hipSetDevice(c->cfg.device);
   for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
   for (auto g : c->graph_defs) (void)hipGraphDestroy(g);
+  if (c->capture_stream) (void)hipStreamDestroy(c->capture_stream);
   for (void* p : c->allocs) (void)hipFree(p);
   delete c;  // lvx_stream_create streams are not destroyed: they live until process exit
 }
@@ -604,6 +607,33 @@ int lvx_ar_forward_row(lvx_ctx* c, int slot, int pos, const float* emb_row, floa
   return LVX_OK;
 }
 
+// Capture `launch(stream)` into a graph cached under `key` (instantiated once). The legacy null
+// stream cannot be captured: its callers' graphs are captured on the context's own stream and
+// replayed on the null stream. Caller holds c->mu.
+static int cached_graph(lvx_ctx* c, const GraphKey& key, hipStream_t s,
+                        const std::function<void(hipStream_t)>& launch, hipGraphExec_t* out) {
+  auto it = c->graphs.find(key);
+  if (it == c->graphs.end()) {
+    hipStream_t cs = s;
+    if (!cs) {
+      if (!c->capture_stream) HIP_TRY(hipStreamCreateWithFlags(&c->capture_stream, hipStreamNonBlocking));
+      cs = c->capture_stream;
+    }
+    hipGraph_t g;
+    HIP_TRY(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+    launch(cs);
+    hipError_t le = hipGetLastError();
+    HIP_TRY(hipStreamEndCapture(cs, &g));
+    if (le != hipSuccess) return fail(LVX_E_HIP, std::string("capture: ") + hipGetErrorString(le));
+    hipGraphExec_t ex;
+    HIP_TRY(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    c->graph_defs.push_back(g);
+    it = c->graphs.emplace(key, ex).first;
+  }
+  *out = it->second;
+  return 0;
+}
+
 static int ar_step_impl(lvx_ctx* c, int n_steps, int B, const int32_t* slots, const int32_t* text_plan,
                         int plan_stride, int32_t* rowstep, int32_t* tok_plan, float* margin_plan, void* stream) {
   NEED_FINAL(c);
@@ -622,6 +652,8 @@ static int ar_step_impl(lvx_ctx* c, int n_steps, int B, const int32_t* slots, co
   st.margin_plan = margin_plan;
   hipStream_t s = (hipStream_t)stream;
   ar_launch_rowinfo_init(st, B, s);  // per-row control records, then advanced by every step
+  // null-stream callers (torch's default stream) launch the steps one by one: replaying the same
+  // steps as graphs on a stream of their own measured no faster (tools/ab_graphs.sh)
   if (!c->use_graphs || s == nullptr) {
     for (int i = 0; i < n_steps; ++i)
       ar_launch_step(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, 0, nullptr, 0, 0, nullptr, s);
@@ -633,22 +665,10 @@ static int ar_step_impl(lvx_ctx* c, int n_steps, int B, const int32_t* slots, co
   // graphs of kGraphSteps consecutive steps (one replay per kGraphSteps tokens) + 1-step graph
   auto get_graph = [&](int nst, hipGraphExec_t* out) -> int {
     GraphKey key{B, plan_stride, nst, slots, text_plan, rowstep, tok_plan, margin_plan, stream};
-    auto it = c->graphs.find(key);
-    if (it == c->graphs.end()) {
-      hipGraph_t g;
-      HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    return cached_graph(c, key, s, [&](hipStream_t cs) {
       for (int i = 0; i < nst; ++i)
-        ar_launch_step(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, 0, nullptr, 0, 0, nullptr, s);
-      hipError_t le = hipGetLastError();
-      HIP_TRY(hipStreamEndCapture(s, &g));
-      if (le != hipSuccess) return fail(LVX_E_HIP, std::string("capture: ") + hipGetErrorString(le));
-      hipGraphExec_t ex;
-      HIP_TRY(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-      c->graph_defs.push_back(g);
-      it = c->graphs.emplace(key, ex).first;
-    }
-    *out = it->second;
-    return 0;
+        ar_launch_step(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, 0, nullptr, 0, 0, nullptr, cs);
+    }, out);
   };
   int left = n_steps;
   if (left >= kGraphSteps) {
@@ -704,9 +724,27 @@ int lvx_probe_kernel(lvx_ctx* c, int which, int B, const int32_t* slots, int ite
   HIP_TRY(hipSetDevice(c->cfg.device));
   ArState st = c->st;  // no plan bound: text_plan / rowstep / tok_plan stay null
   st.slots = const_cast<int32_t*>(slots);
-  const int pr = ar_probe(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, which, iters, (hipStream_t)stream);
+  hipStream_t s = (hipStream_t)stream;
+  // a dry run (no launches) validates the op id / fused case before anything is captured
+  const int pr = ar_probe(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, which, 0, s);
   if (pr < 0) return fail(LVX_E_ARG, "unknown probe kernel id");
   if (pr > 0) return fail(LVX_E_STATE, "this op has no kernel of its own at this batch size (fused into the previous op)");
+  if (!c->use_graphs) {
+    ar_probe(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, which, iters, s);
+    HIP_TRY(hipGetLastError());
+    return LVX_OK;
+  }
+  // the `iters` launches are replayed as one graph, as the decode step is: launched one by one
+  // from the host, back-to-back kernels of 3-5 us measured the host's launch rate as much as
+  // the kernel (the first call of a (op, B, slots, iters) captures; time the second)
+  std::lock_guard<std::mutex> lk(c->mu);
+  GraphKey key{B, -1 - which, iters, slots, nullptr, nullptr, nullptr, nullptr, stream};
+  hipGraphExec_t gx;
+  if (int r = cached_graph(c, key, s, [&](hipStream_t cs) {
+        ar_probe(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, which, iters, cs);
+      }, &gx))
+    return r;
+  HIP_TRY(hipGraphLaunch(gx, s));
   HIP_TRY(hipGetLastError());
   return LVX_OK;
 }

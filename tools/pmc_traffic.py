@@ -2,10 +2,10 @@
 
 usage: python tools/pmc_traffic.py FETCH_CSV WRITE_CSV DTYPE [OUT_JSON]
 
-bench.py's roofline probe (``probe_kernels``) runs, for each op k = 0..5, one
-``ar_rowinfo_init_kernel`` + 10 warm launches, then one ``ar_rowinfo_init_kernel`` + 200 timed
-launches; the rowinfo-init dispatches delimit the segments and the timed ones are the last
-segments of 200 launches.  Bytes per launch = counter sum over the segment / 200.
+bench.py's roofline probe (``probe_kernels``) runs passes over the ops k = 0..5 (one untimed
+capture pass, then the timed ones), each op one ``ar_rowinfo_init_kernel`` + 200 launches (a
+replayed graph); the rowinfo-init dispatches delimit the segments and the last pass's segments
+are used.  Bytes per launch = counter sum over the segment / 200.
 
 Corrections (MI355X_MICROARCH.md, "HBM"): FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
 FETCH_SIZE counts half the bytes of a 16-B/lane coalesced read, so it is doubled; WRITE_SIZE
