@@ -35,14 +35,24 @@ def _run(e, B, slots, calls, graphs):
     tok = torch.full((B, n), -7, dtype=torch.int32, device=dev)
     margin = torch.zeros(B, n, dtype=torch.float32, device=dev)
     e.set_graphs(graphs)
+    # graphs are captured only on a non-default stream (the library launches the steps one by
+    # one on the legacy null stream): the graph case runs on a stream of its own
+    main = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(device=dev) if graphs else None
+    if side is not None:
+        side.wait_stream(main)
     try:
-        for c in calls:
-            e.ar_steps(c, st, plan, rowstep, tok, margin)
+        with torch.cuda.stream(side):
+            for c in calls:
+                e.ar_steps(c, st, plan, rowstep, tok, margin)
+            e.check_errors()
+            pos = [e.slot_position(s) for s in slots if s >= 0]
+            logits = e.last_logits(B)
     finally:
         e.set_graphs(True)
-    e.check_errors()
-    pos = [e.slot_position(s) for s in slots if s >= 0]
-    return tok.cpu().numpy(), margin.cpu().numpy(), rowstep.cpu().numpy(), pos, e.last_logits(B).cpu().numpy()
+    if side is not None:
+        main.wait_stream(side)
+    return tok.cpu().numpy(), margin.cpu().numpy(), rowstep.cpu().numpy(), pos, logits.cpu().numpy()
 
 
 @pytest.mark.parametrize("fuse_mlp", [0, 1], ids=["exact", "fused-mlp"])
@@ -135,3 +145,43 @@ def test_batched_deferred_select_matches_argmax_kernel(eng_batched, B, mode):
     n = sum(calls)
     assert got[2][B // 2] == 0 and (got[0][B // 2] == -7).all()
     assert all(got[2][b] == n for b in range(B) if b != B // 2)
+
+
+@pytest.mark.parametrize("B,slots", [(1, [2]), (2, [0, 3]), (2, [1, -1])], ids=["B1", "B2", "B2-idle"])
+def test_graph_replay_matches_eager(eng, B, slots):
+    """16-step + 1-step graph replays on a side stream == the same steps launched one by one
+    (deterministic path: fused MLP off)."""
+    calls = [3, 17, 1, 16]
+    eng.set_option("fuse_mlp", 0)
+    try:
+        eager = _run(eng, B, slots, calls, False)
+        graph = _run(eng, B, slots, calls, True)
+    finally:
+        eng.set_option("fuse_mlp", 1)
+    for a, b, name in zip(graph, eager, ["tokens", "margins", "rowstep", "positions", "logits"]):
+        np.testing.assert_array_equal(np.asarray(a), np.asarray(b), err_msg=name)
+
+
+@pytest.mark.parametrize("B", [1, 4])
+def test_kernel_probe_graphs(eng, B):
+    """bench.py's roofline probe: every op's launches replay as one graph (captured on the
+    context's own stream for a null-stream caller); the fused mlp c_proj reports LVX_E_STATE;
+    the decode state stays valid."""
+    from llmvox_amd._lib import LvxError
+    dev = eng.device
+    slots = torch.arange(B, dtype=torch.int32, device=dev)
+    for s in range(B):
+        eng.set_slot(s, 100, 7)
+    ran = 0
+    for _ in range(2):  # capture, then replay the cached graph
+        for k in range(6):
+            try:
+                eng.probe_kernel(k, slots, 20)
+                ran += 1
+            except LvxError as e:
+                assert e.code == -2 and k == 4, (k, e.code)
+    torch.cuda.synchronize()
+    eng.check_errors()
+    assert ran >= 10
+    with pytest.raises(LvxError):
+        eng.probe_kernel(6, slots, 20)
