@@ -270,6 +270,12 @@ __device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, f
         } else {
           const int p = ri.y, prev = ri.w;
           int tok = ri.z;
+          // the wpe row goes out with the text / codebook rows (clamped row, unconditional:
+          // issued behind the normalisation it was a round trip of its own)
+          const float* wr = a.wpe + (size_t)min(max(p, 0), BLOCK_SIZE - 1) * D;
+          float4 pe[3];
+#pragma unroll
+          for (int j = 0; j < 3; ++j) pe[j] = *reinterpret_cast<const float4*>(wr + j * 256 + lane * 4);
           if (tok < 0) {
             if (lane == 0 && blockIdx.x == 0) atomicOr(a.st.err, 2);
             tok = 384;
@@ -285,13 +291,10 @@ __device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, f
           }
           ss = wave_sum(ss);
           const float den = fmaxf(sqrtf(ss), 1e-8f);  // F.normalize: x / max(||x||_2, eps)
-          const float* wr = a.wpe + (size_t)p * D;
 #pragma unroll
-          for (int j = 0; j < 3; ++j) {
-            const int k = j * 256 + lane * 4;
-            const float4 pe = *reinterpret_cast<const float4*>(wr + k);
-            v[j] = make_float4(v[j].x / den + pe.x, v[j].y / den + pe.y, v[j].z / den + pe.z, v[j].w / den + pe.w);
-          }
+          for (int j = 0; j < 3; ++j)
+            v[j] = make_float4(v[j].x / den + pe[j].x, v[j].y / den + pe[j].y, v[j].z / den + pe[j].z,
+                               v[j].w / den + pe[j].w);
         }
         if (blockIdx.x == 0)
 #pragma unroll
