@@ -29,7 +29,7 @@ namespace lvx {
 //   IN  0: in = LayerNorm(x[b]) * ln_w            (eps 1e-5, no bias; src/model.py:37-38)
 //   IN  1: in = h[b] (fp32, K = 3072)
 //   IN  2: in = merge of the split-KV attention partials (flash-decoding combine)
-//   IN  4: in = LayerNorm(x[b] + sum_c yacc[c][b]) (the fused MLP's pending output)
+//   IN  4: in = LayerNorm(x[b] + sum_c yacc[b][c]) (the fused MLP's pending output)
 //   IN  3: layer-0 c_attn: builds x[b] first (a2-a4: text row, codebook row of the previous
 //          token or 0 at position 0, L2-normalise eps 1e-8, + wpe[pos]; or, for the drop-in
 //          row forward, the caller's row + wpe[pos]), block 0 stores it, then LayerNorm.
@@ -199,7 +199,7 @@ __device__ __forceinline__ void wave_ln_to_lds(float4 (&v)[3], const float4 (&ga
   }
 }
 
-// x[b] (IN 0) or x[b] + sum_c yacc[c][b] (IN 4) in the lane layout k = j * 256 + lane * 4: the
+// x[b] (IN 0) or x[b] + sum_c yacc[b][c] (IN 4) in the lane layout k = j * 256 + lane * 4: the
 // loads are issued by xrow_issue and summed by xrow_sum, so a prefetch does not wait on them
 template <int IN>
 struct XRow {
@@ -216,7 +216,7 @@ __device__ __forceinline__ void xrow_issue(const GemvArgs& a, int b, int lane, X
     for (int c = 0; c < YCOPIES; ++c)
 #pragma unroll
       for (int j = 0; j < 3; ++j)
-        r.y[c][j] = *reinterpret_cast<const float4*>(a.yacc + ((size_t)c * a.st.max_streams + b) * D + j * 256 + lane * 4);
+        r.y[c][j] = *reinterpret_cast<const float4*>(a.yacc + ((size_t)b * YCOPIES + c) * D + j * 256 + lane * 4);
   }
 }
 template <int IN>
@@ -383,7 +383,7 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
       xep = a.st.x[(size_t)b * D + n];
       if (IN == 2 && a.yacc)
 #pragma unroll
-        for (int c = 0; c < YCOPIES; ++c) yep[c] = a.yacc[((size_t)c * a.st.max_streams + b) * D + n];
+        for (int c = 0; c < YCOPIES; ++c) yep[c] = a.yacc[((size_t)b * YCOPIES + c) * D + n];
     }
   }
   if ((IN == 0 || IN == 3 || IN == 4) && prefetched) {
@@ -530,7 +530,7 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
           if (IN == 2 && a.yacc) {  // c_proj: fold the fused MLP's accumulators into x and clear them
 #pragma unroll
             for (int c = 0; c < YCOPIES; ++c) {
-              float* yp = a.yacc + ((size_t)c * a.st.max_streams + b) * D + n;
+              float* yp = a.yacc + ((size_t)b * YCOPIES + c) * D + n;
               if (a.add_y) t += g0 == 0 ? yep[c] : *yp;
               *yp = 0.f;
             }
@@ -644,12 +644,12 @@ __device__ __forceinline__ void gemv_store(const GemvArgs& a, int n, int b, floa
     float t = *xp;
     if (a.yacc && a.add_y)  // c_proj: fold the pending split-K partials of the previous mlp c_proj
 #pragma unroll
-      for (int c = 0; c < YCOPIES; ++c) t += a.yacc[((size_t)c * a.st.max_streams + b) * D + n];
+      for (int c = 0; c < YCOPIES; ++c) t += a.yacc[((size_t)b * YCOPIES + c) * D + n];
     *xp = t + v;
   } else if (OUT == 2) {
     a.st.h[(size_t)b * DFF + n] = gelu_tanh(v);
   } else if (OUT == 6) {  // split-K partial of mlp c_proj (K slice blockIdx.y) -> pending copy
-    a.yacc[((size_t)blockIdx.y * a.st.max_streams + b) * D + n] = v;
+    a.yacc[((size_t)b * YCOPIES + blockIdx.y) * D + n] = v;
   } else {
     a.dst[(size_t)b * a.N + n] = v;
   }
@@ -848,7 +848,7 @@ __global__ __launch_bounds__(256) void ar_cproj_b1_kernel(GemvArgs a) {
     xep = a.st.x[row0 + lane];
     if (a.yacc)
 #pragma unroll
-      for (int c = 0; c < YCOPIES; ++c) yep[c] = a.yacc[(size_t)c * a.st.max_streams * D + row0 + lane];
+      for (int c = 0; c < YCOPIES; ++c) yep[c] = a.yacc[(size_t)c * D + row0 + lane];
   }
   const TW* __restrict__ W = reinterpret_cast<const TW*>(a.W);
   typename WReg<TW>::T wr[RPW][3];
@@ -900,7 +900,7 @@ __global__ __launch_bounds__(256) void ar_cproj_b1_kernel(GemvArgs a) {
 #pragma unroll
         for (int c = 0; c < YCOPIES; ++c) {
           if (a.add_y) t += yep[c];
-          a.yacc[(size_t)c * a.st.max_streams * D + row0 + r] = 0.f;
+          a.yacc[(size_t)c * D + row0 + r] = 0.f;
         }
       }
       a.st.x[row0 + r] = t + v;
@@ -976,7 +976,7 @@ __global__ __launch_bounds__(256) void ar_mlp_fused_kernel(GemvArgs a, const bf1
     }
   __syncthreads();
   // thread tid: outputs e = tid + 256 jj; pack g element jj * 16 + j = W[e][n0 + 16 g + j]
-  float* y = a.yacc + (size_t)(blockIdx.x % YCOPIES) * a.st.max_streams * D;
+  float* y = a.yacc + (size_t)(blockIdx.x % YCOPIES) * D;  // row bb's copies: y + bb * YCOPIES * D
 #pragma unroll
   for (int bb = 0; bb < BG; ++bb) {
 #pragma unroll
@@ -990,7 +990,7 @@ __global__ __launch_bounds__(256) void ar_mlp_fused_kernel(GemvArgs a, const bf1
         t = fmaf(__uint_as_float(u.y << 16), hs[bb][4 * g + 2], t);
         t = fmaf(__uint_as_float(u.y & 0xffff0000u), hs[bb][4 * g + 3], t);
       }
-      atomicAdd(y + (size_t)bb * D + tid + 256 * jj, t);
+      atomicAdd(y + (size_t)bb * YCOPIES * D + tid + 256 * jj, t);
     }
   }
 }
@@ -1748,7 +1748,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
       a.st.xb[(size_t)b * D + n] = f32_to_bf16(xn);
       xo[e] = xn;
     } else if (OUT == 8) {  // K-slice slab of the split mlp c_proj (reduced by the tile's last arriver)
-      a.yacc[((size_t)blockIdx.y * a.st.max_streams + b) * D + n] = v;
+      a.yacc[((size_t)b * YCOPIES + blockIdx.y) * D + n] = v;
     } else {
       gemv_store<OUT>(a, n, b, v);
     }
@@ -1779,7 +1779,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
       if (b >= B) continue;
       float t = a.st.x[(size_t)b * D + n];
 #pragma unroll
-      for (int c = 0; c < YCOPIES; ++c) t += a.yacc[((size_t)c * a.st.max_streams + b) * D + n];
+      for (int c = 0; c < YCOPIES; ++c) t += a.yacc[((size_t)b * YCOPIES + c) * D + n];
       a.st.x[(size_t)b * D + n] = t;
       a.st.xb[(size_t)b * D + n] = f32_to_bf16(t);
       xo[e] = t;
@@ -1879,7 +1879,7 @@ __global__ __launch_bounds__(256) void ar_mfma_ln_kernel(GemvArgs a) {
       for (int c = 0; c < YCOPIES; ++c)
 #pragma unroll
         for (int j = 0; j < 3; ++j)
-          ya[i < YR ? i : 0][c][j] = *reinterpret_cast<const float4*>(a.yacc + ((size_t)c * a.st.max_streams + b) * D + j * 256 + lane * 4);
+          ya[i < YR ? i : 0][c][j] = *reinterpret_cast<const float4*>(a.yacc + ((size_t)b * YCOPIES + c) * D + j * 256 + lane * 4);
   }
   const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(a.W);
   const int wrow = min(n0 + (lane & 15), a.N - 1);
@@ -1908,7 +1908,7 @@ __global__ __launch_bounds__(256) void ar_mfma_ln_kernel(GemvArgs a) {
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
             const float4 y = i < YR ? ya[i < YR ? i : 0][c][j]
-                                    : *reinterpret_cast<const float4*>(a.yacc + ((size_t)c * a.st.max_streams + b) * D + j * 256 + lane * 4);
+                                    : *reinterpret_cast<const float4*>(a.yacc + ((size_t)b * YCOPIES + c) * D + j * 256 + lane * 4);
             xv[i][j].x += y.x; xv[i][j].y += y.y; xv[i][j].z += y.z; xv[i][j].w += y.w;
           }
       }

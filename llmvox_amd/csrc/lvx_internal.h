@@ -67,7 +67,9 @@ struct ArState {
   float* logits = nullptr;      // [B][4096]
   uint64_t* lmbest = nullptr;   // [LM_MAX_BLOCKS][4][2] per-block top1/top2 granules (fused lm_head + argmax)
   uint32_t* ticket = nullptr;   // [4] arrival counter of the fused lm_head (reset by its last block)
-  float* yacc = nullptr;        // [YCOPIES][max_streams][768] fused-MLP output accumulators (fp32 atomics)
+  float* yacc = nullptr;        // [max_streams][YCOPIES][768] fused-MLP output accumulators (fp32 atomics);
+                                // a row's copies adjacent: spaced by max_streams rows they shared
+                                // L2 channels (B = 1: 82.6 vs 69.6 us/step at max_streams 32)
   void* kc = nullptr;           // [4][max_streams][8][max_pos][96]
   void* vc = nullptr;
   int max_pos = 0, max_streams = 0;
