@@ -1,20 +1,26 @@
 #!/usr/bin/env python3
 """LLMVoX streaming-TTS hot path on MI355X — the driver's benchmark.
 
-Workload (BASELINE.json configs[1]): "30M LLMVoX bf16, 1xMI355X, 1 stream, 256-token chunk,
-greedy". One bench STEP = one 256-token chunk of one utterance stream: 256 greedy AR decode
-steps of the speech-token GPT (17 fused HIP kernels per step at B = 1) + the WavTokenizer
-decode of those 256 codes into 81,920 PCM samples at 24 kHz + the PCM copy to the host.
-Steps continue the same stream (positions 0..K*256-1). Synthetic input: the config's 64-char
-sentence (66 ByT5 ids, then PAD), seeded synthetic weights at the reference init scales
-(no checkpoints offline).
+Default workload (BASELINE.json configs[2], the largest single-GPU configuration): "30M LLMVoX
+bf16, 1xMI355X, 32 concurrent streams batched decode + vocoder". One bench STEP = one 256-token
+chunk of 32 utterance streams: 256 batched greedy AR decode steps of the speech-token GPT (B = 32
+rows per step) + the WavTokenizer decode of the 32 x 256 codes (one batched codec call, 2,621,440
+PCM samples at 24 kHz) + the PCM copy to the host. Steps continue the same streams (positions
+0..K*256-1). Synthetic input: stream 0 speaks the config's 64-char sentence, the others seeded
+random 64-char sentences (ByT5 ids, then PAD); seeded synthetic weights at the reference init
+scales (no checkpoints offline). p50 first-chunk latency is measured separately on one stream of
+the same engine through the service scheduler (FusedScheduler), from the first text word enqueued
+to the first 3,200-sample (10-token) dump as bytes on the host.
 
-Multi-GPU (--gpus N under torch.distributed.run): one process per GPU, each running its own
-stream(s) (independent utterance streams: weak scaling); rank 0 scatters the text-id plans
-and gathers the PCM over RCCL (the path's only exchange, BASELINE north_star).
+Multi-GPU: ``--gpus N`` runs one process per GPU. Under torch.distributed.run (WORLD_SIZE set, it
+must equal N) each rank is one such process; without it bench.py spawns the N ranks itself (before
+any GPU call) on 127.0.0.1. Each rank runs its own streams (independent utterance streams: weak
+scaling); rank 0 scatters the text-id plans and gathers the PCM over RCCL (the path's only
+exchange, BASELINE north_star).
 
 --config selects the other BASELINE.json workloads (per GPU; weak scaling over --gpus):
-  2  32 streams batched, 256-token chunks (configs[2])
+  1  1 stream, 256-token chunks (configs[1])
+  2  32 streams batched, 256-token chunks (configs[2], default)
   3  the service path: FusedScheduler replica streams (replica index = stream % 2, initial dump
      10 / 160, x3 growth to 1280) over one utterance of --utt-tokens 2048 per step; every dump is
      decoded as its own codec call and delivered as f32le bytes on the host (configs[3])
@@ -93,14 +99,56 @@ KNAMES = {0: "ar_gemv c_attn", 1: "ar_attn (split-KV decode)", 2: "ar_gemv c_pro
 KCALLS = {0: 4, 1: 4, 2: 4, 3: 4, 4: 4, 5: 1}
 
 
-def pmc_traffic(prefix, kernel):
-    """HBM bytes per launch of a probed kernel from the committed PMC passes
-    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py), or None if not collected."""
+def pmc_key(dtype, kv_dtype, B, pos):
+    """Key of a probe workload in profiles/pmc_traffic.json (tools/pmc_traffic.py KEY argument):
+    weight dtype, KV dtype, batch rows and the KV position the probe ran at."""
+    return f"{dtype}/kv{kv_dtype}/B{B}/P{pos}"
+
+
+def pmc_traffic(key, kernel):
+    """HBM bytes per launch of a probed kernel from the committed PMC passes over the SAME probe
+    workload (profiles/pmc_traffic.json, written by tools/pmc_traffic.py), or None when no pass
+    was collected at this key: traffic is never paired with a different position or batch."""
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
-        return json.load(open(pmc)).get(f"{prefix}:{kernel}")
+        return json.load(open(pmc)).get(f"{key}:{kernel}")
     except (OSError, ValueError):
         return None
+
+
+def pmc_codec(key):
+    """MFMA busy cycles / GRBM active cycles of the codec's large GEMM (gemm_bf16_kernel) from a
+    committed rocprofv3 pass over the same codec call (profiles/pmc_codec.json, tools/pmc_codec.py)."""
+    pmc = os.path.join(ROOT, "profiles", "pmc_codec.json")
+    try:
+        return json.load(open(pmc)).get(key)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_threads():
+    """Threads for the CPU baseline: this process's physical cores — the CPUs it may run on
+    (sched_getaffinity), one per physical core (SMT siblings dropped), capped by the cgroup CPU
+    quota (a GPU box grants each GPU's jobs a share of the host, e.g. 16 CPUs)."""
+    cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    cores = set()
+    for c in cpus:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                cores.add(f.read().strip().split(",")[0].split("-")[0])
+        except OSError:
+            cores.add(str(c))
+    n, why = len(cores), f"{len(cores)} physical cores of {len(cpus)} CPUs in the affinity mask"
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+            if quota < n:
+                n, why = quota, why + f", cgroup CPU quota {quota}"
+    except (OSError, ValueError):
+        pass
+    return n, why
 
 
 def probe_kernels(eng, slots, t, wbytes, kvbytes, iters=200, rounds=3):
@@ -174,7 +222,7 @@ def cpu_baseline(n_chunks, chunk, min_seconds=10.0, max_seconds=30.0, schedule=N
     at least ``min_seconds`` of CPU work is timed (bounded by ``max_seconds``)."""
     from llmvox_amd import weights as LW
     from oracle import reference_cpu as R
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads, why = cpu_threads()
     torch.set_num_threads(threads)
     gw, cw, tt = LW.synthetic_all(1234)
     W, Wc = R.to_torch(gw), R.to_torch(cw)
@@ -220,7 +268,7 @@ def cpu_baseline(n_chunks, chunk, min_seconds=10.0, max_seconds=30.0, schedule=N
     return {"value": done / dt, "unit": "speech tokens/s", "cores": threads, "kind": "port",
             "sample": f"{done} tokens: fp32 AR steps + one codec decode per dump of {schedule[:8]} tokens, "
                       f"over {passes} utterance(s) of {sum(schedule)} positions, 1 stream, oracle/reference_cpu.py, "
-                      f"{dt:.1f} s on {cpu}"}
+                      f"{dt:.1f} s on {cpu}, torch threads {threads} ({why})"}
 
 
 class _HostCollectives:
@@ -270,13 +318,13 @@ def run_config3(args, eng, world, rank, local, dist):
 
     def utterance():
         streams = []
+        t0 = time.perf_counter()  # first text word enqueued (p50 first-chunk latency starts here)
         for s in range(S):
             g = rank * S + s
             st = sched.open_stream(index=g % 2, dump_size=10 if g % 2 == 0 else 160)
             for w in (SENTENCE if g == 0 else random_sentence(rng)).split(" "):
                 st.feed(w)
             streams.append(st)
-        t0 = time.perf_counter()
         first = None
         while min(len(st.tokens) for st in streams) < N:
             if sched.run_chunk() == 0:
@@ -337,7 +385,8 @@ def run_config3(args, eng, world, rank, local, dist):
         rl = {"bound": "hbm", "kernel": dom["name"], "achieved": round(dom["gbs"], 1), "peak": HBM_PEAK_GBS,
               "unit": "GB/s", "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4), "traffic": None,
               "bytes_per_launch": dom["bytes"], "avg_us": round(dom["avg_us"], 3), "kv_positions": N}
-        rl["traffic"] = pmc_traffic(f"{args.dtype}/P{N}" + (f"/B{S}" if S > 1 else ""), dom["name"])
+        rl["pmc_key"] = pmc_key(args.dtype, args.kv_dtype or args.dtype, S, N)
+        rl["traffic"] = pmc_traffic(rl["pmc_key"], dom["name"])
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(0, 0, schedule=dump_schedule(N, 10))
@@ -357,6 +406,8 @@ def run_config3(args, eng, world, rank, local, dist):
             "audio_samples_per_s": round(320 * value, 1),
             "realtime_factor_per_stream": round(value / (world * S) / 75.0, 1),
             "p50_first_chunk_latency_ms": round(statistics.median(firsts), 3),
+            "dist": ({"backend": dist.get_backend(), "world_size": dist.get_world_size()} if dist is not None
+                     else {"backend": None, "world_size": 1}),
             "roofline": rl, "kv_dtype": args.kv_dtype or args.dtype,
             "codec_weights": args.codec_dtype or args.dtype, "cpu_baseline": cpu,
             "kernels": {v["name"]: {"avg_us": round(v["avg_us"], 2), "GB/s": round(v["gbs"], 1)}
@@ -369,109 +420,113 @@ def run_config3(args, eng, world, rank, local, dist):
 
 
 # ---------------------------------------------------------------------------------------
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=4)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--streams", type=int, default=1, help="streams per GPU (configs[2]: 32)")
-    ap.add_argument("--chunk", type=int, default=256)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--kv-dtype", default=None, choices=["bf16", "fp32", "fp8"],
-                    help="KV cache dtype (default: --dtype); fp8 = OCP e4m3fn (configs[4])")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-probe", action="store_true")
-    ap.add_argument("--probe-pos", type=int, default=0,
-                    help="KV position of the roofline probe (default: steps * chunk, where the run ends)")
-    ap.add_argument("--codec-overlap", action="store_true",
-                    help="run the codec on a second HIP stream beside the next chunk's AR (measured slower)")
-    ap.add_argument("--graph-stream", action="store_true",
-                    help="run on a non-default stream so the decode steps replay as HIP graphs")
-    ap.add_argument("--no-graphs", action="store_true",
-                    help="never replay graphs (steps and kernel probes launched kernel by kernel)")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="gloo: rehearse the multi-rank path on one GPU (collectives on host copies)")
-    ap.add_argument("--config", type=int, default=1, choices=[1, 2, 3, 4],
-                    help="BASELINE.json workload (1: default; 2: 32 streams; 3: scheduler replicas; 4: fp8)")
-    ap.add_argument("--codec-dtype", default=None, choices=["fp8"], help="fp8 codec weights (configs[4])")
-    ap.add_argument("--utt-tokens", type=int, default=2048, help="configs[3]: tokens per utterance (one step)")
-    ap.add_argument("--reset-every", type=int, default=4,
-                    help="configs[4]: chunks per sentence (KV reset at every sentence start)")
-    args = ap.parse_args()
-    if args.config == 2 and args.streams == 1:
-        args.streams = 32
-    if args.config == 4:
-        if args.streams == 1:
-            args.streams = 8
-        args.kv_dtype = args.kv_dtype or "fp8"
-        args.codec_dtype = args.codec_dtype or "fp8"
+def spawn_ranks(n):
+    """--gpus N without torch.distributed.run: one child process per GPU (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR 127.0.0.1 / a free MASTER_PORT), started before this process has
+    touched the GPU. Returns the first failing rank's exit code (the others are then terminated),
+    else 0."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            c = p.poll()
+            if c is None:
+                continue
+            procs.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                for q in procs:
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return rc
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        if args.dist_backend == "gloo":  # rehearsal: every rank may share one GPU
-            local = local % max(1, torch.cuda.device_count())
-            torch.cuda.set_device(local)
-            dist.init_process_group("gloo")
-            dist = _HostCollectives(dist)
-        else:
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
 
-    from llmvox_amd.engine import build_engine
-    S, chunk, K, Wm = args.streams, args.chunk, args.steps, args.warmup
-    if (K + 0) * chunk > 8192:
-        raise SystemExit("steps * chunk must stay within block_size 8192 positions")
-    kvd = args.kv_dtype or args.dtype
-    eng = build_engine(local, args.dtype, kvd, max_streams=max(S, 1), max_positions=8192,
-                       max_codec_frames=max(S * chunk, 1280 * S if args.config == 3 else 0),
-                       codec_dtype=args.codec_dtype)
-    dev = eng.device
-    torch.cuda.set_device(dev)
-    if args.no_graphs:
-        eng.set_graphs(False)
-    if args.graph_stream:
-        # decode steps replayed as HIP graphs need a non-default stream (the legacy null stream,
-        # torch's default, cannot be captured; the library launches its steps one by one there).
-        # Measured no faster than the default (tools/ab_graphs.sh: configs[1] 13.04-13.06k vs
-        # 12.95-13.35k tok/s, configs[2] 210.9-211.9k vs 213.4k)
-        torch.cuda.set_stream(torch.cuda.Stream(device=dev))
-    if args.config == 3:
-        return run_config3(args, eng, world, rank, local, dist)
-
-    # ---- text plans: stream 0 of rank 0 speaks the config sentence; others seeded sentences
-    n_pos = max(K, Wm) * chunk
-    plans = np.zeros((world * S, n_pos), dtype=np.int32)
-    rng = np.random.default_rng(1234)
-    for g in range(world * S):
-        ids = sentence_ids(SENTENCE if g == 0 else random_sentence(rng))
-        plans[g] = plan_for(ids, 0, n_pos)
+def rehearse(args, world, rank):
+    """--rehearse: the multi-rank skeleton of the bench on the CPU (gloo, no GPU): plan scatter from
+    rank 0, a stand-in per-rank 'decode', PCM gather to rank 0, barriers and the max-over-ranks
+    clock. Used by tests/test_bench_launcher.py for the launcher path."""
+    import torch.distributed as dist
     from llmvox_amd.parallel import gather_pcm, scatter_plans
-    # rank 0 scatters the text-id shards over RCCL (the path's inbound exchange)
-    mine = scatter_plans(torch.from_numpy(plans), S, n_pos, dev, dist, rank)
+    dist.init_process_group("gloo")
+    S, n_pos = args.streams, args.chunk
+    plans = None
+    if rank == 0:
+        rng = np.random.default_rng(1234)
+        plans = torch.from_numpy(np.stack([plan_for(sentence_ids(SENTENCE if g == 0 else random_sentence(rng)), 0, n_pos)
+                                           for g in range(world * S)]))
+    dist.barrier()
+    t0 = time.perf_counter()
+    mine = scatter_plans(plans, S, n_pos, "cpu", dist, rank)
+    got = gather_pcm(mine.float(), dist, rank, world)
+    dist.barrier()
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        ok = torch.equal(torch.cat(got).to(torch.int32), plans)
+        print(json.dumps({"rehearsal": True, "dist": {"backend": dist.get_backend(), "world_size": dist.get_world_size()},
+                          "n_gpus": world, "streams_per_rank": S, "gathered_equals_scattered": bool(ok),
+                          "max_over_ranks_s": float(dt.item())}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
 
+
+def first_chunk_latency(eng, reps=12):
+    """p50 first-chunk latency: one fresh stream through the service scheduler
+    (FusedScheduler: tokenisation, text-id plan upload, 10 fused decode steps, the codec call, PCM
+    to the host as f32le bytes), timed from the moment the sentence's words are enqueued to the
+    first 3,200-sample dump on the host; first two runs (graph capture, warm-up) dropped."""
+    from llmvox_amd.streaming import FusedScheduler
+    sched = FusedScheduler(eng, max_chunk=256, max_rows=1)
+    lat = []
+    for r in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st = sched.open_stream(index=0, dump_size=10)
+        for w in SENTENCE.split(" "):
+            st.feed(w)
+        while not any(isinstance(e, bytes) for e in st.events):
+            if sched.run_chunk() == 0:
+                raise RuntimeError("scheduler idle before the first dump")
+        t1 = time.perf_counter()
+        assert len(st.events[0]) == 3200 * 4
+        sched.close_stream(st)
+        if r >= 2:
+            lat.append((t1 - t0) * 1e3)
+    return statistics.median(lat)
+
+
+def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, world=1, codec_overlap=False):
+    """W untimed then K timed bench steps (one step = `chunk` fused decode steps for the S streams,
+    the batched codec decode of their codes, the PCM to the host; the PCM gathered to rank 0 when
+    distributed). Returns (seconds, last token buffer, codec stream, token buffers, PCM buffers)."""
+    from llmvox_amd.parallel import gather_pcm
+    dev = eng.device
     slots = torch.arange(S, dtype=torch.int32, device=dev)
     text_plan = torch.empty(S, chunk, dtype=torch.int32, device=dev)
     rowstep = torch.zeros(S, dtype=torch.int32, device=dev)
     tok_plan = torch.zeros(S, chunk, dtype=torch.int32, device=dev)
     pcm = torch.empty(S, 320 * chunk, dtype=torch.float32, device=dev)
     pcm_host = torch.empty(S, 320 * chunk, dtype=torch.float32, pin_memory=True)
-
     # the codec of chunk c runs after the AR of chunk c on the same stream. A second stream
     # (--codec-overlap) was measured slower: the latency-bound AR chain stalls while the codec's
     # kernels are in flight (22.4 ms AR + 1.2 ms codec = 23.6 ms serial vs 25.5 ms overlapped per
-    # 256-token chunk; CU-partitioned or prioritised streams 28 ms, tools/loop_probe.py).
+    # 256-token chunk; CU-partitioned or prioritised streams 28 ms, round 1).
     # tok_plan / pcm are double-buffered so the overlapped variant stays correct.
-    codec_stream = torch.cuda.Stream(device=dev) if args.codec_overlap else torch.cuda.current_stream(dev)
+    codec_stream = torch.cuda.Stream(device=dev) if codec_overlap else torch.cuda.current_stream(dev)
     tok_bufs = [tok_plan, torch.zeros_like(tok_plan)]
     pcm_bufs = [pcm, torch.empty_like(pcm)]
     ev_ar = [torch.cuda.Event(), torch.cuda.Event()]
     ev_codec = [torch.cuda.Event(), torch.cuda.Event()]
-
-    reset_every = args.reset_every if args.config == 4 else 0
 
     def run_chunk(c):
         i = c & 1
@@ -499,7 +554,7 @@ def main():
         for s in range(S):
             eng.reset_slot(s)
 
-    # ---- setup: capture the decode graphs for both token buffers (untimed), warmup, reset
+    # setup: capture the decode graphs for both token buffers (untimed), warmup, reset
     reset_all()
     for i in range(2):
         rowstep.zero_()
@@ -515,7 +570,7 @@ def main():
     reset_all()
     torch.cuda.synchronize()
 
-    # ---- timed region: K chunks
+    # timed region: K chunks, barrier + synchronize on both sides
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -527,53 +582,161 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     eng.check_errors()
+    return dt, tok_bufs[(K - 1) & 1], codec_stream, tok_bufs, pcm_bufs
+
+
+def parity_mode_line(S, chunk, K=2, Wm=1):
+    """The fp32 parity mode (weights, KV and codec in fp32: bit-exact ids against the reference,
+    tests/test_gpu_parity.py) on the same workload, K steps after Wm warm-up steps."""
+    from llmvox_amd.engine import build_engine
+    eng = build_engine(torch.cuda.current_device(), "fp32", "fp32", max_streams=S, max_positions=max(K, Wm) * chunk,
+                       max_codec_frames=S * chunk)
+    try:
+        n_pos = max(K, Wm) * chunk
+        rng = np.random.default_rng(1234)
+        plans = np.stack([plan_for(sentence_ids(SENTENCE if g == 0 else random_sentence(rng)), 0, n_pos)
+                          for g in range(S)])
+        mine = torch.from_numpy(plans).to(eng.device)
+        dt, _, _, _, _ = run_chunks(eng, mine, S, chunk, K, Wm)
+        return {"value": round(S * K * chunk / dt, 1), "unit": "speech tokens/s", "ms_per_step": round(dt / K * 1e3, 3),
+                "steps": K, "warmup": Wm, "dtype": "fp32", "kv_dtype": "fp32", "codec_weights": "fp32"}
+    finally:
+        eng.close()
+
+
+def main():
+    import faulthandler
+    faulthandler.enable()
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--streams", type=int, default=0, help="streams per GPU (default: the config's: 1 / 32 / 1 / 8)")
+    ap.add_argument("--chunk", type=int, default=256)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--kv-dtype", default=None, choices=["bf16", "fp32", "fp8"],
+                    help="KV cache dtype (default: --dtype); fp8 = OCP e4m3fn (configs[4])")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--no-parity-line", action="store_true", help="skip the fp32 parity-mode line")
+    ap.add_argument("--probe-pos", type=int, default=0,
+                    help="KV position of the roofline probe (default: the run's mean position, steps * chunk / 2)")
+    ap.add_argument("--codec-overlap", action="store_true",
+                    help="run the codec on a second HIP stream beside the next chunk's AR (measured slower)")
+    ap.add_argument("--graph-stream", action="store_true",
+                    help="run on a non-default stream so the decode steps replay as HIP graphs")
+    ap.add_argument("--no-graphs", action="store_true",
+                    help="never replay graphs (steps and kernel probes launched kernel by kernel)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse the multi-rank path on one GPU (collectives on host copies)")
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4],
+                    help="BASELINE.json workload (2: default, 32 streams; 1: one stream; 3: scheduler replicas; 4: fp8)")
+    ap.add_argument("--codec-dtype", default=None, choices=["fp8"], help="fp8 codec weights (configs[4])")
+    ap.add_argument("--utt-tokens", type=int, default=2048, help="configs[3]: tokens per utterance (one step)")
+    ap.add_argument("--reset-every", type=int, default=4,
+                    help="configs[4]: chunks per sentence (KV reset at every sentence start)")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="CPU-only rehearsal of the multi-rank skeleton (gloo; tests/test_bench_launcher.py)")
+    args = ap.parse_args()
+    if args.streams == 0:
+        args.streams = {1: 1, 2: 32, 3: 1, 4: 8}[args.config]
+    if args.config == 4:
+        args.kv_dtype = args.kv_dtype or "fp8"
+        args.codec_dtype = args.codec_dtype or "fp8"
+
+    # one process per GPU: under torch.distributed.run WORLD_SIZE is set (and must equal --gpus);
+    # without it, --gpus N > 1 spawns the N ranks here, before anything touches the GPU
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    world = int(world_env or 1)
+    if world != args.gpus:
+        sys.stderr.write(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a "
+                         "different GPU count than requested\n")
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.rehearse:
+        return rehearse(args, world, rank)
+    dist, dist_info = None, None
+    if world > 1:
+        import torch.distributed as tdist
+        if args.dist_backend == "gloo":  # rehearsal: every rank may share one GPU
+            local = local % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(local)
+            tdist.init_process_group("gloo")
+            dist = _HostCollectives(tdist)
+        else:
+            torch.cuda.set_device(local)
+            tdist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+            dist = tdist
+        dist_info = {"backend": tdist.get_backend(), "world_size": tdist.get_world_size()}
+
+    from llmvox_amd.engine import build_engine
+    S, chunk, K, Wm = args.streams, args.chunk, args.steps, args.warmup
+    if max(K, Wm) * chunk > 8192:
+        raise SystemExit("steps * chunk must stay within block_size 8192 positions")
+    kvd = args.kv_dtype or args.dtype
+    eng = build_engine(local, args.dtype, kvd, max_streams=max(S, 1), max_positions=8192,
+                       max_codec_frames=max(S * chunk, 1280 * S if args.config == 3 else 0),
+                       codec_dtype=args.codec_dtype)
+    dev = eng.device
+    torch.cuda.set_device(dev)
+    if args.no_graphs:
+        eng.set_graphs(False)
+    if args.graph_stream:
+        # decode steps replayed as HIP graphs need a non-default stream (the legacy null stream,
+        # torch's default, cannot be captured; the library launches its steps one by one there).
+        # Measured no faster than the default in round 1 (configs[1] 13.04-13.06k vs 12.95-13.35k
+        # tok/s, configs[2] 210.9-211.9k vs 213.4k)
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev))
+    if args.config == 3:
+        return run_config3(args, eng, world, rank, local, dist)
+
+    # ---- text plans: stream 0 of rank 0 speaks the config sentence; others seeded sentences
+    n_pos = max(K, Wm) * chunk
+    plans = np.zeros((world * S, n_pos), dtype=np.int32)
+    rng = np.random.default_rng(1234)
+    for g in range(world * S):
+        ids = sentence_ids(SENTENCE if g == 0 else random_sentence(rng))
+        plans[g] = plan_for(ids, 0, n_pos)
+    from llmvox_amd.parallel import scatter_plans
+    # rank 0 scatters the text-id shards over RCCL (the path's inbound exchange)
+    mine = scatter_plans(torch.from_numpy(plans), S, n_pos, dev, dist, rank)
+
+    reset_every = args.reset_every if args.config == 4 else 0
+    dt, last_tok, codec_stream, tok_bufs, pcm_bufs = run_chunks(
+        eng, mine, S, chunk, K, Wm, reset_every, dist, rank, world, args.codec_overlap)
     if dist is not None:
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-
     total_tokens = world * S * K * chunk
     value = total_tokens / dt
-    toks_rank0 = tok_bufs[(K - 1) & 1][0].cpu().numpy()
+    toks_rank0 = last_tok[0].cpu().numpy()
 
-    # ---- p50 first-chunk latency: fresh segment -> first 10-token dump (3,200 samples) on host
-    lat = []
-    first = torch.empty(1, 320 * 10, dtype=torch.float32, pin_memory=True)
-    one_slot = slots[:1]
-    tp1 = torch.empty(1, 10, dtype=torch.int32, device=dev)
-    rs1 = torch.zeros(1, dtype=torch.int32, device=dev)
-    tk1 = torch.zeros(1, 10, dtype=torch.int32, device=dev)
-    for r in range(12):
-        torch.cuda.synchronize()
-        ta = time.perf_counter()
-        eng.reset_slot(0)
-        tp1.copy_(mine[:1, :10])
-        rs1.zero_()
-        eng.ar_steps(10, one_slot, tp1, rs1, tk1)
-        p = eng.decode_codes(tk1, 0)
-        first.copy_(p)
-        torch.cuda.synchronize()
-        if r >= 2:
-            lat.append((time.perf_counter() - ta) * 1e3)
-    p50 = statistics.median(lat)
+    p50 = first_chunk_latency(eng)
 
-    # ---- roofline: dominant kernel class, timed live with HIP events on the compute stream
+    # ---- roofline: dominant kernel class at the run's mean KV position, timed live with HIP
+    # events on the compute stream; traffic from a PMC pass over the same probe workload
     rl, kern = None, None
+    slots = torch.arange(S, dtype=torch.int32, device=dev)
     if not args.no_probe:
-        reset_all()
-        ppos = args.probe_pos or (min(K, reset_every) if reset_every else K) * chunk
+        for s in range(S):
+            eng.reset_slot(s)
+        span = (min(K, reset_every) if reset_every else K) * chunk
+        ppos = args.probe_pos or max(1, span // 2)
         for s in range(S):
             eng.set_slot(s, ppos - 1, 0)
         wb = 2 if args.dtype == "bf16" else 4
         kb = {"bf16": 2, "fp8": 1, "fp32": 4}[kvd]
         kern = probe_kernels(eng, slots, ppos, wb, kb)
-        # profiles/pmc_traffic.json key prefix (tools/pmc_traffic.py DTYPE argument)
-        pmc_prefix = args.dtype + (f"/kv{kvd}" if kvd != args.dtype else "") + (f"/B{S}" if S > 1 else "")
         dom = max(kern.values(), key=lambda r: r["share_us_per_step"])
+        key = pmc_key(args.dtype, kvd, S, ppos)
         rl = {"bound": "hbm", "kernel": dom["name"], "achieved": round(dom["gbs"], 1), "peak": HBM_PEAK_GBS,
-              "unit": "GB/s", "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4), "traffic": None,
-              "bytes_per_launch": dom["bytes"], "avg_us": round(dom["avg_us"], 3), "kv_positions": ppos}
-        rl["traffic"] = pmc_traffic(pmc_prefix, dom["name"])
+              "unit": "GB/s", "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(key, dom["name"]),
+              "bytes_per_launch": dom["bytes"], "avg_us": round(dom["avg_us"], 3), "kv_positions": ppos,
+              "pmc_key": key}
 
     # ---- codec: one batched decode of a chunk (S streams x chunk frames), HIP events on the
     # stream it runs on; algorithmic FLOPs per SURVEY 8(d): 125,566,976 + 3,072 L per frame
@@ -589,9 +752,15 @@ def main():
     codec_ms = c0.elapsed_time(c1) / 5
     codec_flops = S * chunk * (125_566_976 + 3_072 * chunk)
     codec_peak = 2500.0 if args.dtype == "bf16" else 157.3  # dense bf16 MFMA / exact-f32 MFMA, TFLOP/s
+    ckey = f"{args.codec_dtype or args.dtype}/F{S * chunk}/L{chunk}"
     codec = {"frames": S * chunk, "avg_ms": round(codec_ms, 3),
              "achieved": round(codec_flops / (codec_ms * 1e-3) / 1e12, 2), "peak": codec_peak, "unit": "TFLOP/s",
-             "frac": round(codec_flops / (codec_ms * 1e-3) / 1e12 / codec_peak, 4)}
+             "frac": round(codec_flops / (codec_ms * 1e-3) / 1e12 / codec_peak, 4),
+             "gemm_mfma_busy": pmc_codec(ckey), "pmc_key": ckey}
+
+    parity = None
+    if rank == 0 and not args.no_parity_line and args.dtype == "bf16" and args.config in (1, 2):
+        parity = parity_mode_line(S, chunk)
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
@@ -610,12 +779,14 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": args.dtype,
-            "data": "synthetic (config 64-char sentence -> ByT5 ids, seeded synthetic weights at reference init scales)",
-            "config": {"workload": f"configs[{args.config if args.config != 1 or S == 1 else 2}]: 30M LLMVoX {args.dtype}, "
+            "data": "synthetic (config 64-char sentence + seeded random 64-char sentences -> ByT5 ids, "
+                    "seeded synthetic weights at reference init scales)",
+            "config": {"workload": f"configs[{args.config}]: 30M LLMVoX {args.dtype}, "
                                    f"{S} stream(s)/GPU, {chunk}-token chunk, greedy AR + WavTokenizer decode + PCM to host"
                                    + (f", fp8 KV + fp8 codec weights, KV reset every {reset_every} chunks" if reset_every else ""),
                        "streams_per_gpu": S, "chunk_tokens": chunk, "positions": K * chunk,
                        "parallelism": f"streams sharded over {world} GPU(s), RCCL scatter text / gather PCM"},
+            "dist": dist_info or {"backend": None, "world_size": 1},
             "audio_samples_per_s": round(320 * value, 1),
             "realtime_factor_per_stream": round(value / (world * S) / 75.0, 1),
             "p50_first_chunk_latency_ms": round(p50, 3),
@@ -623,6 +794,7 @@ def main():
             "codec_roofline": codec,
             "kv_dtype": kvd,
             "codec_weights": args.codec_dtype or args.dtype,
+            "parity_mode_fp32": parity,
             "cpu_baseline": cpu,
             "kernels": {v["name"]: {"avg_us": round(v["avg_us"], 2), "GB/s": round(v["gbs"], 1)}
                         for v in kern.values()} if kern else None,

@@ -123,6 +123,15 @@ int lvx_stream_set(lvx_ctx* ctx, int slot, int pos, int prev_token, void* stream
  * Writes only scratch and the K/V row at the current position (which the next real step
  * overwrites). LVX_E_STATE when the op has no kernel of its own at this B (fused). */
 int lvx_probe_kernel(lvx_ctx* ctx, int which, int B, const int32_t* slots_dev, int iters, void* stream);
+/* Test hook: the greedy select (argmax(softmax(logits)) with the reference's tie semantics,
+ * streaming_server.py:342-346) of one production kernel path over caller-given logits float32
+ * [B][4096], committed exactly as a decode step commits it (tok_plan[b][rowstep[b]], margin,
+ * slot prev / position, rowstep advance). path 0: ar_argmax_kernel; 1: the lm_head-granule
+ * reduction of the B <= 2 deferred select (B <= 4 here); 2: the batched deferred select
+ * (ar_embed_select_kernel). plan_stride >= 2. */
+int lvx_select_probe(lvx_ctx* ctx, int path, int B, const int32_t* slots_dev, const float* logits_dev,
+                     const int32_t* text_plan_dev, int plan_stride, int32_t* rowstep_dev, int32_t* tok_plan_dev,
+                     float* margin_plan_dev, void* stream);
 /* Host-side view of a slot's position (synchronises the stream). */
 int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
 /* Kernel-variant switches for in-process A/B timing (defaults and measurements: DESIGN.md §4 and

@@ -101,6 +101,36 @@ __device__ __forceinline__ Best best_wave(Best r) {
   return best_merge(best_merge(best_lane(r, 0), best_lane(r, 16)), best_merge(best_lane(r, 32), best_lane(r, 48)));
 }
 
+// The reference selects argmax(softmax(logits)) on the CPU in fp32 (streaming_server.py:343-346).
+// ATen's last-dim softmax is exp(x - max) * (1 / sum): two probabilities are equal exactly when
+// exp(x - max) rounds to 1.0f, i.e. x - max >= -2^-25 (exact subtraction this close to the max;
+// exp behaves correctly rounded there: pinned against torch in tests/test_select_rule.py), and
+// argmax then takes the first of them. best_merge's (top1, first index, top2) decides alone when
+// top1 - top2 > 2^-25; otherwise the wave rescans the row for the first index within 2^-25 of the
+// maximum (never taken on real logits short of an exact tie). r must be wave-uniform; returns
+// the reference's index in r.i (r.v / r.v2 unchanged: the margin stays top1 - top2).
+constexpr float SOFTMAX_TIE = 2.98023223876953125e-08f;  // 2^-25
+__device__ __noinline__ int softmax_tie_scan(const float* __restrict__ row, float m, int lane) {
+  int first = 0x7fffffff;
+  const float4* p = reinterpret_cast<const float4*>(row);
+  for (int k = 0; k < VOCAB / 256; ++k) {
+    const float4 v = p[k * 64 + lane];
+    const int i0 = (k * 64 + lane) * 4;
+    if (v.w - m >= -SOFTMAX_TIE) first = i0 + 3;
+    if (v.z - m >= -SOFTMAX_TIE) first = i0 + 2;
+    if (v.y - m >= -SOFTMAX_TIE) first = i0 + 1;
+    if (v.x - m >= -SOFTMAX_TIE) first = i0;
+    if (first != 0x7fffffff) break;  // this lane's later chunks hold only larger indices
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) first = min(first, __shfl_xor(first, o));
+  return first;
+}
+__device__ __forceinline__ Best softmax_ties(const float* __restrict__ row, Best r, int lane) {
+  if (!(r.v - r.v2 > SOFTMAX_TIE)) r.i = softmax_tie_scan(row, r.v, lane);
+  return r;
+}
+
 // text id of row b at plan step j (-1: past the end of the plan; PAD when no plan is bound)
 __device__ __forceinline__ int plan_tok(const ArState& st, int b, int j) {
   if (!st.text_plan) return 384;
@@ -428,7 +458,7 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
     // the shadow records, attention layer 0 copies them back) and build this step's record. The
     // reduction and the record select run unconditionally so that the granule loads stay in the
     // prologue (used only under a branch, the compiler sinks them into it: one more round trip).
-    const Best r = lmg_reduce(lmg);
+    const Best r = softmax_ties(a.st.logits + (size_t)min(wave, a.B - 1) * VOCAB, lmg_reduce(lmg), lane);
     const int s = ripre.x, j = rxp.x, p = ripre.y + 1;
     const bool take = selpend && s >= 0;
     const int4 rn = take ? make_int4(s, min(p, a.st.max_pos - 1), rxp.y, min(max(r.i, 0), VOCAB - 1)) : ripre;
@@ -1361,10 +1391,11 @@ __global__ __launch_bounds__(256) void ar_argmax_kernel(ArState st) {
   bt = best_wave(bt);
   if (lane == 0) { sv[wave] = bt.v; sv2[wave] = bt.v2; si[wave] = bt.i; }
   __syncthreads();
-  if (tid == 0) {
+  if (wave == 0) {
     Best r{sv[0], sv2[0], si[0]};
     for (int w = 1; w < 4; ++w) r = best_merge(r, Best{sv[w], sv2[w], si[w]});
-    argmax_commit(st, b, ri, r);
+    r = softmax_ties(st.logits + (size_t)b * VOCAB, r, lane);
+    if (lane == 0) argmax_commit(st, b, ri, r);
   }
 }
 
@@ -1529,6 +1560,7 @@ __global__ __launch_bounds__(256) void ar_embed_select_kernel(GemvArgs a) {
     Best r{sv[0], sv2[0], si[0]};
 #pragma unroll
     for (int w = 1; w < 4; ++w) r = best_merge(r, Best{sv[w], sv2[w], si[w]});
+    r = softmax_ties(a.st.logits + (size_t)b * VOCAB, r, lane);
     const int s = ri.x, p = ri.y + 1, j = rx.x;
     const int4 rn = make_int4(s, min(p, a.st.max_pos - 1), rx.y, min(max(r.i, 0), VOCAB - 1));
     if (lane == 0) {  // argmax_commit
@@ -2437,7 +2469,7 @@ __global__ __launch_bounds__(64) void ar_select_final_kernel(ArState st) {
   const int2 rx = st.rowx[b];
   LmGran q;
   lmg_issue(st, b, lane, q);
-  const Best r = lmg_reduce(q);
+  const Best r = softmax_ties(st.logits + (size_t)b * VOCAB, lmg_reduce(q), lane);
   if (lane == 0) {
     if (b == 0) *st.selp = 0u;
     if (ri.x >= 0) {
@@ -2445,6 +2477,44 @@ __global__ __launch_bounds__(64) void ar_select_final_kernel(ArState st) {
       argmax_commit(st, b, ri, r);
     }
   }
+}
+
+// Test hook (lvx_select_probe): the greedy select of each production path over given logits
+// (st.logits). path 0: ar_argmax_kernel; 1: per-block lm_head granules formed as OUT 9 forms them
+// (8 consecutive vocabulary rows per block), reduced by ar_select_final_kernel (lmg_reduce +
+// softmax_ties, the same code as the deferred select in c_attn layer 0, IN 5); 2: the batched
+// deferred select, ar_embed_select_kernel.
+__global__ void ar_select_probe_prep_kernel(ArState st, int B, int path) {
+  const int blk = blockIdx.x, b = threadIdx.x;
+  if (b >= B) return;
+  if (path == 1) {
+    Best r{-INFINITY, -INFINITY, 0x7fffffff};
+    for (int n = blk * 8; n < blk * 8 + 8; ++n) r = best_merge(r, Best{st.logits[(size_t)b * VOCAB + n], -INFINITY, n});
+    u64x2_t g;
+    g.x = ((unsigned long long)(unsigned)r.i << 32) | __float_as_uint(r.v);
+    g.y = (unsigned long long)__float_as_uint(r.v2);
+    reinterpret_cast<u64x2_t*>(st.lmbest)[(size_t)blk * 4 + b] = g;
+  }
+  if (blk == 0) {
+    st.selrow[b] = 1u;
+    if (b == 0) *st.selp = 1u;
+  }
+}
+
+int ar_select_probe(const ArWeights& w, const ArState& st, int B, int path, hipStream_t s) {
+  if (path < 0 || path > 2 || B < 1 || (path == 1 && B > 4)) return -1;
+  hipLaunchKernelGGL(ar_rowinfo_init_kernel, dim3((B + 63) / 64), dim3(64), 0, s, st, B);
+  hipLaunchKernelGGL(ar_select_probe_prep_kernel, dim3(LM_SEL_BLOCKS), dim3(64), 0, s, st, B, path);
+  if (path == 0) {
+    hipLaunchKernelGGL(ar_argmax_kernel, dim3(B), dim3(256), 0, s, st);
+  } else if (path == 1) {
+    hipLaunchKernelGGL(ar_select_final_kernel, dim3(B), dim3(64), 0, s, st);
+  } else {
+    GemvArgs a = make_args<float>(w, st, LVX_DTYPE_F32, B, nullptr);
+    a.ln_w = w.ln1[0];
+    hipLaunchKernelGGL(ar_embed_select_kernel, dim3(B), dim3(256), 0, s, a);
+  }
+  return 0;
 }
 
 void ar_launch_steps_end(const ArState& st, int wdtype, int B, hipStream_t s) {

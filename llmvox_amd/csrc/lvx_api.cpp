@@ -749,6 +749,29 @@ int lvx_probe_kernel(lvx_ctx* c, int which, int B, const int32_t* slots, int ite
   return LVX_OK;
 }
 
+int lvx_select_probe(lvx_ctx* c, int path, int B, const int32_t* slots, const float* logits,
+                     const int32_t* text_plan, int plan_stride, int32_t* rowstep, int32_t* tok_plan,
+                     float* margin_plan, void* stream) {
+  NEED_FINAL(c);
+  if (B < 1 || B > c->cfg.max_streams || (path == 1 && B > 4)) return fail(LVX_E_ARG, "B out of range for this path");
+  if (path < 0 || path > 2) return fail(LVX_E_ARG, "path must be 0, 1 or 2");
+  if (!slots || !logits || !text_plan || !rowstep || !tok_plan || plan_stride < 2)
+    return fail(LVX_E_ARG, "null argument or plan_stride < 2");
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  hipStream_t s = (hipStream_t)stream;
+  ArState st = c->st;
+  st.slots = const_cast<int32_t*>(slots);
+  st.text_plan = text_plan;
+  st.plan_stride = plan_stride;
+  st.rowstep = rowstep;
+  st.tok_plan = tok_plan;
+  st.margin_plan = margin_plan;
+  HIP_TRY(hipMemcpyAsync(st.logits, logits, (size_t)B * VOCAB * 4, hipMemcpyDeviceToDevice, s));
+  ar_select_probe(c->arw, st, B, path, s);
+  HIP_TRY(hipGetLastError());
+  return LVX_OK;
+}
+
 static int codec_check(lvx_ctx* c, int B, int L, int bw) {
   if (B < 1 || L < 1) return fail(LVX_E_ARG, "B and L must be >= 1");
   if ((long long)B * L > c->cfg.max_codec_frames)

@@ -105,6 +105,15 @@ class Engine:
     def probe_kernel(self, which: int, slots: torch.Tensor, iters: int):
         _lib.check(self.lib.lvx_probe_kernel(self.h, which, slots.numel(), _ptr(slots), iters, self.stream_handle()))
 
+    def select_probe(self, path: int, slots: torch.Tensor, logits: torch.Tensor, text_plan: torch.Tensor,
+                     rowstep: torch.Tensor, tok_plan: torch.Tensor, margin_plan: Optional[torch.Tensor] = None):
+        """Test hook: one production select path (0 argmax kernel, 1 deferred lm_head granules,
+        2 batched deferred select) over the given logits [B, 4096], committed as a step commits."""
+        B, stride = text_plan.shape
+        logits = logits.to(self.device, torch.float32).contiguous()
+        _lib.check(self.lib.lvx_select_probe(self.h, path, B, _ptr(slots), _ptr(logits), _ptr(text_plan), stride,
+                                             _ptr(rowstep), _ptr(tok_plan), _ptr(margin_plan), self.stream_handle()))
+
     def last_logits(self, B: int) -> torch.Tensor:
         out = torch.empty(B, 4096, device=self.device, dtype=torch.float32)
         _lib.check(self.lib.lvx_ar_logits(self.h, B, _ptr(out), self.stream_handle()))

@@ -87,6 +87,14 @@ def load_reference(ref_root):
     return gpt, wt, embed
 
 
+def _pcm_summary(name, p):
+    """RMS (float64), 512-sample head and tail, every 64th sample of a PCM vector."""
+    p = np.asarray(p, dtype=np.float32)
+    return {f"{name}_rms": np.float64(np.sqrt(np.mean(p.astype(np.float64) ** 2))),
+            f"{name}_head": p[:512].copy(), f"{name}_tail": p[-512:].copy(), f"{name}_s64": p[::64].copy(),
+            f"{name}_len": np.int32(p.size)}
+
+
 class RefHandler:
     """The ModelHandler members audio_generator_sync touches, backed by the
     reference modules (inference/model_handler.py:45-63)."""
@@ -103,9 +111,10 @@ class _Stop(Exception):
     pass
 
 
-def run_reference_scheduler(handler, words, index, dump_size, max_model_calls, timeout=600):
+def run_reference_scheduler(handler, words, index, dump_size, max_model_calls, timeout=600, record=None):
     """Drive the reference's own audio_generator_sync in a thread and return the
-    list of items it put on the audio queue."""
+    list of items it put on the audio queue. ``record`` (a list) receives, per model call, the
+    (id, top1-top2 margin) the reference's select (softmax -> argmax) makes of its logits."""
     import streaming_server as S
     text_q, audio_q = queue.Queue(), queue.Queue()
     for w in words:
@@ -117,7 +126,12 @@ def run_reference_scheduler(handler, words, index, dump_size, max_model_calls, t
         if calls["n"] >= max_model_calls:
             raise _Stop()
         calls["n"] += 1
-        return real_model(*a, **k)
+        out = real_model(*a, **k)
+        if record is not None:
+            lg = out[0][0, -1]
+            t2 = torch.topk(lg, 2).values
+            record.append((int(torch.softmax(lg, -1).argmax().item()), float(t2[0] - t2[1])))
+        return out
 
     handler.model = counted
     done = threading.Event()
@@ -269,6 +283,17 @@ def main(ref_root="/root/reference"):
                 codec["backbone_10"] = bb.numpy().astype(np.float32)
                 codec["features_10"] = feats.numpy().astype(np.float32)
     np.savez_compressed(os.path.join(HERE, "codec_golden.npz"), **codec)
+    # the reference's large dumps (streaming_server.py:373-375: 10/160 -> x3 -> 1280):
+    # RMS, 512-sample head and tail, and every 64th sample of the PCM
+    big = {}
+    with torch.inference_mode(), _quiet():
+        for L in (270, 480, 810, 1280):
+            codes = torch.from_numpy(rng.integers(0, 4096, size=(1, L)).astype(np.int64))
+            pcm = wt.decode(wt.codes_to_features(codes), bandwidth_id=torch.tensor([0])).numpy()[0]
+            big[f"codes_{L}"] = codes.numpy().astype(np.int32)
+            big.update(_pcm_summary(f"pcm_{L}", pcm))
+    np.savez_compressed(os.path.join(HERE, "codec_large_golden.npz"), **big)
+    print("codec large: rms", {L: float(big[f"pcm_{L}_rms"]) for L in (270, 480, 810, 1280)})
     print("codec: pcm_10 rms", float(np.sqrt(np.mean(codec["pcm_10"] ** 2))))
 
     # --- end to end: the reference's own audio_generator_sync on the sentence
@@ -281,6 +306,33 @@ def main(ref_root="/root/reference"):
     np.savez_compressed(os.path.join(HERE, "stream_golden.npz"), sizes=np.array(sizes, np.int32),
                         chunk0=chunks[0], chunk1=chunks[1], chunk2=chunks[2],
                         model_calls=np.int32(n))
+
+    # --- the same stream run until replica 0's dumps reach max_dump_size:
+    # 10 + 30 + 90 + 270 + 810 + 1280 = 2490 model calls (configs[3]'s dump sizes)
+    rec = []
+    h = RefHandler(gpt, wt, embed, tok)
+    with _quiet():
+        items, finished, n = run_reference_scheduler(h, words, 0, 10, 2490, timeout=3600, record=rec)
+    chunks = [np.frombuffer(it, dtype=np.float32) for it in items if isinstance(it, (bytes, bytearray))]
+    long = {"sizes": np.array([len(c) for c in chunks], np.int32), "model_calls": np.int32(n),
+            "ids": np.array([r[0] for r in rec], np.int32), "margins": np.array([r[1] for r in rec], np.float32),
+            "text_ids": np.array(text_ids, np.int32)}
+    for i, c in enumerate(chunks):
+        long.update(_pcm_summary(f"chunk{i}", c))
+    # replica 1 (index 1, initial dump 160: 160 + 480 + 1280 = 1920 model calls) on the same text
+    rec1 = []
+    h = RefHandler(gpt, wt, embed, tok)
+    with _quiet():
+        items, finished, n1 = run_reference_scheduler(h, words, 1, 160, 1920, timeout=3600, record=rec1)
+    chunks = [np.frombuffer(it, dtype=np.float32) for it in items if isinstance(it, (bytes, bytearray))]
+    assert [r[0] for r in rec1] == long["ids"][:len(rec1)].tolist()  # the dump policy never feeds back
+    long["r1_sizes"] = np.array([len(c) for c in chunks], np.int32)
+    long["r1_model_calls"] = np.int32(n1)
+    for i, c in enumerate(chunks):
+        long.update(_pcm_summary(f"r1_chunk{i}", c))
+    np.savez_compressed(os.path.join(HERE, "stream_long_golden.npz"), **long)
+    print("long stream chunks", long["sizes"].tolist(), "calls", n, "min margin", float(long["margins"].min()),
+          "replica 1 chunks", long["r1_sizes"].tolist())
 
     # --- scheduler control traces with scripted tokens
     tr = scheduler_traces(tok)

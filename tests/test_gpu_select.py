@@ -185,3 +185,39 @@ def test_kernel_probe_graphs(eng, B):
     assert ran >= 10
     with pytest.raises(LvxError):
         eng.probe_kernel(6, slots, 20)
+
+
+@pytest.mark.parametrize("path,B", [(0, 1), (0, 8), (1, 1), (1, 2), (1, 4), (2, 4), (2, 16)],
+                         ids=["argmax-B1", "argmax-B8", "granules-B1", "granules-B2", "granules-B4",
+                              "batched-B4", "batched-B16"])
+def test_select_paths_reproduce_softmax_argmax(eng_batched, path, B):
+    """Every production select path over constructed near-tie logits (rivals 0..6 ulps and up to
+    3 x 2^-25 below the maximum, before and after it) picks what the reference's
+    softmax -> argmax picks on the same fp32 logits (oracle greedy_token = torch CPU), and the
+    margin is top1 - top2. Rows are committed as a decode step commits them."""
+    from oracle import reference_cpu as R
+    from tests.select_cases import near_tie_rows
+    e = eng_batched
+    dev = e.device
+    picked, want = [], []
+    for rep in range(12):
+        rows = near_tie_rows(B, seed=1000 * path + 10 * B + rep)
+        for s in range(B):
+            e.set_slot(s, 5, 0)
+        slots = torch.arange(B, dtype=torch.int32, device=dev)
+        plan = torch.full((B, 4), 97, dtype=torch.int32, device=dev)
+        rowstep = torch.ones(B, dtype=torch.int32, device=dev)
+        tok = torch.full((B, 4), -7, dtype=torch.int32, device=dev)
+        marg = torch.zeros(B, 4, dtype=torch.float32, device=dev)
+        e.select_probe(path, slots, torch.from_numpy(rows), plan, rowstep, tok, marg)
+        torch.cuda.synchronize()
+        t, m, rs = tok.cpu().numpy(), marg.cpu().numpy(), rowstep.cpu().numpy()
+        for b in range(B):
+            ref = R.greedy_token(torch.from_numpy(rows[b]).view(1, 1, -1))
+            top2 = np.sort(rows[b])[-2:]
+            picked.append(int(t[b, 1]))
+            want.append(ref)
+            assert m[b, 1] == np.float32(top2[1] - top2[0])
+            assert rs[b] == 2 and t[b, 0] == -7 and t[b, 2] == -7
+        assert [e.slot_position(s) for s in range(B)] == [6] * B
+    assert picked == want

@@ -69,3 +69,27 @@ def test_istft_envelope_and_length(W):
     spec = torch.randn(1, 641, 7, dtype=torch.complex64)
     y = R.istft_same(spec)
     assert y.shape == (1, 7 * 320)
+
+
+@pytest.mark.parametrize("L", [270, 1280])
+def test_codec_large_dumps_bitexact(W, L):
+    """configs[3]'s dump sizes (streaming_server.py:373-375): the oracle against the reference's PCM
+    summaries (tests/golden/codec_large_golden.npz)."""
+    g = np.load(os.path.join(GOLDEN, "codec_large_golden.npz"))
+    _, Wc, _ = W
+    pcm = R.decode_codes(Wc, torch.from_numpy(g[f"codes_{L}"]).long()).numpy()[0]
+    assert pcm.size == int(g[f"pcm_{L}_len"])
+    np.testing.assert_array_equal(pcm[:512], g[f"pcm_{L}_head"])
+    np.testing.assert_array_equal(pcm[-512:], g[f"pcm_{L}_tail"])
+    np.testing.assert_array_equal(pcm[::64], g[f"pcm_{L}_s64"])
+
+
+def test_long_stream_ids_through_smallest_margin(W):
+    """The reference's long stream (2,490 calls): the oracle reproduces its ids bit for bit through
+    step 520, past the stream's smallest top1-top2 margin (2.1e-6 at step 498)."""
+    g = np.load(os.path.join(GOLDEN, "stream_long_golden.npz"))
+    Wg, Wc, tt = W
+    n = 520
+    ids, margins, _ = R.ar_decode(Wg, tt, Wc[R.CODEBOOK_KEY], g["text_ids"].tolist(), n)
+    assert ids == g["ids"][:n].tolist()
+    np.testing.assert_array_equal(np.float32(margins), g["margins"][:n])
