@@ -589,7 +589,7 @@ def parity_mode_line(S, chunk, K=2, Wm=1):
     """The fp32 parity mode (weights, KV and codec in fp32: bit-exact ids against the reference,
     tests/test_gpu_parity.py) on the same workload, K steps after Wm warm-up steps."""
     from llmvox_amd.engine import build_engine
-    eng = build_engine(torch.cuda.current_device(), "fp32", "fp32", max_streams=S, max_positions=max(K, Wm) * chunk,
+    eng = build_engine(torch.cuda.current_device(), "fp32", "fp32", max_streams=S, max_positions=max(K, Wm) * chunk + 1,
                        max_codec_frames=S * chunk)
     try:
         n_pos = max(K, Wm) * chunk

@@ -35,6 +35,8 @@ extern "C" {
 #define LVX_E_CAPACITY (-4) /* position >= block_size or KV capacity (reference: AssertionError,
                                src/model.py:205) */
 #define LVX_E_NAME (-5)     /* unknown weight name */
+#define LVX_E_INDEX (-6)    /* an embedding id out of range, reported by lvx_check_errors (reference:
+                               IndexError from nn.Embedding / the codebook gather) */
 
 #define LVX_DTYPE_F32 0
 #define LVX_DTYPE_BF16 1
@@ -74,7 +76,9 @@ int lvx_missing_weights(lvx_ctx* ctx, const char** first_missing);
 
 /* ---- text / code embeddings -------------------------------------------- */
 /* ModelHandler.llm_model(ids): T5 encoder.embed_tokens gather
- * (streaming_server.py:315,319). ids int64 [n] -> out float32 [n,256] */
+ * (streaming_server.py:315,319). ids int64 [n] -> out float32 [n,256]. An id outside [0, 386) is
+ * clamped and flagged: the next lvx_check_errors returns LVX_E_INDEX (the same for codes outside
+ * [0, 4096) in lvx_codes_to_features). */
 int lvx_text_embed(lvx_ctx* ctx, const int64_t* ids_dev, int n, float* out_dev, void* stream);
 /* WavTokenizer.codes_to_features (decoder/pretrained.py:209-239), n_q = 1:
  * codes int64 [B,L] -> features float32 [B,512,L] */
@@ -111,9 +115,9 @@ int lvx_ar_steps(lvx_ctx* ctx, int n_steps, int B, const int32_t* slots_dev, con
                  void* stream);
 /* Copy the logits [B][4096] of the last lvx_ar_step(s) call (diagnostics / tests). */
 int lvx_ar_logits(lvx_ctx* ctx, int B, float* dst_dev, void* stream);
-/* Synchronises the stream and reports (then clears) device-side capacity errors: a slot past
- * max_positions (reference: the block_size AssertionError, src/model.py:205) or a row past
- * the end of its plan. */
+/* Synchronises the stream and reports (then clears) device-side errors: an embedding id out of
+ * range (LVX_E_INDEX), a slot past max_positions (LVX_E_CAPACITY; reference: the block_size
+ * AssertionError, src/model.py:205) or a row past the end of its plan (LVX_E_CAPACITY). */
 int lvx_check_errors(lvx_ctx* ctx, void* stream);
 /* Set a slot's position and previous token (rewind after a speculative run-ahead, or jump). */
 int lvx_stream_set(lvx_ctx* ctx, int slot, int pos, int prev_token, void* stream);

@@ -20,6 +20,7 @@ LVX_E_STATE = -2
 LVX_E_HIP = -3
 LVX_E_CAPACITY = -4
 LVX_E_NAME = -5
+LVX_E_INDEX = -6
 LVX_DTYPE_F32 = 0
 LVX_DTYPE_BF16 = 1
 LVX_DTYPE_FP8 = 2  # kv_dtype only (OCP e4m3fn)
@@ -47,6 +48,10 @@ class LvxCapacityError(LvxError, AssertionError):
 
 class LvxArgError(LvxError, ValueError):
     pass
+
+
+class LvxIndexError(LvxError, IndexError):
+    """An embedding id out of range: the reference's nn.Embedding raises IndexError."""
 
 
 _P = ctypes.c_void_p
@@ -107,6 +112,8 @@ def check(code: int):
     msg = _lib.lvx_last_error().decode(errors="replace") if _lib else "unknown"
     if code == LVX_E_CAPACITY:
         raise LvxCapacityError(code, msg)
+    if code == LVX_E_INDEX:
+        raise LvxIndexError(code, msg)
     if code in (LVX_E_ARG, LVX_E_NAME):
         raise LvxArgError(code, msg)
     raise LvxError(code, msg)

@@ -2527,20 +2527,26 @@ void ar_launch_steps_end(const ArState& st, int wdtype, int B, hipStream_t s) {
 // ---------------------------------------------------------------------------------
 // gathers exposed through the drop-in members
 // ---------------------------------------------------------------------------------
+// An id outside the table raises IndexError in the reference (nn.Embedding): here the gather is
+// clamped (never faults) and error bit 4 is set, reported by lvx_check_errors as LVX_E_INDEX.
 __global__ void text_embed_kernel(const float* __restrict__ table, const int64_t* __restrict__ ids, int n,
-                                  float* __restrict__ out) {
+                                  float* __restrict__ out, int32_t* err) {
   const int r = blockIdx.x;
-  const int64_t id = min(max(ids[r], (int64_t)0), (int64_t)(TEXT_VOCAB - 1));  // clamp: never fault
+  const int64_t raw = ids[r];
+  if ((raw < 0 || raw >= TEXT_VOCAB) && threadIdx.x == 0) atomicOr(err, 4);
+  const int64_t id = min(max(raw, (int64_t)0), (int64_t)(TEXT_VOCAB - 1));
   out[(size_t)r * TEXT_DIM + threadIdx.x] = table[(size_t)id * TEXT_DIM + threadIdx.x];
 }
 
 // codes [B][L] -> feats [B][512][L]
 __global__ void codes_to_features_kernel(const float* __restrict__ cb, const int64_t* __restrict__ codes, int L,
-                                         float* __restrict__ feats) {
+                                         float* __restrict__ feats, int32_t* err) {
   const int b = blockIdx.y, c0 = blockIdx.x * 64;
   const int tid = threadIdx.x;
   for (int t = tid; t < L; t += 256) {
-    const int64_t code = min(max(codes[(size_t)b * L + t], (int64_t)0), (int64_t)4095);
+    const int64_t raw = codes[(size_t)b * L + t];
+    if ((raw < 0 || raw > 4095) && blockIdx.x == 0) atomicOr(err, 4);  // reference: IndexError
+    const int64_t code = min(max(raw, (int64_t)0), (int64_t)4095);
     for (int c = c0; c < c0 + 64; ++c) feats[((size_t)b * SPEECH_DIM + c) * L + t] = cb[(size_t)code * SPEECH_DIM + c];
   }
 }
@@ -2558,15 +2564,15 @@ void launch_set_slot(int32_t* pos, int32_t* prev, int slot, int p, int tok, hipS
   hipLaunchKernelGGL(set_slot_kernel, dim3(1), dim3(1), 0, s, pos, prev, slot, p, tok);
 }
 
-void launch_text_embed(const float* table, const int64_t* ids, int n, float* out, hipStream_t s) {
-  if (n > 0) hipLaunchKernelGGL(text_embed_kernel, dim3(n), dim3(TEXT_DIM), 0, s, table, ids, n, out);
+void launch_text_embed(const float* table, const int64_t* ids, int n, float* out, int32_t* err, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(text_embed_kernel, dim3(n), dim3(TEXT_DIM), 0, s, table, ids, n, out, err);
 }
 
 void launch_codes_to_features(const float* codebook, const int64_t* codes, int B, int L, float* feats,
-                              hipStream_t s) {
+                              int32_t* err, hipStream_t s) {
   if (B > 0 && L > 0)
     hipLaunchKernelGGL(codes_to_features_kernel, dim3(SPEECH_DIM / 64, B), dim3(256), 0, s, codebook, codes, L,
-                       feats);
+                       feats, err);
 }
 
 }  // namespace lvx

@@ -478,7 +478,7 @@ int lvx_text_embed(lvx_ctx* c, const int64_t* ids, int n, float* out, void* stre
   NEED_FINAL(c);
   if (n < 0 || (n > 0 && (!ids || !out))) return fail(LVX_E_ARG, "bad ids/out");
   HIP_TRY(hipSetDevice(c->cfg.device));
-  launch_text_embed(c->arw.text_table, ids, n, out, (hipStream_t)stream);
+  launch_text_embed(c->arw.text_table, ids, n, out, c->st.err, (hipStream_t)stream);
   HIP_TRY(hipGetLastError());
   return LVX_OK;
 }
@@ -487,7 +487,7 @@ int lvx_codes_to_features(lvx_ctx* c, const int64_t* codes, int B, int L, float*
   NEED_FINAL(c);
   if (B < 0 || L < 0 || ((B * L) > 0 && (!codes || !feats))) return fail(LVX_E_ARG, "bad codes/feats");
   HIP_TRY(hipSetDevice(c->cfg.device));
-  launch_codes_to_features(c->arw.codebook, codes, B, L, feats, (hipStream_t)stream);
+  launch_codes_to_features(c->arw.codebook, codes, B, L, feats, c->st.err, (hipStream_t)stream);
   HIP_TRY(hipGetLastError());
   return LVX_OK;
 }
@@ -520,7 +520,7 @@ int lvx_stream_position(lvx_ctx* c, int slot, int* pos_out, void* stream) {
   HIP_TRY(hipMemcpyAsync(&v[1], c->st.err, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   *pos_out = v[0];
-  if (v[1]) {
+  if (v[1] & 1) {
     (void)hipMemsetAsync(c->st.err, 0, 4, (hipStream_t)stream);
     return fail(LVX_E_CAPACITY, "a stream exceeded its KV capacity (max_positions)");
   }
@@ -712,6 +712,8 @@ int lvx_check_errors(lvx_ctx* c, void* stream) {
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   if (v) {
     (void)hipMemsetAsync(c->st.err, 0, 4, (hipStream_t)stream);
+    if (v & 4) return fail(LVX_E_INDEX, "index out of range in self (a text id outside [0, 386) or a code "
+                                         "outside [0, 4096) given to lvx_text_embed / lvx_codes_to_features)");
     if (v & 1) return fail(LVX_E_CAPACITY, "a stream exceeded its KV capacity (max_positions)");
     return fail(LVX_E_CAPACITY, "a batch row ran past the end of its text plan (plan_stride)");
   }

@@ -87,9 +87,9 @@ void ar_launch_rowinfo_init(const ArState& st, int B, hipStream_t s);
 void ar_launch_steps_end(const ArState& st, int wdtype, int B, hipStream_t s);  // deferred select: commit the last step
 int ar_select_probe(const ArWeights& w, const ArState& st, int B, int path, hipStream_t s);  // test hook
 void launch_set_slot(int32_t* pos, int32_t* prev, int slot, int p, int tok, hipStream_t s);
-void launch_text_embed(const float* table, const int64_t* ids, int n, float* out, hipStream_t s);
+void launch_text_embed(const float* table, const int64_t* ids, int n, float* out, int32_t* err, hipStream_t s);
 void launch_codes_to_features(const float* codebook, const int64_t* codes, int B, int L, float* feats,
-                              hipStream_t s);
+                              int32_t* err, hipStream_t s);
 
 // ---------------- codec ----------------
 struct CodecWeights {

@@ -26,6 +26,15 @@ from .tokenizer import ByteTokenizer
 from . import weights as LW
 
 
+def _check_ids(ids: torch.Tensor, n: int):
+    """nn.Embedding's IndexError for ids outside [0, n), raised at the call as the reference does
+    when the ids are on the host (the reference builds them there, streaming_server.py:313-314,
+    328, 363). Device-resident ids are checked by the gather kernel instead (LVX_E_INDEX, raised as
+    IndexError by the next Engine.check_errors) so the call stays asynchronous."""
+    if ids.device.type == "cpu" and ids.numel() and (int(ids.min()) < 0 or int(ids.max()) >= n):
+        raise IndexError("index out of range in self")
+
+
 class _SlotLease:
     """One KV slot owned by one decode sequence; returned to the pool when the last
     handle of the sequence is garbage-collected (the reference drops its cache by
@@ -124,6 +133,7 @@ class TextEmbedding:
         self.embedding_dim = C.TEXT_DIM
 
     def __call__(self, ids: torch.Tensor) -> torch.Tensor:
+        _check_ids(ids, C.TEXT_VOCAB)
         return self.engine.text_embed(ids)
 
 
@@ -142,6 +152,7 @@ class WavTokenizerDecoder:
             raise ValueError("codes must be (K, L) or (K, B, L)")
         if codes.shape[0] != 1:
             raise IndexError("index out of range in self (n_q = 1: only one codebook)")
+        _check_ids(codes, C.VOCAB)
         return self.engine.codes_to_features(codes[0])
 
     def decode(self, features_input: torch.Tensor, bandwidth_id: Optional[torch.Tensor] = None, **kw):

@@ -20,8 +20,13 @@ Differences, on purpose:
     as an LLM stream would end, so the replica that receives it ends the response at its
     end-of-audio token.
   * ``max_tokens`` bounds a request (the reference relies on the model emitting end-of-audio;
-    synthetic weights never do): when a request's streams have generated that many tokens each,
-    their undumped tail is decoded and the response ends.
+    synthetic weights never do): a stream that was fed text stops once it has generated
+    ``max_tokens`` tokens, or when its segment would outgrow the KV capacity (``max_positions``);
+    when every fed stream of a request has stopped or gone idle, their undumped tails are decoded
+    and the response ends. A stream that never received text (a one-sentence request leaves
+    replica 1 empty) does not hold a request open.
+  * a KV-capacity error of the decode step ends the request(s) whose streams are at the capacity
+    edge (all open requests if none is), not the service.
 """
 
 import threading
@@ -37,6 +42,7 @@ class _Session:
         self.streams = streams
         self.queues = queues
         self.done = False
+        self.error: Optional[BaseException] = None
 
 
 class TTSService:
@@ -92,6 +98,8 @@ class TTSService:
             self.close(session)
         if self.error is not None:
             raise RuntimeError("TTS scheduler thread failed") from self.error
+        if session.error is not None:
+            raise RuntimeError("request ended by a KV-capacity error") from session.error
 
     def close(self, session: _Session):
         with self.lock:
@@ -108,28 +116,47 @@ class TTSService:
         self.thread.join(timeout=5)
 
     # -- scheduler thread --
-    def _cap(self):
-        """End every session whose streams reached max_tokens: decode their undumped tails in
-        speaking order, then 'end' on both queues."""
-        for s in list(self.sessions):
-            if s.done or min(len(st.tokens) for st in s.streams) < self.max_tokens:
-                continue
-            s.done = True
-            tails = [(st, st.m.speech_outputs) for st in s.streams if st.m.speech_outputs]
-            for st, toks in tails:
-                st.m.speech_outputs = []
-                import torch
-                codes = torch.tensor([toks], dtype=torch.int32, device=self.engine.device)
-                st._out(self.engine.decode_codes(codes).cpu().numpy()[0].astype("float32").tobytes())
-            for q in s.queues:
-                q.put("end")
+    def _stopped(self, st) -> bool:
+        """A fed stream stops at max_tokens, or when its segment would outgrow the KV capacity
+        within the next chunk; stopping closes its text side (the scheduler then skips it)."""
+        if not st.m.closed and (len(st.tokens) >= self.max_tokens or
+                                st.m.position + self.sched.max_chunk >= self.engine.max_positions):
+            st.m.closed = True
+        return st.m.closed
+
+    def _end(self, s: _Session, error: Optional[BaseException] = None):
+        """Decode the undumped tails of the session's fed streams, then 'end' on both queues."""
+        import torch
+        s.done = True
+        s.error = error
+        if error is None:
             for st in s.streams:
-                if st in self.sched.streams:
-                    self.sched.close_stream(st)
+                if st.fed and st.m.speech_outputs:
+                    toks, st.m.speech_outputs = st.m.speech_outputs, []
+                    codes = torch.tensor([toks], dtype=torch.int32, device=self.engine.device)
+                    st._out(self.engine.decode_codes(codes).cpu().numpy()[0].astype("float32").tobytes())
+        for q in s.queues:
+            q.put("end")
+        for st in s.streams:
+            if st in self.sched.streams:
+                self.sched.close_stream(st)
+
+    def _cap(self):
+        """End every session whose fed streams have all stopped (max_tokens / KV capacity) or gone
+        idle (no text left), provided at least one of them stopped."""
+        for s in list(self.sessions):
+            if s.done:
+                continue
+            fed = [st for st in s.streams if st.fed]
+            stopped = [self._stopped(st) for st in fed]
+            idle = [st.m.closed or st.m.next_text_id() is None for st in fed]
+            if fed and any(stopped) and all(idle):
+                self._end(s)
 
     def _loop(self):
-        try:
-            while True:
+        from ._lib import LvxCapacityError
+        while True:
+            try:
                 with self.lock:
                     if not self.running:
                         return
@@ -137,10 +164,19 @@ class TTSService:
                     if n:
                         self._cap()
                     else:
+                        self._cap()
                         self.lock.wait(timeout=0.01)
-        except BaseException as e:  # surfaced to every waiting request
-            self.error = e
-
+            except LvxCapacityError as e:  # only the sessions at the capacity edge fail
+                with self.lock:
+                    live = [s for s in self.sessions if not s.done]
+                    edge = [s for s in live
+                            if any(st.m.position + self.sched.max_chunk >= self.engine.max_positions
+                                   for st in s.streams)]
+                    for s in edge or live:
+                        self._end(s, error=e)
+            except BaseException as e:  # surfaced to every waiting request
+                self.error = e
+                return
 
 def create_app(service):
     """FastAPI app with the reference's /tts contract (TTSRequest {text} -> octet-stream)."""

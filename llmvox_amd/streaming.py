@@ -355,8 +355,10 @@ class FusedStream:
         self.sink = sink if sink is not None else Queue()
         self.events: List[object] = []   # decoded items in order: bytes or signals
         self.tokens: List[int] = []      # every greedy token consumed (diagnostics / tests)
+        self.fed = False                 # a word has been fed (the service caps only fed streams)
 
     def feed(self, word):
+        self.fed = True
         self.m.feed(word)
 
     def _out(self, item):

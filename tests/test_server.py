@@ -38,7 +38,8 @@ def test_tts_endpoint_streams_f32le_chunks():
 def test_tts_service_matches_fused_scheduler():
     """Replica 0 gets the first sentence (and the EOS token routed after the last one), replica 1
     the second. Replica 1's audio would follow replica 0's end-of-audio signal; synthetic weights
-    never emit end-of-audio, so the response is replica 0's chunks plus its tail at max_tokens."""
+    never emit end-of-audio, so the response is replica 0's chunks plus its tail at max_tokens
+    (each fed stream stops at its own max_tokens)."""
     import torch  # noqa: F401
     from fastapi.testclient import TestClient
     from llmvox_amd.engine import build_engine
@@ -59,8 +60,11 @@ def test_tts_service_matches_fused_scheduler():
         a.feed(w)
     for w in "Jumps over the dog.".split():
         b.feed(w)
-    while min(len(a.tokens), len(b.tokens)) < 200:
+    while not (a.m.closed and b.m.closed):  # each stream stops at its own 200th token
         sch.run_chunk()
+        for st in (a, b):
+            if len(st.tokens) >= 200:
+                st.m.closed = True
     sch.flush()
     ref = []
     for st in (a,):
@@ -74,3 +78,82 @@ def test_tts_service_matches_fused_scheduler():
     want = np.frombuffer(b"".join(ref), dtype=np.float32)
     assert got.shape == want.shape
     assert np.abs(got - want).max() < 1e-5
+
+
+@pytest.fixture(scope="module")
+def handler():
+    from llmvox_amd.config import default_config
+    from llmvox_amd.handler import ModelHandler
+    return ModelHandler(default_config(weight_dtype="fp32", kv_dtype="fp32", max_streams=8, max_positions=1024),
+                        device_id=0)
+
+
+@pytest.mark.gpu
+def test_one_sentence_without_period_ends_and_service_survives(handler):
+    """'hello world' routes every word and the EOS token to replica 0; replica 1 never gets text.
+    The request must still end (replica 0 stops at max_tokens), and the service must keep serving."""
+    from fastapi.testclient import TestClient
+    from llmvox_amd.server import TTSService, create_app
+    svc = TTSService(handler.engine, max_chunk=32, max_tokens=96)
+    try:
+        client = TestClient(create_app(svc))
+        for text in ("hello world", "again, no period"):
+            r = client.post("/tts", json={"text": text})
+            assert r.status_code == 200
+            pcm = np.frombuffer(r.content, dtype=np.float32)
+            assert pcm.size == 320 * 96  # 10 + 30 (dumps) + the 56-token tail at the cap
+        assert client.get("/health").json() == {"ok": True, "sessions": 0}
+    finally:
+        svc.shutdown()
+
+
+def _segment_tokens(eng, words, n):
+    from llmvox_amd.streaming import FusedScheduler
+    sch = FusedScheduler(eng, max_chunk=64)
+    st = sch.open_stream(index=0, dump_size=10_000)
+    for w in words:
+        st.feed(w)
+    while len(st.tokens) < n:
+        assert sch.run_chunk() > 0
+    sch.close_stream(st)
+    return st.tokens[:n]
+
+
+@pytest.mark.gpu
+def test_tts_two_replica_order_matches_reference_consumers(handler):
+    """POST /tts with an end-of-audio id that every segment emits (chosen from the synthetic model's
+    own tokens): replica 0's chunks -> its switch signal -> replica 1's chunks -> its switch back ->
+    replica 0's EOS segment -> 'end' (streaming_server.py:397-404,428-469). The response body must
+    be the byte stream the reference's consumers produce on the same engine: two
+    audio_generator_sync threads' queues (the drop-in ModelHandler) read in speaking order."""
+    import queue
+    from fastapi.testclient import TestClient
+    from llmvox_amd import streaming as S
+    from llmvox_amd.server import TTSService, create_app
+    eng = handler.engine
+    text = "The quick brown fox. Jumps over the dog."
+    segs = [["The", "quick", "brown", "fox."], ["Jumps", "over", "the", "dog."], ["<|eot_id|>"]]
+    toks = [_segment_tokens(eng, w, 120) for w in segs]
+    common = [t for t in toks[0][12:] if t in toks[1][5:] and t in toks[2][5:]]
+    assert common, "no token shared by the three segments"
+    eoa = common[0]
+    cfg = {"eoa_token_id": eoa}
+    # the reference-shaped consumers, one replica after the other (each ends at its None word)
+    qs_text, qs_audio = [queue.Queue(), queue.Queue()], [queue.Queue(), queue.Queue()]
+    routed = S.route_text(text.split() + ["<|eot_id|>"], qs_text)
+    assert routed[-1] == "<|eot_id|>"
+    for q in qs_text:
+        q.put(None)
+    for i, dump in ((0, 10), (1, 160)):
+        S.audio_generator_sync(i, dump, handler, qs_text[i], qs_audio[i], config=cfg)
+    trace = [list(q.queue) for q in qs_audio]
+    assert trace[0].count(1) == 1 and trace[0].count("end") == 1 and trace[1].count(0) == 1
+    want = b"".join(S.audio_chunks(qs_audio[0], qs_audio[1], timeout=0.01))
+    svc = TTSService(eng, max_chunk=32, max_tokens=4000, eoa_id=eoa)
+    try:
+        body = TestClient(create_app(svc)).post("/tts", json={"text": text}).content
+    finally:
+        svc.shutdown()
+    got, ref = np.frombuffer(body, dtype=np.float32), np.frombuffer(want, dtype=np.float32)
+    assert got.shape == ref.shape and got.size > 0
+    assert np.abs(got - ref).max() < 1e-5

@@ -1,13 +1,30 @@
 #!/bin/bash
-# kernel-trace profiles: AR at B = 1 and 32, codec at 1 x 256 and 32 x 256 frames
+# Round measurement refresh (round 2+): PMC passes over the driver's default bench command
+# (configs[2], --steps 20: the roofline probe at KV position 2,560), kernel-trace stats of it, and
+# the bench line itself. Outputs under gpurun_out/$TAG; copy the summaries to profiles/.
+#   FETCH_SIZE and WRITE_SIZE passes  -> tools/pmc_traffic.py  -> pmc_traffic.json
+#   SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE pass -> tools/pmc_codec.py -> pmc_codec.json
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 export PYTHONPATH=.
-mkdir -p gpurun_out
-rm -rf gpurun_out/p_*
-for cfg in "ar1 tools/prof_ar.py bf16 1" "ar32 tools/prof_ar.py bf16 32" "c1 tools/prof_codec.py bf16 256 1" "c32 tools/prof_codec.py bf16 256 32"; do
-  set -- $cfg
-  tag=$1; shift
-  timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/p_$tag -o run --output-format csv -- python3 "$@" > gpurun_out/p_$tag.log 2>&1 || { echo "FAIL $tag"; exit 1; }
-done
-echo OK
+TAG=${TAG:-r02}
+O=gpurun_out/$TAG; mkdir -p $O
+ARGS=${ARGS:-"--steps 20 --warmup 0 --no-cpu-baseline --no-parity-line"}
+KEY=${KEY:-bf16/kvbf16/B32/P2560}
+CKEY=${CKEY:-bf16/F8192/L256}
+run() { # tag, timeout, rocprof args..., -- cmd
+  local tag=$1 t=$2; shift 2
+  timeout -s KILL $t rocprofv3 "$@" > $O/$tag.log 2>&1 || { echo "FAIL $tag"; tail -30 $O/$tag.log; exit 1; }
+}
+csv() { find $O/$1 -name "*counter_collection.csv" | head -1; }
+run f 300 --pmc FETCH_SIZE -d $O/f -o run --output-format csv -- python3 bench.py $ARGS
+run w 300 --pmc WRITE_SIZE -d $O/w -o run --output-format csv -- python3 bench.py $ARGS
+python3 tools/pmc_traffic.py $(csv f) $(csv w) $KEY $O/pmc_traffic.json > $O/pmc_traffic.txt || exit 1
+cat $O/pmc_traffic.txt
+run m 300 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d $O/m -o run --output-format csv -- python3 bench.py $ARGS
+python3 tools/pmc_codec.py $(csv m) $CKEY $O/pmc_codec.json || exit 1
+run kt 300 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 bench.py $ARGS
+find $O/kt -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
+timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.jsonl 2> $O/bench.err || { echo BENCH_FAIL; tail -20 $O/bench.err; exit 1; }
+tail -c 600 $O/bench.jsonl
+echo PROF_OK
