@@ -21,10 +21,13 @@ run f 300 --pmc FETCH_SIZE -d $O/f -o run --output-format csv -- python3 bench.p
 run w 300 --pmc WRITE_SIZE -d $O/w -o run --output-format csv -- python3 bench.py $ARGS
 python3 tools/pmc_traffic.py $(csv f) $(csv w) $KEY $O/pmc_traffic.json > $O/pmc_traffic.txt || exit 1
 cat $O/pmc_traffic.txt
+rm -rf $O/f $O/w  # raw per-dispatch CSVs: too large to merge back (gpurun_out <= 64 MiB)
 run m 300 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d $O/m -o run --output-format csv -- python3 bench.py $ARGS
 python3 tools/pmc_codec.py $(csv m) $CKEY $O/pmc_codec.json || exit 1
+rm -rf $O/m
 run kt 300 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 bench.py $ARGS
 find $O/kt -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
+rm -rf $O/kt
 timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.jsonl 2> $O/bench.err || { echo BENCH_FAIL; tail -20 $O/bench.err; exit 1; }
 tail -c 600 $O/bench.jsonl
 echo PROF_OK
