@@ -1779,39 +1779,41 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
       a.st.x[(size_t)b * D + n] = xn;
       a.st.xb[(size_t)b * D + n] = f32_to_bf16(xn);
       xo[e] = xn;
-    } else if (OUT == 8) {  // K-slice slab of the split mlp c_proj (reduced by the tile's last arriver)
-      a.yacc[((size_t)b * YCOPIES + blockIdx.y) * D + n] = v;
+    } else if (OUT == 8) {  // K-slice slab of the split mlp c_proj (reduced by the tile's last arriver):
+      // write-through (sc1) store, so the hand-off needs no release fence (cdna_hip_programming.md
+      // Guideline 16 R1)
+      __hip_atomic_store((gu32*)(a.yacc + ((size_t)b * YCOPIES + blockIdx.y) * D + n),
+                         __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       gemv_store<OUT>(a, n, b, v);
     }
   }
   if constexpr (OUT == 8) {
     // In-launch split-K combine (cdna_hip_programming.md, "Projection GEMM at M = 256" item 2, the
-    // Guideline 16 counter form): slabs drained, agent release, ticket; the tile's last arriving
-    // slice acquires, sums the slabs in slice order (deterministic), adds the residual and leaves
-    // final x + its bf16 copy + the column statistics, so the next LayerNorm needs no rows kernel.
+    // Guideline 16 counter form with write-through slabs): every wave drains its sc1 slab stores,
+    // barrier, one relaxed agent ticket per block; the tile's last arriving slice reads the slabs
+    // with sc1 loads (no acquire fence, R1), sums them in slice order (deterministic), adds the
+    // residual and leaves final x + its bf16 copy + the column statistics, so the next LayerNorm
+    // needs no rows kernel. x of this tile's columns is written only by this block in the launch.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned tk = __hip_atomic_fetch_add(a.st.tick + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned tk = __hip_atomic_fetch_add((gu32*)(a.st.tick + blockIdx.x), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const bool last = tk == gridDim.y - 1;
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(a.st.tick + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      if (last) __hip_atomic_store((gu32*)(a.st.tick + blockIdx.x), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       red[0][0] = last ? 1.f : 0.f;
     }
     __syncthreads();
     if (red[0][0] == 0.f) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below here
     for (int e = tid; e < 16 * NT * 16; e += NW * 64) {
       const int r = e / (NT * 16), b = r0 + e - r * (NT * 16), n = n0 + r;
       if (b >= B) continue;
       float t = a.st.x[(size_t)b * D + n];
 #pragma unroll
-      for (int c = 0; c < YCOPIES; ++c) t += a.yacc[((size_t)b * YCOPIES + c) * D + n];
+      for (int c = 0; c < YCOPIES; ++c)
+        t += __uint_as_float(__hip_atomic_load((gu32*)(a.yacc + ((size_t)b * YCOPIES + c) * D + n),
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
       a.st.x[(size_t)b * D + n] = t;
       a.st.xb[(size_t)b * D + n] = f32_to_bf16(t);
       xo[e] = t;

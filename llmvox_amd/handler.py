@@ -87,10 +87,11 @@ class SpeechGPT:
     inference (is_train False). Only the last row of ``emb`` is computed; its position is
     t-1 and K/V of the earlier rows live in the library's slot for this sequence."""
 
-    def __init__(self, engine: Engine, pool: _SlotPool):
+    def __init__(self, engine: Engine, pool: _SlotPool, block_size: int = C.BLOCK_SIZE):
         self.engine = engine
         self.pool = pool
         self.config = C
+        self.block_size = int(block_size)
 
     def __call__(self, emb: torch.Tensor, targets=None, kvcache=None):
         if targets is not None:
@@ -98,7 +99,7 @@ class SpeechGPT:
         if emb.dim() != 3 or emb.shape[0] != 1 or emb.shape[2] != C.N_EMBD:
             raise ValueError(f"expected emb [1, t, {C.N_EMBD}], got {tuple(emb.shape)}")
         t = emb.shape[1]
-        assert t <= C.BLOCK_SIZE, f"Cannot forward sequence of length {t}, block size is only {C.BLOCK_SIZE}"
+        assert t <= self.block_size, f"Cannot forward sequence of length {t}, block size is only {self.block_size}"
         if not kvcache:
             if t != 1:
                 raise NotImplementedError(
@@ -180,22 +181,23 @@ class ModelHandler:
             raise RuntimeError("llmvox_amd.ModelHandler needs a ROCm GPU; there is no CPU path")
         dev = 0 if device_id is None else int(device_id)
         get = config.get if hasattr(config, "get") else (lambda k, d=None: getattr(config, k, d))
-        self.engine = Engine(dev, get("weight_dtype", "fp32"), get("kv_dtype", "fp32"),
-                             int(get("max_streams", 8)), int(get("max_positions", C.BLOCK_SIZE)),
-                             int(get("max_codec_frames", C.MAX_DUMP_SIZE)), get("codec_dtype", None))
-        self.device = self.engine.device
         src = get("weights", "synthetic")
         if src == "synthetic":
             gw, cw, tt = LW.synthetic_all(int(get("seed", 1234)))
-        else:
+        else:  # the reference's three checkpoints (model_handler.py:80-106,140-166)
             gw = LW.load_llmvox_checkpoint(get("llmvox_checkpoint_path"))
             cw = LW.load_wavtokenizer_checkpoint(get("wav_model_path"))
             tt = LW.load_text_embed_from_t5(_load_t5_state(get("encoder_model_path")))
+        block = int(getattr(gw, "block_size", C.BLOCK_SIZE))
+        self.engine = Engine(dev, get("weight_dtype", "fp32"), get("kv_dtype", "fp32"),
+                             int(get("max_streams", 8)), min(int(get("max_positions", C.BLOCK_SIZE)), block),
+                             int(get("max_codec_frames", C.MAX_DUMP_SIZE)), get("codec_dtype", None))
+        self.device = self.engine.device
         self.engine.load_weights(gw, cw, tt)
         self.wavtokenizer = WavTokenizerDecoder(self.engine)
         self.tokenizer = ByteTokenizer()
         self.llm_model = TextEmbedding(self.engine)
-        self.model = SpeechGPT(self.engine, _SlotPool(self.engine.max_streams))
+        self.model = SpeechGPT(self.engine, _SlotPool(self.engine.max_streams), block)
 
     # upstream LLM producers are outside the hot path
     def initialize_stream_model(self):

@@ -169,28 +169,50 @@ def synthetic_all(seed: int = 1234):
 # file: torch.load(weights_only=True).
 # ---------------------------------------------------------------------------
 
-def load_llmvox_checkpoint(path: str) -> Weights:
-    """ckpt_english_tiny.pt: {'model': state_dict, 'model_args': {...}} with an optional
-    ``_orig_mod.`` prefix from torch.compile (inference/model_handler.py:148-163)."""
+class GPTWeights(dict):
+    """GPT state dict (reference keys, fp32 numpy) + the checkpoint's ``block_size`` (the reference's
+    GPT.forward asserts t <= block_size, src/model.py:205)."""
+    block_size: int = C.BLOCK_SIZE
+
+
+def load_llmvox_checkpoint(path: str) -> GPTWeights:
+    """A checkpoint in the reference's save layout (src/utils.py:147-153: 'model', 'optimizer',
+    'model_args', 'iter_num', 'config'), read as inference/model_handler.py:148-165 reads it:
+    ``model_args`` fixes the architecture, ``_orig_mod.`` prefixes (torch.compile) are stripped,
+    missing keys would keep their init under strict=False (here the hot-path keys are required).
+
+    block_size: the library's position table holds 8192 rows (GPTConfig.block_size of the shipped
+    model); a smaller block_size pads wpe with zero rows it can never reach (the returned
+    ``block_size`` bounds positions, as the reference's assert does), a larger one is rejected."""
     import torch
     ck = torch.load(path, map_location="cpu", weights_only=True)
-    args = ck.get("model_args", {})
+    if "model" not in ck or "model_args" not in ck:
+        raise KeyError("not an LLMVoX checkpoint: needs 'model' and 'model_args' (src/utils.py:147-153)")
+    args = ck["model_args"]
     for k, v in (("n_layer", C.N_LAYER), ("n_head", C.N_HEAD), ("n_embd", C.N_EMBD), ("vocab_size", C.VOCAB)):
         if k in args and int(args[k]) != v:
             raise ValueError(f"checkpoint {k}={args[k]} but this build is specialised for {v}")
     if args.get("bias", False):
         raise ValueError("checkpoint has bias=True; the reference inference model uses bias=False")
-    sd = ck["model"]
-    out = {}
-    for k, v in sd.items():
+    block = int(args.get("block_size", C.BLOCK_SIZE))
+    if not 1 <= block <= C.BLOCK_SIZE:
+        raise ValueError(f"checkpoint block_size={block}: this build holds at most {C.BLOCK_SIZE} positions")
+    out = GPTWeights()
+    out.block_size = block
+    for k, v in ck["model"].items():
         if k.startswith("_orig_mod."):
             k = k[len("_orig_mod."):]
         out[k] = v.float().cpu().numpy()
     # strict=False in the reference: missing keys keep their init; we require the hot-path ones.
-    missing = [k for k in gpt_param_shapes(block=out.get("transformer.wpe.weight", np.zeros((C.BLOCK_SIZE, 1))).shape[0])
-               if k not in out]
+    missing = [k for k in gpt_param_shapes(block=block) if k not in out]
     if missing:
         raise KeyError(f"checkpoint lacks hot-path weights: {missing[:4]}...")
+    wpe = out["transformer.wpe.weight"]
+    if wpe.shape != (block, C.N_EMBD):
+        raise ValueError(f"transformer.wpe.weight is {wpe.shape}, model_args block_size {block}")
+    if block < C.BLOCK_SIZE:
+        out["transformer.wpe.weight"] = np.concatenate(
+            [wpe, np.zeros((C.BLOCK_SIZE - block, C.N_EMBD), np.float32)], 0)
     return out
 
 

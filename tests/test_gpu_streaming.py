@@ -152,3 +152,45 @@ def test_fused_overlap_delivers_same_items(handler):
         for x, y in zip(a, b):
             assert type(x) is type(y)
             assert x == y
+
+
+def test_checkpoint_handler_reproduces_reference_stream(tmp_path_factory):
+    """ModelHandler(weights="checkpoint") on the reference's three checkpoint layouts (written by
+    tests/ckpt_files.py from the synthetic weights, optimizer / config entries included) runs the
+    reference-shaped stream and reproduces the reference's golden chunks."""
+    from llmvox_amd.config import default_config
+    from llmvox_amd.handler import ModelHandler
+    from tests.ckpt_files import write_all
+    paths = write_all(str(tmp_path_factory.mktemp("ckpt")))
+    cfg = dict(default_config(weight_dtype="fp32", kv_dtype="fp32", max_streams=4, max_positions=1024),
+               weights="checkpoint", **paths)
+    h = ModelHandler(cfg, device_id=0)
+    g = np.load(os.path.join(GOLDEN, "stream_golden.npz"))
+    items = _run_dropin(h, WORDS, int(g["model_calls"]))
+    chunks = [np.frombuffer(b, dtype=np.float32) for b in items]
+    assert [len(c) for c in chunks] == g["sizes"].tolist()
+    for i in range(3):
+        assert np.abs(chunks[i] - g[f"chunk{i}"]).max() < 2e-4
+    h.engine.close()
+
+
+def test_checkpoint_block_size_bounds_positions(tmp_path_factory):
+    """A checkpoint with block_size 64: the drop-in .model raises the reference's AssertionError at
+    t = 65 (src/model.py:205)."""
+    import torch.nn.functional as F
+    from llmvox_amd.config import default_config
+    from llmvox_amd.handler import ModelHandler
+    from tests.ckpt_files import write_all
+    paths = write_all(str(tmp_path_factory.mktemp("ckpt64")), block_size=64)
+    cfg = dict(default_config(weight_dtype="fp32", kv_dtype="fp32", max_streams=2, max_positions=1024),
+               weights="checkpoint", **paths)
+    h = ModelHandler(cfg, device_id=0)
+    assert h.engine.max_positions == 64
+    hist, kv = None, None
+    for i in range(64):
+        x = F.normalize(torch.randn(1, 1, 768, device=h.device), dim=2)
+        hist = x if hist is None else torch.cat([hist, x], dim=1)
+        _, _, kv = h.model(hist, kvcache=kv)
+    with pytest.raises(AssertionError, match="block size is only 64"):
+        h.model(torch.cat([hist, x], dim=1), kvcache=kv)
+    h.engine.close()
