@@ -138,17 +138,16 @@ int lvx_select_probe(lvx_ctx* ctx, int path, int B, const int32_t* slots_dev, co
                      float* margin_plan_dev, void* stream);
 /* Host-side view of a slot's position (synchronises the stream). */
 int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
-/* Kernel-variant switches for in-process A/B timing (defaults and measurements: DESIGN.md §4 and
- * the comments at their definitions in ar_kernels.hip / codec_kernels.hip): "gemv_reg"
- * (register-path GEMV, B <= 4), "attn_v2", "cproj_b1", "prefetch_in", "mfma_batch" (smallest B of
- * the bf16 MFMA path; 0 off), "fuse_mlp" (bf16 fused MLP, B <= 2: 1 = 16 h rows per block, 2 = 32,
- * 3 = 12; 0 off), "fuse_argmax" (greedy select inside lm_head, B <= 4), "defer_select" (greedy
- * select in the next step's first kernel: 1 = B <= 2 and B >= 4, 2 = also B = 3, 0 = separate
- * argmax kernel), "mfma_ln" (largest B whose batched GEMMs normalise their rows in the prologue),
- * "bt" / "bt_rows" / "bt_merge" (batched v3 path), "ln_stats", "attn_blocks", "attn_depth",
- * "attn_waves", "b1_splits", "codec_g2", "codec_g2_min", "codec_xcd", "codec_bm256".
- * The variants compute the same step (bit-equal or within bf16 rounding: tests/test_gpu_select.py,
- * tests/test_gpu_batched.py); changing an option drops the captured graphs. */
+/* Cross-check switches between two correct implementations of the same step (process-wide; every
+ * context drops its captured graphs on its next call after a change). Defaults are the measured-
+ * faster variants:
+ *   "defer_select" 1: the greedy select is committed by the next step's first kernel (B <= 2: c_attn
+ *                     layer 0 reduces lm_head's granules; B >= 4: ar_embed_select); 0: ar_argmax_kernel
+ *                     after every lm_head (bit-identical results: tests/test_gpu_select.py);
+ *   "fuse_mlp"     1: bf16, B <= 2: c_fc + gelu + mlp c_proj in one kernel (fp32 atomics in arrival
+ *                     order); 0: the two deterministic GEMV kernels;
+ *   "bt"           1: batched path v3 for 32 < B <= 64; 2: v3 for every batched B; 0: never;
+ *   "codec_g2"     1: large-M bf16 codec GEMMs on the 128 x 128 MFMA tile kernel; 0: the general one. */
 int lvx_set_option(lvx_ctx* ctx, const char* name, int value);
 /* Enable/disable HIP-graph replay of lvx_ar_step for a given B (default on). */
 int lvx_set_graphs(lvx_ctx* ctx, int enable);

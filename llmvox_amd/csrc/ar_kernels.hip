@@ -56,7 +56,6 @@ struct GemvArgs {
   const float* codebook;
   const float* wpe;
   const float* emb_row;  // drop-in row mode when non-null
-  int prefetch;          // inputs of the first group issued before the weights (option "prefetch_in")
   // fused MLP (ar_mlp_fused_kernel): its output sits in YCOPIES accumulators until c_proj folds it in
   float* yacc;           // non-null when the step runs the fused MLP
   int add_y;             // c_proj: fold the accumulators into x (layers >= 1; 0 at layer 0 = just clear)
@@ -398,7 +397,7 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
   // embedding math then overlaps the weight stream instead of waiting behind it
   XRow<IN == 4 ? 4 : 0> xpre;
   int4 ripre = make_int4(-1, 0, 0, 0);
-  const bool prefetched = a.prefetch && wave < min(BG, a.B);
+  const bool prefetched = wave < min(BG, a.B);
   // control record of this lane's epilogue row in the first batch group (bb = lane % BG): the
   // KV append needs (slot, pos); loading it here keeps it off the epilogue's critical path
   int4 riep = make_int4(-1, 0, 0, 0);
@@ -570,7 +569,7 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
           a.st.h[(size_t)b * DFF + n] = gelu_tanh(v);
         } else {
           a.dst[(size_t)b * a.N + n] = v;
-          if (OUT == 4 || OUT == 9) part[wave][r][bb] = v;
+          if (OUT == 9) part[wave][r][bb] = v;
         }
       }
     }
@@ -595,67 +594,9 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
     }
     if (blockIdx.x == 0 && tid == 0) *a.st.selp = 1u;
   }
-  if constexpr (OUT == 4) {
-    // fused greedy select (B <= BG: one batch group). Each block publishes its top1/top2 per row
-    // as two 8-byte granules with write-through (sc1) atomic stores, drains them, and draws a
-    // ticket; the last arriving block reads every block's granules with sc1 loads (no acquire
-    // fence needed for this hand-off form, cdna_hip_programming.md Guideline 16 R1) and commits.
-    __syncthreads();
-    if (tid < a.B) {
-      Best r{-INFINITY, -INFINITY, 0x7fffffff};
-#pragma unroll
-      for (int w = 0; w < 4; ++w)
-#pragma unroll
-        for (int rr = 0; rr < RPW; ++rr) {
-          const int n = (blockIdx.x * 4 + w) * RPW + rr;
-          if (n < a.N) r = best_merge(r, Best{part[w][rr][tid], -INFINITY, n});
-        }
-      gu64* g = ((gu64*)a.st.lmbest) + ((size_t)blockIdx.x * 4 + tid) * 2;
-      __hip_atomic_store(g, ((unsigned long long)(unsigned)r.i << 32) | __float_as_uint(r.v), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(g + 1, (unsigned long long)__float_as_uint(r.v2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      const unsigned tk = __hip_atomic_fetch_add(((gu32*)a.st.ticket), 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-      part[0][0][0] = (tk == gridDim.x - 1) ? 1.f : 0.f;
-    }
-    __syncthreads();
-    if (part[0][0][0] == 0.f) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (wave < a.B) {  // wave b reduces row b over all blocks
-      // all granule loads in flight at once (one round trip): gridDim.x <= 8 * 64 (host-checked)
-      unsigned long long g0v[8], g1v[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int blk = lane + 64 * k;
-        if (blk < (int)gridDim.x) {
-          const gu64* g = ((const gu64*)a.st.lmbest) + ((size_t)blk * 4 + wave) * 2;
-          g0v[k] = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          g1v[k] = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-      Best r{-INFINITY, -INFINITY, 0x7fffffff};
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (lane + 64 * k < (int)gridDim.x)
-          r = best_merge(r, Best{__uint_as_float((unsigned)g0v[k]), __uint_as_float((unsigned)g1v[k]), (int)(g0v[k] >> 32)});
-      r = best_wave(r);
-      if (lane == 0) argmax_commit(a.st, wave, a.st.rowinfo[wave], r);
-    }
-    if (tid == 0) __hip_atomic_store(((gu32*)a.st.ticket), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
 }
 
-// ---------------------------------------------------------------------------------
-// Register-path GEMV for B <= 4 rows (the B = 1 latency path). No LDS and no barrier unless K is
-// split across waves: every wave loads its inputs FIRST (x rows / h chunks / control records),
-// then its weight rows, and computes LayerNorm / the embedding in registers while the weight
-// stream is in flight (vmcnt counts in issue order, so inputs issued first are usable first).
-// The lane layout of the inputs (k = i*256 + lane*4) is the lane layout of the weight chunks.
-// ---------------------------------------------------------------------------------
+// GEMV / batched-GEMM epilogue store of output n of batch row b
 template <int OUT>
 __device__ __forceinline__ void gemv_store(const GemvArgs& a, int n, int b, float v) {
   if (OUT == 0) {
@@ -700,152 +641,6 @@ __device__ __forceinline__ void wave_ln_regs(float4 (&v)[3], const float4 (&g)[3
 #pragma unroll
   for (int j = 0; j < 3; ++j)
     v[j] = make_float4(v[j].x * rstd * g[j].x, v[j].y * rstd * g[j].y, v[j].z * rstd * g[j].z, v[j].w * rstd * g[j].w);
-}
-
-template <typename TW, int K, int KW, int RPW, int BB, int IN, int OUT>
-__global__ __launch_bounds__(256) void ar_gemv_reg_kernel(GemvArgs a) {
-  static_assert(IN != 2, "the split-KV merge needs the LDS path");
-  static_assert(IN == 1 || KW == 1, "LayerNorm inputs need the whole row in one wave");
-  constexpr int KC = K / KW, NI = KC / 256, WROWS = 4 / KW;
-  __shared__ float part[KW > 1 ? 4 * RPW * BB : 1];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int rg = wave / KW, kp = wave % KW;
-  const int row0 = (blockIdx.x * WROWS + rg) * RPW;
-  const int B = a.B;
-  // 1. inputs first
-  float4 xin[BB][NI];
-  int4 ri[BB];
-  float4 g[3];
-  if (IN == 0 || IN == 3) {
-#pragma unroll
-    for (int j = 0; j < 3; ++j) g[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
-  }
-#pragma unroll
-  for (int b = 0; b < BB; ++b) {
-    if (b >= B) continue;
-    if (IN == 0) {
-#pragma unroll
-      for (int i = 0; i < NI; ++i) xin[b][i] = *reinterpret_cast<const float4*>(a.st.x + (size_t)b * D + i * 256 + lane * 4);
-    } else if (IN == 1) {
-#pragma unroll
-      for (int i = 0; i < NI; ++i)
-        xin[b][i] = *reinterpret_cast<const float4*>(a.st.h + (size_t)b * K + kp * KC + i * 256 + lane * 4);
-    } else {
-      ri[b] = a.st.rowinfo[b];
-    }
-  }
-  // 2. the weight stream
-  const TW* __restrict__ W = reinterpret_cast<const TW*>(a.W);
-  typename WReg<TW>::T wr[RPW][NI];
-#pragma unroll
-  for (int r = 0; r < RPW; ++r) {
-    const int n = row0 + r;
-#pragma unroll
-    for (int i = 0; i < NI; ++i)
-      wr[r][i] = WReg<TW>::load(W + (size_t)min(n, a.N - 1) * K + kp * KC + i * 256 + lane * 4);  // clamped, unconditional
-  }
-  // 3. prologue math in registers
-  if (IN == 3) {
-#pragma unroll
-    for (int b = 0; b < BB; ++b) {
-      if (b >= B) continue;
-      float4 (&v)[NI] = xin[b];
-      if (a.emb_row) {  // drop-in row forward: caller's normalised row + wpe[pos]
-        const float* wr_ = a.wpe + (size_t)ri[b].y * D;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const float4 e = *reinterpret_cast<const float4*>(a.emb_row + j * 256 + lane * 4);
-          const float4 pe = *reinterpret_cast<const float4*>(wr_ + j * 256 + lane * 4);
-          v[j] = make_float4(e.x + pe.x, e.y + pe.y, e.z + pe.z, e.w + pe.w);
-        }
-      } else if (ri[b].x < 0) {
-#pragma unroll
-        for (int j = 0; j < 3; ++j) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-      } else {
-        const int p = ri[b].y, prev = ri[b].w;
-        int tok = ri[b].z;
-        if (tok < 0) {
-          if (lane == 0 && blockIdx.x == 0 && wave == 0) atomicOr(a.st.err, 2);
-          tok = 384;
-        }
-        const float* wr_ = a.wpe + (size_t)p * D;
-        float4 pe[3];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) pe[j] = *reinterpret_cast<const float4*>(wr_ + j * 256 + lane * 4);
-        float ss = 0.f;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const int k = j * 256 + lane * 4;
-          if (j == 0) v[j] = *reinterpret_cast<const float4*>(a.text_table + (size_t)tok * TEXT_DIM + k);
-          else if (p == 0) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-          else v[j] = *reinterpret_cast<const float4*>(a.codebook + (size_t)prev * SPEECH_DIM + (k - TEXT_DIM));
-          ss += (v[j].x * v[j].x + v[j].y * v[j].y) + (v[j].z * v[j].z + v[j].w * v[j].w);
-        }
-        const float den = fmaxf(sqrtf(wave_sum(ss)), 1e-8f);  // F.normalize: x / max(||x||_2, eps)
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-          v[j] = make_float4(v[j].x / den + pe[j].x, v[j].y / den + pe[j].y, v[j].z / den + pe[j].z, v[j].w / den + pe[j].w);
-      }
-      if (blockIdx.x == 0 && wave == 0)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = v[j];
-    }
-  }
-  if (IN == 0 || IN == 3) {
-#pragma unroll
-    for (int b = 0; b < BB; ++b)
-      if (b < B) wave_ln_regs(reinterpret_cast<float4 (&)[3]>(xin[b]), g);
-  }
-  // 4. FMA
-  float acc[RPW][BB];
-#pragma unroll
-  for (int r = 0; r < RPW; ++r)
-#pragma unroll
-    for (int b = 0; b < BB; ++b) acc[r][b] = 0.f;
-#pragma unroll
-  for (int i = 0; i < NI; ++i)
-#pragma unroll
-    for (int r = 0; r < RPW; ++r) {
-      const float4 w = WReg<TW>::f(wr[r][i]);
-#pragma unroll
-      for (int b = 0; b < BB; ++b) {
-        if (b >= B) continue;
-        const float4 xv = xin[b][i];
-        acc[r][b] = dot4_fma(acc[r][b], w, xv);
-      }
-    }
-  // 5. reduce (+ combine the K-split waves through LDS)
-#pragma unroll
-  for (int r = 0; r < RPW; ++r)
-#pragma unroll
-    for (int b = 0; b < BB; ++b) {
-      if (b >= B) continue;
-      acc[r][b] = wave_sum(acc[r][b]);
-      if (KW > 1 && lane == 0) part[(wave * RPW + r) * BB + b] = acc[r][b];
-    }
-  if (KW > 1) {
-    __syncthreads();
-    if (kp != 0) return;
-#pragma unroll
-    for (int r = 0; r < RPW; ++r)
-#pragma unroll
-      for (int b = 0; b < BB; ++b) {
-        if (b >= B) continue;
-        float v = 0.f;
-#pragma unroll
-        for (int q = 0; q < KW; ++q) v += part[((rg * KW + q) * RPW + r) * BB + b];
-        acc[r][b] = v;
-      }
-  }
-  // 6. epilogue
-#pragma unroll
-  for (int r = 0; r < RPW; ++r)
-#pragma unroll
-    for (int b = 0; b < BB; ++b) {
-      const int n = row0 + r;
-      if (b >= B || n >= a.N || lane != ((r * BB + b) & 63)) continue;
-      gemv_store<OUT>(a, n, b, acc[r][b]);
-    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -1057,29 +852,11 @@ __global__ void ar_row_state_kernel(ArState st, int slot, int pos) {
 
 // ---------------------------------------------------------------------------------
 // split-KV decode attention (src/model.py:79-95 with T_q = 1, is_causal False, scale 1/sqrt(96)):
-// grid (NSPLIT, 8 heads, B); a block owns a contiguous key range of its (stream, head) and
-// walks it in 64-key tiles staged through LDS with coalesced 16-B loads. Scores: 4 lanes per
-// key (24 dims each); online softmax across tiles; P.V with one thread per (dim, key half).
-// Partials (m, l, o) are merged in the c_proj prologue.
+// grid (splits, 8 heads, B); a block owns a contiguous key range of its (stream, head). Partials
+// (m, l, o) are merged in the c_proj prologue (B <= 2) or the merge kernel; with one split per
+// (row, head) the block writes the normalised head output itself.
 // ---------------------------------------------------------------------------------
-constexpr int ATK = 64;        // keys per tile
-constexpr int KS_LD = HD + 1;  // padded K row: conflict-free 4-lanes-per-key reads
-
-template <typename TKV>
-__device__ __forceinline__ void load_piece8(const TKV* p, float* v);
-template <>
-__device__ __forceinline__ void load_piece8<float>(const float* p, float* v) {
-  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
-  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-}
-template <>
-__device__ __forceinline__ void load_piece8<bf16_t>(const bf16_t* p, float* v) {
-  const uint4 u = *reinterpret_cast<const uint4*>(p);
-  v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
-  v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
-  v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xffff0000u);
-  v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xffff0000u);
-}
+constexpr int ATK = 64;  // keys per split granule
 
 template <typename TKV> struct KvPiece;
 template <> struct KvPiece<float> {
@@ -1113,111 +890,7 @@ template <> struct KvPiece<fp8_t> {
   }
 };
 
-template <typename TKV>
-__global__ __launch_bounds__(256) void ar_attn_kernel(ArState st, int layer) {
-  constexpr int PPT = ATK * (HD / 8) / 256;  // 8-element pieces per thread per tile (3)
-  __shared__ __attribute__((aligned(16))) float qs[HD];
-  __shared__ float Ks[ATK * KS_LD];
-  __shared__ __attribute__((aligned(16))) float Vs[ATK * HD];
-  __shared__ float ps[ATK];
-  __shared__ float red[8];
-  __shared__ float ohalf[HD];
-  const int sp = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int4 ri = st.rowinfo[b];
-  const int s = ri.x;
-  if (s < 0) return;
-  const int t = ri.y + 1;
-  const int ns = min(NSPLIT, (t + ATK - 1) / ATK);
-  if (sp >= ns) return;
-  const int chunk = (t + ns - 1) / ns;
-  const int k0 = sp * chunk, k1 = min(t, k0 + chunk);
-  const size_t base = (((size_t)layer * st.max_streams + s) * N_HEAD + head) * st.max_pos;
-  const TKV* __restrict__ Kg = reinterpret_cast<const TKV*>(st.kc) + base * HD;
-  const TKV* __restrict__ Vg = reinterpret_cast<const TKV*>(st.vc) + base * HD;
-  // register-staged tile pipeline: tile i+1 is loaded while tile i is computed
-  KvPiece<TKV> kp[PPT], vp[PPT];
-  auto issue = [&](int kb) {
-    const int nk = min(ATK, k1 - kb);
-#pragma unroll
-    for (int i = 0; i < PPT; ++i) {
-      const int pc = tid + 256 * i, kk = pc / (HD / 8), d0 = (pc % (HD / 8)) * 8;
-      if (kk < nk) {
-        kp[i].load(Kg + (size_t)(kb + kk) * HD + d0);
-        vp[i].load(Vg + (size_t)(kb + kk) * HD + d0);
-      }
-    }
-  };
-  issue(k0);
-  if (tid < HD) qs[tid] = st.q[(size_t)b * D + head * HD + tid] * 0.10206207261596575f;  // 96 ** -0.5
-  const int key = tid >> 2, part = tid & 3;
-  const int od = tid % HD, oh = tid / HD;  // P.V: thread (dim, key half), tid < 192
-  float m = -INFINITY, l = 0.f, o = 0.f;
-  for (int kb = k0; kb < k1; kb += ATK) {
-    const int nk = min(ATK, k1 - kb);
-    __syncthreads();  // previous tile's LDS reads are done
-#pragma unroll
-    for (int i = 0; i < PPT; ++i) {
-      const int pc = tid + 256 * i, kk = pc / (HD / 8), d0 = (pc % (HD / 8)) * 8;
-      if (kk < nk) {
-        float v[8];
-        kp[i].get(v);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) Ks[kk * KS_LD + d0 + e] = v[e];
-        vp[i].get(v);
-        *reinterpret_cast<float4*>(Vs + kk * HD + d0) = make_float4(v[0], v[1], v[2], v[3]);
-        *reinterpret_cast<float4*>(Vs + kk * HD + d0 + 4) = make_float4(v[4], v[5], v[6], v[7]);
-      }
-    }
-    __syncthreads();
-    if (kb + ATK < k1) issue(kb + ATK);
-    float sc = -INFINITY;
-    {
-      float acc = 0.f;
-      if (key < nk) {
-        const float* kr = Ks + key * KS_LD + part * 24;
-        const float* qr = qs + part * 24;
-#pragma unroll
-        for (int d = 0; d < 24; ++d) acc = fmaf(qr[d], kr[d], acc);
-      }
-      acc += __shfl_xor(acc, 1, 64);
-      acc += __shfl_xor(acc, 2, 64);
-      if (key < nk) sc = acc;
-    }
-    const float wm = wave_max(sc);
-    if (lane == 0) red[wave] = wm;
-    __syncthreads();
-    const float mt = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    const float mn = fmaxf(m, mt);
-    const float alpha = (m == -INFINITY) ? 0.f : expf(m - mn);
-    const float p = (key < nk) ? expf(sc - mn) : 0.f;
-    if (part == 0) ps[key] = p;
-    const float wsum = wave_sum(part == 0 ? p : 0.f);
-    if (lane == 0) red[4 + wave] = wsum;
-    __syncthreads();  // ps and the tile sums are visible
-    if (tid < 2 * HD) {
-      float acc = 0.f;
-      const int j0 = oh * (ATK / 2), j1 = min(nk, j0 + ATK / 2);
-      for (int j = j0; j < j1; ++j) acc = fmaf(ps[j], Vs[j * HD + od], acc);
-      o = o * alpha + acc;
-    }
-    l = l * alpha + ((red[4] + red[5]) + (red[6] + red[7]));
-    m = mn;
-  }
-  if (tid >= HD && tid < 2 * HD) ohalf[od] = o;
-  __syncthreads();
-  if (tid < HD) {
-    float* po = st.part_o + ((size_t)(b * N_HEAD + head) * NSPLIT + sp) * HD;
-    po[tid] = o + ohalf[tid];
-  }
-  if (tid == 0) {
-    float* ml = st.part_ml + ((size_t)(b * N_HEAD + head) * NSPLIT + sp) * 2;
-    ml[0] = m;
-    ml[1] = l;
-  }
-}
-
-// Variant 2 (option "attn_v2"): no LDS in the key loop. A block walks its key range in 64-key
+// No LDS in the key loop: a block walks its key range in 64-key
 // tiles; lane quad (tid/4) owns one key per tile and lane tid%4 owns 24 of its 96 dims: the K and
 // V pieces (48 B bf16 each) load straight to registers, the score needs two quad shuffles, and
 // every wave keeps its own online-softmax state (m, l, o[24] per lane) so the loop has no
@@ -1402,36 +1075,28 @@ __global__ __launch_bounds__(256) void ar_argmax_kernel(ArState st) {
 // ---------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------
-int g_opt_gemv_reg = 0;  // runtime A/B switches (lvx_set_option); measured: LDS path faster at B=1
-int g_opt_b1_splits = 16;  // B = 1 attention splits per head (8 or 16; c_proj merges that many);
-// measured (us/step at t < 256 / t = 768-1023): 16: 86.9 / 89.3, 8: 85.1 / 90.3 -- a wash over an utterance
-int g_opt_attn_v2 = 1;
-int g_opt_cproj_b1 = 1;
-int g_opt_prefetch_in = 1;
-int g_opt_fuse_argmax = 0;  // measured at B = 1: the in-launch tail costs more than the boundary it saves
-int g_opt_defer_select = 1;  // B <= 2: greedy select in the next step's c_attn layer 0 (no argmax kernel)
-int g_opt_fuse_mlp = 1;
+// Kernel-variant switches kept for cross-checks (lvx_set_option): each selects between two correct
+// implementations of the same step that tests/ compare (defaults are the measured-faster ones).
+int g_opt_defer_select = 1;  // 1: greedy select deferred into the next step's first kernel (B <= 2: c_attn
+                             // layer 0 reduces lm_head's granules; B >= 4: ar_embed_select); 0: ar_argmax_kernel
+int g_opt_fuse_mlp = 1;      // bf16, B <= 2: c_fc + gelu + mlp c_proj in one kernel (fp32 atomics, arrival
+                             // order); 0: two deterministic GEMV kernels
 
 template <typename TW, int K, int KW, int RPW, int IN, int OUT>
 static void launch_gemv(const GemvArgs& a, hipStream_t s) {
   const int rows_per_block = (4 / KW) * RPW;
   dim3 grid((a.N + rows_per_block - 1) / rows_per_block);
   constexpr int BGMAX = (K == 768) ? 16 : 4;
-  if constexpr (OUT == 4 || OUT == 9 || IN == 5) {  // select variants: one batch group of <= 4 rows (launch_op checks)
+  if constexpr (OUT == 9 || IN == 5) {  // select variants: one batch group of <= 4 rows (launch_op checks)
     if (a.B <= 1) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 1, IN, OUT>), grid, dim3(256), 0, s, a);
     else if (a.B <= 2) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 2, IN, OUT>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 4, IN, OUT>), grid, dim3(256), 0, s, a);
   } else {
     if constexpr (IN == 2 && OUT == 1 && K == 768 && KW == 1) {
-      if (g_opt_cproj_b1 && a.B == 1) {
-        if (g_opt_b1_splits <= 8) hipLaunchKernelGGL((ar_cproj_b1_kernel<TW, RPW, 8>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((ar_cproj_b1_kernel<TW, RPW, NSPLIT>), grid, dim3(256), 0, s, a);
+      if (a.B == 1) {  // B = 1 c_proj: the split merge once per block, 16 splits
+        hipLaunchKernelGGL((ar_cproj_b1_kernel<TW, RPW, NSPLIT>), grid, dim3(256), 0, s, a);
         return;
       }
-    }
-    if constexpr (IN != 2) {
-      if (g_opt_gemv_reg && a.B <= 1) { hipLaunchKernelGGL((ar_gemv_reg_kernel<TW, K, KW, RPW, 1, IN, OUT>), grid, dim3(256), 0, s, a); return; }
-      if (g_opt_gemv_reg && a.B <= 4) { hipLaunchKernelGGL((ar_gemv_reg_kernel<TW, K, KW, RPW, 4, IN, OUT>), grid, dim3(256), 0, s, a); return; }
     }
     if (a.B <= 1) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 1, IN, OUT>), grid, dim3(256), 0, s, a);
     else if (a.B <= 2) hipLaunchKernelGGL((ar_gemv_kernel<TW, K, KW, RPW, 2, IN, OUT>), grid, dim3(256), 0, s, a);
@@ -1449,10 +1114,10 @@ __device__ __forceinline__ uint2 pack4_bf16(float4 v) {
                     (uint32_t)f32_to_bf16(v.z) | ((uint32_t)f32_to_bf16(v.w) << 16));
 }
 
-int g_opt_mfma_batch = 3;  // smallest B on the batched MFMA path (0: off); measured B = 3: 117 vs 154 us, B = 2: 119 vs 114
+constexpr int MFMA_BATCH_MIN = 3;  // smallest B on the batched MFMA path (measured B = 3: 117 vs 154 us, B = 2: 119 vs 114)
 // batched path: LayerNorm / embedding fused into the MFMA GEMM prologue for B <= this value
 // (measured: B = 8 147 vs 156 us/step; B = 32 slower, every block re-normalising 32 rows)
-int g_opt_mfma_ln = 8;
+constexpr int MFMA_LN_MAX = 8;
 
 // ---------------------------------------------------------------------------------
 // Batched path v2 (bf16 weights, 4 < B <= 32): every per-row prologue runs ONCE per row into a
@@ -1645,7 +1310,7 @@ template <int K, int NT, int OUT, int KTOT = K, int XM = 0>
 __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   constexpr int NW = K / 192;  // waves per block, each a 192-wide K slice (6 MFMA k-steps)
   __shared__ float red[NW][NT * 256];
-  __shared__ float xo[(OUT == 7 || OUT == 8) ? 16 * NT * 16 : 1];
+  __shared__ float xo[OUT == 7 ? 16 * NT * 16 : 1];
   __shared__ float2 rs[XM == 1 ? NT * 16 : 1];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int n0 = blockIdx.x * 16;
@@ -1779,47 +1444,11 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
       a.st.x[(size_t)b * D + n] = xn;
       a.st.xb[(size_t)b * D + n] = f32_to_bf16(xn);
       xo[e] = xn;
-    } else if (OUT == 8) {  // K-slice slab of the split mlp c_proj (reduced by the tile's last arriver):
-      // write-through (sc1) store, so the hand-off needs no release fence (cdna_hip_programming.md
-      // Guideline 16 R1)
-      __hip_atomic_store((gu32*)(a.yacc + ((size_t)b * YCOPIES + blockIdx.y) * D + n),
-                         __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       gemv_store<OUT>(a, n, b, v);
     }
   }
-  if constexpr (OUT == 8) {
-    // In-launch split-K combine (cdna_hip_programming.md, "Projection GEMM at M = 256" item 2, the
-    // Guideline 16 counter form with write-through slabs): every wave drains its sc1 slab stores,
-    // barrier, one relaxed agent ticket per block; the tile's last arriving slice reads the slabs
-    // with sc1 loads (no acquire fence, R1), sums them in slice order (deterministic), adds the
-    // residual and leaves final x + its bf16 copy + the column statistics, so the next LayerNorm
-    // needs no rows kernel. x of this tile's columns is written only by this block in the launch.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      const unsigned tk = __hip_atomic_fetch_add((gu32*)(a.st.tick + blockIdx.x), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const bool last = tk == gridDim.y - 1;
-      if (last) __hip_atomic_store((gu32*)(a.st.tick + blockIdx.x), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      red[0][0] = last ? 1.f : 0.f;
-    }
-    __syncthreads();
-    if (red[0][0] == 0.f) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below here
-    for (int e = tid; e < 16 * NT * 16; e += NW * 64) {
-      const int r = e / (NT * 16), b = r0 + e - r * (NT * 16), n = n0 + r;
-      if (b >= B) continue;
-      float t = a.st.x[(size_t)b * D + n];
-#pragma unroll
-      for (int c = 0; c < YCOPIES; ++c)
-        t += __uint_as_float(__hip_atomic_load((gu32*)(a.yacc + ((size_t)b * YCOPIES + c) * D + n),
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      a.st.x[(size_t)b * D + n] = t;
-      a.st.xb[(size_t)b * D + n] = f32_to_bf16(t);
-      xo[e] = t;
-    }
-  }
-  if constexpr (OUT == 7 || OUT == 8) {  // (mean, M2) of this block's 16 columns for every batch row
+  if constexpr (OUT == 7) {  // (mean, M2) of this block's 16 columns for every batch row
     __syncthreads();
     if (tid < NT * 16 && r0 + tid < B) {
       float mean = 0.f;
@@ -1837,29 +1466,18 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   }
 }
 
-int g_opt_mfma_btile = 0;  // B > 16: batch tiles of 16 rows in grid.z instead of NT = 2 / 4 per block;
-                           // measured slower (B = 32 t = 256+: 144.6 vs 142.2 us/step, B = 24: 132.4
-                           // vs 129.6): twice the blocks each re-read the weights
-
+// measured alternatives to the batched v2 layout (round 1/2, us/step at B = 32, t = 256-512), removed:
+// 16-row batch tiles in grid.z (twice the blocks re-read the weights: 144.6 vs 142.2); LayerNorm of
+// c_attn / lm_head from an unsplit mlp c_proj's row statistics (48 blocks of 16 waves: 178 vs 156);
+// the split mlp c_proj combined in-launch by each column tile's last arriving slice (release /
+// acquire fences: 182 vs 157; write-through slabs and sc1 loads, no fences: 171.9 vs 162-168)
 template <int K, int OUT, int XM = 0>
 static void launch_mfma2(const GemvArgs& a, hipStream_t s) {
   dim3 grid((a.N + 15) / 16), block((K / 192) * 64);
-  if (g_opt_mfma_btile && a.B > 16 && OUT != 8) {  // 16-row batch tiles: half / quarter the bytes per block
-    grid.z = (a.B + 15) / 16;
-    hipLaunchKernelGGL((ar_mfma2_kernel<K, 1, OUT, K, XM>), grid, block, 0, s, a);
-    return;
-  }
   if (a.B <= 16) hipLaunchKernelGGL((ar_mfma2_kernel<K, 1, OUT, K, XM>), grid, block, 0, s, a);
   else if (a.B <= 32) hipLaunchKernelGGL((ar_mfma2_kernel<K, 2, OUT, K, XM>), grid, block, 0, s, a);
   else hipLaunchKernelGGL((ar_mfma2_kernel<K, 4, OUT, K, XM>), grid, block, 0, s, a);
 }
-// batched v2: 1 = c_fc normalises from c_proj's row statistics (no rows kernel before c_fc);
-// 2 = also c_attn / lm_head from an unsplit mlp c_proj's statistics (no rows kernels at all):
-// measured slower (B = 32: 178 vs 156 us/step, B = 16: 144 vs 134): the unsplit K = 3072 GEMM (48
-// blocks of 16 waves) costs more than the two rows kernels it removes; 3 = the split mlp c_proj
-// with an in-launch combine by each column tile's last arriving slice (agent release / ticket /
-// acquire) leaving the statistics: also slower (B = 32: 182 vs 157, B = 16: 146 vs 137)
-int g_opt_ln_stats = 1;
 
 // mlp c_proj (K = 3072) split into YCOPIES K slices of 768: 4x the blocks of the unsplit GEMM;
 // each slice's partial goes to its pending copy (plain stores, deterministic), folded into x by
@@ -1868,11 +1486,6 @@ template <int OUT>
 static void launch_mproj_split(const GemvArgs& a, hipStream_t s) {
   static_assert(DFF == YCOPIES * 768, "one pending copy per K slice");
   dim3 grid((a.N + 15) / 16, YCOPIES), block(256);
-  if (g_opt_mfma_btile && a.B > 16 && OUT != 8) {
-    grid.z = (a.B + 15) / 16;
-    hipLaunchKernelGGL((ar_mfma2_kernel<768, 1, OUT, DFF>), grid, block, 0, s, a);
-    return;
-  }
   if (a.B <= 16) hipLaunchKernelGGL((ar_mfma2_kernel<768, 1, OUT, DFF>), grid, block, 0, s, a);
   else if (a.B <= 32) hipLaunchKernelGGL((ar_mfma2_kernel<768, 2, OUT, DFF>), grid, block, 0, s, a);
   else hipLaunchKernelGGL((ar_mfma2_kernel<768, 4, OUT, DFF>), grid, block, 0, s, a);
@@ -1991,7 +1604,7 @@ static void launch_mfma_ln(const GemvArgs& a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------------
-// Batched path v3 (bf16 weights, g_opt_mfma_batch <= B <= 64; option "bt"): five kernels per
+// Batched path v3 (bf16 weights, MFMA_BATCH_MIN <= B <= 64; option "bt"): five kernels per
 // layer and no pending partials, so every x row is final at each kernel boundary:
 //   c_attn       LN1(x) prologue (layer 0: embedding, which also stores x), q / KV-append epilogue
 //   attention    split-KV ar_attn_v2
@@ -2004,14 +1617,13 @@ static void launch_mfma_ln(const GemvArgs& a, hipStream_t s) {
 // partial 16 x R tiles are summed through LDS in fixed order (deterministic, equal rows bit-equal).
 // ---------------------------------------------------------------------------------
 template <int K, int NT, int IN, int OUT>
-__global__ __launch_bounds__(K / 192 * 64) void ar_bt_kernel(GemvArgs a, int ns_max) {
+__global__ __launch_bounds__(K / 192 * 64) void ar_bt_kernel(GemvArgs a) {
   constexpr int NW = K / 192, R = NT * 16, NTH = NW * 64;
   constexpr bool STAGE = IN != 1;  // operand tile staged in LDS (K == 768)
   static_assert(!STAGE || K == 768, "the LDS operand tile holds K = 768 rows");
   constexpr int LDX = D + 8;  // bf16 row stride of the tile (16-B pad)
   __shared__ __attribute__((aligned(16))) bf16_t xs[STAGE ? R * LDX : 8];
   __shared__ float red[NW][16 * R];
-  __shared__ float cf[IN == 2 ? R * N_HEAD * NSPLIT : 1];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int n0 = blockIdx.x * 16, r0 = blockIdx.y * R;
   const int B = a.B;
@@ -2064,57 +1676,6 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_bt_kernel(GemvArgs a, int ns_
         }
       }
     }
-  } else if constexpr (IN == 2) {
-    // split-KV merge: y = sum_s c_s o_s, c_s = e^{m_s - M} / sum_s' e^{m_s' - M} l_s'
-    // phase A: one thread per (row, head) -> coefficients (zero for unused splits)
-#pragma unroll
-    for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(W + (size_t)wrow * K + k0 + kk * 32);
-    for (int qa = tid; qa < R * N_HEAD; qa += NTH) {
-      const int b = r0 + qa / N_HEAD, head = qa % N_HEAD;
-      float* c = cf + qa * NSPLIT;
-      if (b >= B) {
-#pragma unroll
-        for (int i = 0; i < NSPLIT; ++i) c[i] = 0.f;
-        continue;
-      }
-      const int4 ri = a.st.rowinfo[b];
-      const float2* mlp = reinterpret_cast<const float2*>(a.st.part_ml) + (size_t)(b * N_HEAD + head) * NSPLIT;
-      float2 ml[NSPLIT];
-#pragma unroll
-      for (int i = 0; i < NSPLIT; ++i) ml[i] = i < ns_max ? mlp[i] : make_float2(-INFINITY, 0.f);
-      const int ns = ri.x < 0 ? 0 : min(ns_max, (ri.y + 1 + 63) / 64);
-      float M = -INFINITY;
-#pragma unroll
-      for (int i = 0; i < NSPLIT; ++i) if (i < ns) M = fmaxf(M, ml[i].x);
-      float den = 0.f, f[NSPLIT];
-#pragma unroll
-      for (int i = 0; i < NSPLIT; ++i) {
-        f[i] = (i < ns && ml[i].x != -INFINITY) ? expf(ml[i].x - M) : 0.f;
-        den += f[i] * ml[i].y;
-      }
-      const float inv = ns ? 1.0f / den : 0.f;
-#pragma unroll
-      for (int i = 0; i < NSPLIT; ++i) c[i] = f[i] * inv;
-    }
-    __syncthreads();
-    // phase B: (row, 4-element group) pairs, every used split summed (part_o holds finite values)
-    for (int e = tid; e < R * (D / 4); e += NTH) {
-      const int rr = e / (D / 4), c4 = (e - rr * (D / 4)) * 4, b = r0 + rr;
-      uint2* dst = reinterpret_cast<uint2*>(xs + rr * LDX + c4);
-      if (b >= B) { *dst = make_uint2(0u, 0u); continue; }
-      const int head = c4 / HD, d = c4 - head * HD;
-      const float* po = a.st.part_o + ((size_t)(b * N_HEAD + head) * NSPLIT) * HD + d;
-      const float* c = cf + (rr * N_HEAD + head) * NSPLIT;
-      float4 y = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int i = 0; i < NSPLIT; ++i) {
-        if (i < ns_max) {
-          const float4 p = *reinterpret_cast<const float4*>(po + (size_t)i * HD);
-          y.x += c[i] * p.x; y.y += c[i] * p.y; y.z += c[i] * p.z; y.w += c[i] * p.w;
-        }
-      }
-      *dst = pack4_bf16(y);
-    }
   } else {  // IN 1: bf16 operand rows (hb, or xn of the separate merge kernel) straight from global
 #pragma unroll
     for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(W + (size_t)wrow * K + k0 + kk * 32);
@@ -2161,75 +1722,47 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_bt_kernel(GemvArgs a, int ns_
 // time of these short GEMMs: B = 8 / 16 / 32 v2 149 / 162 / 191 vs v3 172 / 181 / 203 (16-row
 // tiles, separate merge); a fused merge re-reads ns_max partials per row and block: 271 / 302 / 266.
 // v3 therefore runs only where v2 has no kernels (32 < B <= 64: 250 us, 16-row tiles).
-int g_opt_bt = 1;        // 0: off; 1: batched path v3 for 32 < B <= 64; 2: v3 for every batched B
-int g_opt_bt_rows = 16;  // batch rows per block (16 / 32 / 64)
-int g_opt_bt_merge = 0;  // split-KV merge in the c_proj prologue (0: separate ar_merge_bf16 kernel)
+int g_opt_bt = 1;  // 1: batched path v3 for 32 < B <= 64; 2: v3 for every batched B (cross-check of v2); 0: off
 
 template <int K, int IN, int OUT>
-static void launch_bt(const GemvArgs& a, int ns_max, hipStream_t s) {
-  const int R = g_opt_bt_rows <= 16 ? 16 : (g_opt_bt_rows <= 32 ? 32 : 64);
-  const int Bp = (a.B + 15) / 16 * 16;
-  const int NT = (R < Bp ? R : Bp) / 16;
-  dim3 grid((a.N + 15) / 16, (a.B + NT * 16 - 1) / (NT * 16)), block(K / 192 * 64);
-  if (NT == 1) hipLaunchKernelGGL((ar_bt_kernel<K, 1, IN, OUT>), grid, block, 0, s, a, ns_max);
-  else if (NT == 2) hipLaunchKernelGGL((ar_bt_kernel<K, 2, IN, OUT>), grid, block, 0, s, a, ns_max);
-  else if (NT == 3) hipLaunchKernelGGL((ar_bt_kernel<K, 3, IN, OUT>), grid, block, 0, s, a, ns_max);
-  else hipLaunchKernelGGL((ar_bt_kernel<K, 4, IN, OUT>), grid, block, 0, s, a, ns_max);
+static void launch_bt(const GemvArgs& a, hipStream_t s) {
+  // 16 batch rows per block (32 / 64 measured slower: fewer blocks, more bytes each)
+  dim3 grid((a.N + 15) / 16, (a.B + 15) / 16), block(K / 192 * 64);
+  hipLaunchKernelGGL((ar_bt_kernel<K, 1, IN, OUT>), grid, block, 0, s, a);
 }
 
-int g_opt_attn_waves = 4;  // waves per attention block for B > 2 (4, or 8: 128-key tiles). us/step
-                           // 4 / 8 waves: B = 32 t = 256+ 149.4 / 153.7; B = 64 209.0 / 211.1;
-                           // B = 16 t = 1024+ 152.4 / 156.4; B = 8 t = 512+ 121.9 / 123.9
-int g_opt_attn_depth = 2;  // KV tiles in flight per attention block for B > 2 (2, or 4 for whole
-                           // groups of tiles). us/step (tools/step_sweep.py) depth 2 / 4, after the DPP
-                           // reductions: B = 32, t = 256+: 152.0 / 157.9; B = 64: 216.3 / 234.2 (with
-                           // the ds_bpermute reductions depth 4 had won: 173.5 / 167.9, 248.8 / 242.4)
-int g_opt_attn_blocks = 256;  // split count target: ns * 8 heads * B <= this (batched paths); measured
-// (tools/step_sweep.py, us/step at t = 256-511): B = 32: 1024 -> 164, 512 -> 169, 256 (one split:
-// the attention writes xn directly, no merge kernel) -> 155.5; B = 16: 138 / 136 / 131 (128 blocks);
-// B = 8: 144 / 133 / 130
+// Attention launch shape, measured (tools/step_sweep.py, us/step): 4 waves per block (8 waves,
+// 128-key tiles: B = 32 t = 256+ 153.7 vs 149.4; B = 64 211.1 vs 209.0), 2 KV tiles in flight per
+// wave (4: B = 32 157.9 vs 152.0, B = 64 234.2 vs 216.3), splits until ns x 8 heads x B <= 256
+// blocks (B = 32 at t = 256-511: 1024 blocks 164, 512 169, 256 = one split that writes xn
+// itself 155.5; B = 16: 138 / 136 / 131; B = 8: 144 / 133 / 130).
+constexpr int ATTN_BLOCKS = 256;
 static int attn_ns_max(int B) {  // enough splits to fill the chip, no more (early-exit blocks cost)
   int ns = NSPLIT;
-  while (ns > 1 && ns * N_HEAD * B > g_opt_attn_blocks) ns >>= 1;
+  while (ns > 1 && ns * N_HEAD * B > ATTN_BLOCKS) ns >>= 1;
   return ns;
 }
 
 static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_t s, int ns_max = NSPLIT,
                         int direct = 0, int selcopy = 0) {
-  if (g_opt_attn_v2 || kvdtype == LVX_DTYPE_FP8 || direct || selcopy) {
-    dim3 grid(ns_max, N_HEAD, B);
-    const bool deep = g_opt_attn_depth >= 4 && B > 2;  // B <= 2: ~1 tile per split at t <= 1024
-    const bool wide = g_opt_attn_waves >= 8 && B > 2;   // 8 waves (128-key tiles) per block
-    const dim3 blk(wide ? 512 : 256);
-#define LVX_ATTN(T)                                                                                       \
-    do {                                                                                                  \
-      if (wide) hipLaunchKernelGGL((ar_attn_v2_kernel<T, 2, 8>), grid, blk, 0, s, st, l, ns_max, direct, selcopy); \
-      else if (deep) hipLaunchKernelGGL((ar_attn_v2_kernel<T, 4, 4>), grid, blk, 0, s, st, l, ns_max, direct, selcopy); \
-      else hipLaunchKernelGGL((ar_attn_v2_kernel<T, 2, 4>), grid, blk, 0, s, st, l, ns_max, direct, selcopy); \
-    } while (0)
-    if (kvdtype == LVX_DTYPE_BF16) LVX_ATTN(bf16_t);
-    else if (kvdtype == LVX_DTYPE_FP8) LVX_ATTN(fp8_t);
-    else LVX_ATTN(float);
-#undef LVX_ATTN
-  } else {
-    dim3 grid(NSPLIT, N_HEAD, B);
-    if (kvdtype == LVX_DTYPE_BF16) hipLaunchKernelGGL((ar_attn_kernel<bf16_t>), grid, dim3(256), 0, s, st, l);
-    else hipLaunchKernelGGL((ar_attn_kernel<float>), grid, dim3(256), 0, s, st, l);
-  }
+  dim3 grid(ns_max, N_HEAD, B);
+  if (kvdtype == LVX_DTYPE_BF16)
+    hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2, 4>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
+  else if (kvdtype == LVX_DTYPE_FP8)
+    hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t, 2, 4>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
+  else
+    hipLaunchKernelGGL((ar_attn_v2_kernel<float, 2, 4>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
 }
 
 // one op of the decode step, with the B-dependent kernel choice (shared by the step and the probes)
 // op: 0 c_attn (layer 0: + embedding) 1 attention 2 c_proj (+ split merge) 3 c_fc 4 mlp c_proj 5 lm_head
-// fused lm_head + greedy select (B <= 4 GEMV path, fused step only); returns whether op 5 did the select
-template <typename TW>
-static bool use_bt(int B) {
-  return sizeof(TW) == 2 && g_opt_bt && g_opt_mfma_batch && B >= g_opt_mfma_batch && B <= 64 &&
-         (B > 32 || g_opt_bt == 2);
-}
-
 template <typename TW>
 static bool use_mfma(int B) {
-  return sizeof(TW) == 2 && g_opt_mfma_batch && B >= g_opt_mfma_batch && B <= 64;
+  return sizeof(TW) == 2 && B >= MFMA_BATCH_MIN && B <= 64;
+}
+template <typename TW>
+static bool use_bt(int B) {
+  return use_mfma<TW>(B) && g_opt_bt && (B > 32 || g_opt_bt == 2);
 }
 
 // batched path v3: one kernel per op (plus the attention), final x rows at every boundary
@@ -2243,33 +1776,23 @@ static void launch_op_bt(int op, GemvArgs& a, const ArWeights& w, int l, int kvd
       a.W = w.w_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
       if (l == 0 && a.defer_sel == 2) {  // embedding + the previous step's select, then c_attn
         hipLaunchKernelGGL(ar_embed_select_kernel, dim3(B), dim3(256), 0, s, a);
-        launch_bt<768, 1, 0>(a, 0, s);
+        launch_bt<768, 1, 0>(a, s);
       } else if (l == 0) {
-        launch_bt<768, 3, 0>(a, 0, s);
+        launch_bt<768, 3, 0>(a, s);
       } else {
-        launch_bt<768, 0, 0>(a, 0, s);
+        launch_bt<768, 0, 0>(a, s);
       }
       break;
     case 1: launch_attn(a.st, kvdtype, B, l, s, nsm); break;
     case 2:
       a.W = w.w_aproj[l]; a.N = D;
-      if (g_opt_bt_merge) {
-        launch_bt<768, 2, 1>(a, nsm, s);
-      } else {
-        launch_merge_bf16(a.st, B, nsm, s);
-        launch_bt<768, 1, 1>(a, 0, s);
-      }
+      launch_merge_bf16(a.st, B, nsm, s);
+      launch_bt<768, 1, 1>(a, s);
       break;
-    case 3: a.W = w.w_fc[l]; a.N = DFF; a.ln_w = w.ln2[l]; launch_bt<768, 0, 5>(a, 0, s); break;
-    case 4: a.W = w.w_mproj[l]; a.N = D; launch_bt<3072, 1, 1>(a, 0, s); break;
-    case 5: a.W = w.w_lm; a.N = VOCAB; a.ln_w = w.lnf; launch_bt<768, 0, 3>(a, 0, s); break;
+    case 3: a.W = w.w_fc[l]; a.N = DFF; a.ln_w = w.ln2[l]; launch_bt<768, 0, 5>(a, s); break;
+    case 4: a.W = w.w_mproj[l]; a.N = D; launch_bt<3072, 1, 1>(a, s); break;
+    case 5: a.W = w.w_lm; a.N = VOCAB; a.ln_w = w.lnf; launch_bt<768, 0, 3>(a, s); break;
   }
-}
-
-template <typename TW>
-static bool fused_select(int B) {
-  static_assert(VOCAB / 8 <= 512 && VOCAB / 8 <= LM_MAX_BLOCKS, "fused select: lm_head grid must fit the tail");
-  return g_opt_fuse_argmax && B <= 4 && !use_mfma<TW>(B);
 }
 
 // deferred select: every row of the step is prefetched by its own wave of c_attn layer 0 (B <= 2,
@@ -2277,17 +1800,18 @@ static bool fused_select(int B) {
 template <typename TW>
 static bool defer_select(int B) {
   static_assert(LM_SEL_BLOCKS <= LM_MAX_BLOCKS && LM_SEL_BLOCKS % 64 == 0, "deferred select granules");
-  return g_opt_defer_select && g_opt_prefetch_in && B <= 2 && !use_mfma<TW>(B) && !use_bt<TW>(B) &&
-         !fused_select<TW>(B);
+  return g_opt_defer_select && B <= 2 && !use_mfma<TW>(B);
 }
 template <typename TW>
 static bool defer_select_batched(int B) {
-  // us/step (tools/step_sweep.py, t = 256+) argmax kernel / deferred: B = 3: 112.9 / 114.7 (left on
-  // the argmax kernel unless defer_select = 2), B = 4: 106.0 / 104.9, 8: 120.7 / 118.3,
-  // 12: 123.0 / 120.5, 16: 128.4 / 125.5, 32: 150.3 / 147.3, 64: 213.4 / 206.8
-  return g_opt_defer_select && ((use_mfma<TW>(B) && (B >= 4 || g_opt_defer_select >= 2)) || use_bt<TW>(B));
+  // us/step (tools/step_sweep.py, t = 256+) argmax kernel / deferred: B = 3: 112.9 / 114.7 (B = 3
+  // keeps the argmax kernel), B = 4: 106.0 / 104.9, 8: 120.7 / 118.3, 12: 123.0 / 120.5,
+  // 16: 128.4 / 125.5, 32: 150.3 / 147.3, 64: 213.4 / 206.8
+  return g_opt_defer_select && ((use_mfma<TW>(B) && B >= 4) || use_bt<TW>(B));
 }
 
+// measured at B = 1 (round 1): 16 h rows per block (192 blocks) 76.7 us/step; 32 rows (96 blocks)
+// +6.8 us; 12 rows (256 blocks, one per CU) 77.4 us; 8 accumulator copies slower than 4
 template <typename TW>
 static bool fused_mlp(int B) {
   return sizeof(TW) == 2 && g_opt_fuse_mlp && B <= 2 && !use_mfma<TW>(B);
@@ -2295,15 +1819,14 @@ static bool fused_mlp(int B) {
 
 // returns false when the op has no kernel of its own at this B (mlp c_proj inside the fused MLP)
 template <typename TW>
-static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtype, int B, hipStream_t s,
-                      bool select = false) {
+static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtype, int B, hipStream_t s) {
   if (use_bt<TW>(B) && !a.emb_row) {
     launch_op_bt(op, a, w, l, kvdtype, B, s);
     return true;
   }
   const bool mf = use_mfma<TW>(B);
   const bool fm = fused_mlp<TW>(B);
-  const int nsm = mf ? attn_ns_max(B) : (B == 1 && g_opt_cproj_b1 && g_opt_b1_splits <= 8 ? 8 : NSPLIT);
+  const int nsm = mf ? attn_ns_max(B) : NSPLIT;
   a.layer = l;
   a.yacc = (fm || mf) ? a.st.yacc : nullptr;
   a.add_y = l > 0;
@@ -2313,12 +1836,10 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       if (mf && l == 0 && a.defer_sel == 2) {  // embedding + the previous step's select, then c_attn
         hipLaunchKernelGGL(ar_embed_select_kernel, dim3(B), dim3(256), 0, s, a);
         launch_mfma2<768, 0>(a, s);
-      } else if (mf && B <= g_opt_mfma_ln) {
+      } else if (mf && B <= MFMA_LN_MAX) {
         if (l == 0) launch_mfma_ln<0, 3>(a, s);
         else launch_mfma_ln<0, 4>(a, s);
-      } else if (mf && l > 0 && g_opt_ln_stats >= 2) {
-        launch_mfma2<768, 0, 1>(a, s);  // LN1 from the previous mlp c_proj's statistics
-      } else if (mf) {
+      } else if (mf) {  // rows kernel: LayerNorm (layer 0: of the embedding; else of x + the MLP copies)
         if (l == 0) hipLaunchKernelGGL((ar_rows_kernel<3>), dim3(B), dim3(64), 0, s, a);
         else hipLaunchKernelGGL((ar_rows_kernel<4>), dim3(B), dim3(64), 0, s, a);
         launch_mfma2<768, 0>(a, s);
@@ -2336,9 +1857,9 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
     case 2:
       a.W = w.w_aproj[l]; a.N = D;
       if (mf) {
-        if (B > g_opt_mfma_ln) a.add_y = 0;  // ar_rows_kernel<4> of this layer's c_attn folded them
+        if (B > MFMA_LN_MAX) a.add_y = 0;  // ar_rows_kernel<4> of this layer's c_attn folded them
         if (nsm > 1) launch_merge_bf16(a.st, B, nsm, s);  // nsm == 1: the attention wrote xn itself
-        if (B > g_opt_mfma_ln && g_opt_ln_stats) launch_mfma2<768, 7>(a, s);  // + bf16 x and row stats
+        if (B > MFMA_LN_MAX) launch_mfma2<768, 7>(a, s);  // + bf16 x and row statistics for c_fc
         else launch_mfma2<768, 1>(a, s);
       } else {
         launch_gemv<TW, 768, 1, 1, 2, 1>(a, s);
@@ -2346,26 +1867,15 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       break;
     case 3:
       a.W = w.w_fc[l]; a.N = DFF; a.ln_w = w.ln2[l];
-      if (fm) {
+      if (fm) {  // 16 h rows per block (192 blocks)
         const bf16_t* wfc = reinterpret_cast<const bf16_t*>(w.w_fc[l]);
         const bf16_t* wpk = reinterpret_cast<const bf16_t*>(w.w_mproj_pk[l]);
-        if (g_opt_fuse_mlp == 2) {  // 32 h rows per block (96 blocks)
-          if (B <= 1) hipLaunchKernelGGL((ar_mlp_fused_kernel<1, 32>), dim3(DFF / 32), dim3(256), 0, s, a, wfc, wpk);
-          else hipLaunchKernelGGL((ar_mlp_fused_kernel<2, 32>), dim3(DFF / 32), dim3(256), 0, s, a, wfc, wpk);
-        } else if (g_opt_fuse_mlp == 3) {  // 12 h rows per block (256 blocks: one per CU)
-          if (B <= 1) hipLaunchKernelGGL((ar_mlp_fused_kernel<1, 12>), dim3(DFF / 12), dim3(256), 0, s, a, wfc, wpk);
-          else hipLaunchKernelGGL((ar_mlp_fused_kernel<2, 12>), dim3(DFF / 12), dim3(256), 0, s, a, wfc, wpk);
-        } else {  // 16 h rows per block (192 blocks)
-          if (B <= 1) hipLaunchKernelGGL((ar_mlp_fused_kernel<1, 16>), dim3(DFF / 16), dim3(256), 0, s, a, wfc, wpk);
-          else hipLaunchKernelGGL((ar_mlp_fused_kernel<2, 16>), dim3(DFF / 16), dim3(256), 0, s, a, wfc, wpk);
-        }
-      } else if (mf && B <= g_opt_mfma_ln) {
+        if (B <= 1) hipLaunchKernelGGL((ar_mlp_fused_kernel<1, 16>), dim3(DFF / 16), dim3(256), 0, s, a, wfc, wpk);
+        else hipLaunchKernelGGL((ar_mlp_fused_kernel<2, 16>), dim3(DFF / 16), dim3(256), 0, s, a, wfc, wpk);
+      } else if (mf && B <= MFMA_LN_MAX) {
         launch_mfma_ln<5, 0>(a, s);
-      } else if (mf && g_opt_ln_stats) {
-        launch_mfma2<768, 5, 1>(a, s);  // LayerNorm from c_proj's statistics in the prologue
       } else if (mf) {
-        hipLaunchKernelGGL((ar_rows_kernel<0>), dim3(B), dim3(64), 0, s, a);
-        launch_mfma2<768, 5>(a, s);
+        launch_mfma2<768, 5, 1>(a, s);  // LayerNorm from c_proj's row statistics in the prologue
       } else {
         launch_gemv<TW, 768, 1, 2, 0, 2>(a, s);
       }
@@ -2373,26 +1883,19 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
     case 4:
       a.W = w.w_mproj[l]; a.N = D;
       if (fm) return false;
-      if (mf && B > g_opt_mfma_ln && g_opt_ln_stats == 2) launch_mfma2<DFF, 7>(a, s);  // final x + stats
-      else if (mf && B > g_opt_mfma_ln && g_opt_ln_stats == 3) launch_mproj_split<8>(a, s);  // + in-launch combine
-      else if (mf) launch_mproj_split<6>(a, s);
+      if (mf) launch_mproj_split<6>(a, s);
       else launch_gemv<TW, 3072, 4, 2, 1, 1>(a, s);
       break;
     case 5:
       a.W = w.w_lm; a.N = VOCAB; a.ln_w = w.lnf;
-      if (mf && B <= g_opt_mfma_ln) {
+      if (mf && B <= MFMA_LN_MAX) {
         launch_mfma_ln<3, 4>(a, s);
-      } else if (mf && g_opt_ln_stats >= 2) {
-        launch_mfma2<768, 3, 1>(a, s);  // ln_f from the last mlp c_proj's statistics
       } else if (mf) {
         hipLaunchKernelGGL((ar_rows_kernel<4>), dim3(B), dim3(64), 0, s, a);
         launch_mfma2<768, 3>(a, s);
       } else if (a.defer_sel) {
         if (fm) launch_gemv<TW, 768, 1, 2, 4, 9>(a, s);
         else launch_gemv<TW, 768, 1, 2, 0, 9>(a, s);
-      } else if (select) {
-        if (fm) launch_gemv<TW, 768, 1, 2, 4, 4>(a, s);
-        else launch_gemv<TW, 768, 1, 2, 0, 4>(a, s);
       } else if (fm) {
         launch_gemv<TW, 768, 1, 2, 4, 3>(a, s);
       } else {
@@ -2413,11 +1916,10 @@ static GemvArgs make_args(const ArWeights& w, const ArState& st, int kvdtype, in
   a.codebook = w.codebook;
   a.wpe = w.wpe;
   a.emb_row = emb_row;
-  a.prefetch = g_opt_prefetch_in;
   return a;
 }
 
-// returns whether the greedy select was fused into lm_head
+// returns whether the greedy select is deferred into the next step (no argmax kernel after lm_head)
 template <typename TW>
 static bool ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B, const float* emb_row, int slot,
                       int pos, float* logits_dst, bool select, hipStream_t s) {
@@ -2427,9 +1929,8 @@ static bool ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B,
   for (int l = 0; l < N_LAYER; ++l)
     for (int op = 0; op < 5; ++op) launch_op<TW>(op, a, w, l, kvdtype, B, s);
   a.dst = logits_dst;
-  const bool fused = select && fused_select<TW>(B);
-  launch_op<TW>(5, a, w, N_LAYER - 1, kvdtype, B, s, fused);
-  return fused || a.defer_sel;
+  launch_op<TW>(5, a, w, N_LAYER - 1, kvdtype, B, s);
+  return a.defer_sel != 0;
 }
 
 // Launch one op of the decode step `iters` times (bench.py times it with HIP events); layer 1.
@@ -2443,7 +1944,7 @@ static int ar_probe_impl(const ArWeights& w, const ArState& st, int kvdtype, int
   a.dst = st.logits;
   hipLaunchKernelGGL(ar_rowinfo_init_kernel, dim3((B + 63) / 64), dim3(64), 0, s, st, B);
   for (int i = 0; i < iters; ++i)
-    if (!launch_op<TW>(which, a, w, which == 5 ? N_LAYER - 1 : 1, kvdtype, B, s, which == 5 && fused_select<TW>(B)))
+    if (!launch_op<TW>(which, a, w, which == 5 ? N_LAYER - 1 : 1, kvdtype, B, s))
       return 1;  // no kernel of its own at this B
   return 0;
 }
@@ -2458,9 +1959,9 @@ void ar_launch_step(const ArWeights& w, const ArState& st, int wdtype, int kvdty
                     const float* emb_row, int slot, int pos, float* logits_out, hipStream_t s) {
   float* dst = mode == 0 ? st.logits : logits_out;
   const float* er = mode == 0 ? nullptr : emb_row;
-  const bool fused = wdtype == LVX_DTYPE_BF16 ? ar_layers<bf16_t>(w, st, kvdtype, B, er, slot, pos, dst, mode == 0, s)
-                                             : ar_layers<float>(w, st, kvdtype, B, er, slot, pos, dst, mode == 0, s);
-  if (mode == 0 && !fused) hipLaunchKernelGGL(ar_argmax_kernel, dim3(B), dim3(256), 0, s, st);
+  const bool deferred = wdtype == LVX_DTYPE_BF16 ? ar_layers<bf16_t>(w, st, kvdtype, B, er, slot, pos, dst, mode == 0, s)
+                                                : ar_layers<float>(w, st, kvdtype, B, er, slot, pos, dst, mode == 0, s);
+  if (mode == 0 && !deferred) hipLaunchKernelGGL(ar_argmax_kernel, dim3(B), dim3(256), 0, s, st);
 }
 
 // deferred select: the last step's lm_head granules are committed here (argmax_commit), once per

@@ -586,29 +586,22 @@ __global__ __launch_bounds__(256) void gemm2_splitk_reduce(GemmArgs g) {
   }
 }
 
-int g_opt_codec_g2 = 1;       // large-M bf16 GEMM (gemm_bf16_kernel) on/off
-int g_opt_codec_xcd = 1;      // its XCD-aware tile order
-int g_opt_codec_g2_min = 128;  // smallest M that takes it (measured: M = 256 0.86 vs 1.04 ms, M = 10 0.64 vs 0.59)
-
-// 256-row tiles when (M/256) x (N/128) tiles >= this (one block per CU); 0: off. Measured slower
-// (tools/codec_sweep.py, 32 x 256 frames: 3.51 vs 2.99 ms; 64 x 256: 7.04 vs 5.16 ms): one resident
-// block per CU exposes the load latency that two 128-row blocks hide for each other.
-int g_opt_codec_bm256 = 0;
+int g_opt_codec_g2 = 1;  // 1: large-M bf16 GEMMs on gemm_bf16_kernel; 0: on gemm_mfma (cross-check)
+// smallest M that takes gemm_bf16_kernel (measured: M = 256 0.86 vs 1.04 ms, M = 10 0.64 vs 0.59).
+// 256-row tiles (one block per CU) measured slower (32 x 256 frames: 3.51 vs 2.99 ms; 64 x 256: 7.04
+// vs 5.16): one resident block per CU exposes the load latency that two 128-row blocks hide for each other.
+constexpr int CODEC_G2_MIN_M = 128;
 
 template <typename TA, typename TB, int AMODE, int EPI, typename TC>
 static void gemm2_launch(GemmArgs g, hipStream_t s) {
-  // 256-row tiles when there are enough of them to keep every CU busy (one block per CU)
-  const bool big = g_opt_codec_bm256 > 0 && (size_t)((g.M + 255) / 256) * ((g.N + G2_BN - 1) / G2_BN) >= (size_t)g_opt_codec_bm256;
-  const int BMr = big ? 256 : 128;
-  const int tiles = ((g.N + G2_BN - 1) / G2_BN) * ((g.M + BMr - 1) / BMr);
+  const int tiles = ((g.N + G2_BN - 1) / G2_BN) * ((g.M + 127) / 128);
   const int nkt = g.K / G2_BK;
   int ks = 1;
   while (tiles * ks * 2 <= 512 && nkt / (ks * 2) >= 4 && (size_t)(ks * 2) * g.M * g.N <= g_ws_floats) ks *= 2;
   g.ksplit = ks;
-  g.xcd_remap = g_opt_codec_xcd;
-  dim3 grid((g.N + G2_BN - 1) / G2_BN, (g.M + BMr - 1) / BMr, ks);
-  if (big) hipLaunchKernelGGL((gemm_bf16_kernel<TA, TB, AMODE, EPI, TC, 256>), grid, dim3(256), 0, s, g);
-  else hipLaunchKernelGGL((gemm_bf16_kernel<TA, TB, AMODE, EPI, TC, 128>), grid, dim3(256), 0, s, g);
+  g.xcd_remap = 1;
+  dim3 grid((g.N + G2_BN - 1) / G2_BN, (g.M + 127) / 128, ks);
+  hipLaunchKernelGGL((gemm_bf16_kernel<TA, TB, AMODE, EPI, TC, 128>), grid, dim3(256), 0, s, g);
   if (ks > 1) {
     const int blocks = (int)std::min<size_t>(((size_t)g.M * g.N + 255) / 256, 2048);
     hipLaunchKernelGGL((gemm2_splitk_reduce<EPI, TC>), dim3(blocks), dim3(256), 0, s, g);
@@ -621,7 +614,7 @@ template <typename TW, typename TA, int AMODE, int EPI, typename TC = float>
 static void gemm_w(const GemmArgs& g, hipStream_t s) {
   if constexpr (sizeof(TW) == 2) {
     if (g.wscale) gemm2_launch<TA, fp8_t, AMODE, EPI, TC>(g, s);  // fp8 codec weights: any M
-    else if (g_opt_codec_g2 && g.M >= g_opt_codec_g2_min) gemm2_launch<TA, bf16_t, AMODE, EPI, TC>(g, s);
+    else if (g_opt_codec_g2 && g.M >= CODEC_G2_MIN_M) gemm2_launch<TA, bf16_t, AMODE, EPI, TC>(g, s);
     else gemm_launch<true, TA, bf16_t, AMODE, EPI, TC>(g, 1, s);
   } else {
     static_assert(sizeof(TA) == 4 && sizeof(TC) == 4, "parity mode keeps fp32 activations");

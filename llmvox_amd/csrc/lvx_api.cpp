@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdio>
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -27,6 +28,9 @@ static constexpr int kGraphSteps = 16;  // decode steps per captured graph
 namespace {
 
 thread_local std::string g_err;
+// bumped by every lvx_set_option (the switches are process-wide): a context whose graphs were
+// captured under an older epoch drops them before its next replay
+std::atomic<unsigned> g_opt_epoch{0};
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -159,6 +163,7 @@ struct lvx_ctx {
   std::map<GraphKey, hipGraphExec_t> graphs;
   std::vector<hipGraph_t> graph_defs;
   bool use_graphs = true;
+  unsigned graph_epoch = 0;  // g_opt_epoch when the cached graphs were captured
   hipStream_t capture_stream = nullptr;  // graphs of null-stream callers are captured here
   std::mutex mu;
 
@@ -531,31 +536,12 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   if (!c || !name) return fail(LVX_E_ARG, "null argument");
   std::string n(name);
   std::lock_guard<std::mutex> lk(c->mu);
-  if (n == "gemv_reg") g_opt_gemv_reg = value;
-  else if (n == "attn_v2") g_opt_attn_v2 = value;
-  else if (n == "cproj_b1") g_opt_cproj_b1 = value;
-  else if (n == "prefetch_in") g_opt_prefetch_in = value;
-  else if (n == "mfma_batch") g_opt_mfma_batch = value;
-  else if (n == "fuse_argmax") g_opt_fuse_argmax = value;
-  else if (n == "defer_select") g_opt_defer_select = value;
-  else if (n == "fuse_mlp") g_opt_fuse_mlp = value;
-  else if (n == "mfma_ln") g_opt_mfma_ln = value;
-  else if (n == "bt") g_opt_bt = value;
-  else if (n == "bt_rows") g_opt_bt_rows = value;
-  else if (n == "bt_merge") g_opt_bt_merge = value;
-  else if (n == "codec_g2") g_opt_codec_g2 = value;
-  else if (n == "codec_g2_min") g_opt_codec_g2_min = value;
-  else if (n == "codec_xcd") g_opt_codec_xcd = value;
-  else if (n == "attn_blocks") g_opt_attn_blocks = value;
-  else if (n == "attn_depth") g_opt_attn_depth = value;
-  else if (n == "attn_waves") g_opt_attn_waves = value;
-  else if (n == "mfma_btile") g_opt_mfma_btile = value;
-  else if (n == "ln_stats") g_opt_ln_stats = value;
-  else if (n == "codec_bm256") g_opt_codec_bm256 = value;
-  else if (n == "b1_splits") g_opt_b1_splits = value;
+  if (n == "defer_select") g_opt_defer_select = value != 0;
+  else if (n == "fuse_mlp") g_opt_fuse_mlp = value != 0;
+  else if (n == "bt") g_opt_bt = std::min(std::max(value, 0), 2);
+  else if (n == "codec_g2") g_opt_codec_g2 = value != 0;
   else return fail(LVX_E_NAME, "unknown option " + n);
-  for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);  // captured kernels change
-  c->graphs.clear();
+  g_opt_epoch.fetch_add(1);  // every context's captured kernels change (checked in cached_graph)
   return LVX_OK;
 }
 
@@ -612,6 +598,12 @@ int lvx_ar_forward_row(lvx_ctx* c, int slot, int pos, const float* emb_row, floa
 // replayed on the null stream. Caller holds c->mu.
 static int cached_graph(lvx_ctx* c, const GraphKey& key, hipStream_t s,
                         const std::function<void(hipStream_t)>& launch, hipGraphExec_t* out) {
+  const unsigned epoch = g_opt_epoch.load();
+  if (c->graph_epoch != epoch) {  // an option changed since these graphs were captured
+    for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
+    c->graphs.clear();
+    c->graph_epoch = epoch;
+  }
   auto it = c->graphs.find(key);
   if (it == c->graphs.end()) {
     hipStream_t cs = s;

@@ -17,8 +17,7 @@ constexpr int NSPLIT = 16;  // max KV splits per (stream, head) in decode attent
 #endif
 constexpr int YCOPIES = LVX_YCOPIES;  // accumulator copies of the fused MLP (spreads atomic contention)
 constexpr int LM_MAX_BLOCKS = 1024;  // lm_head blocks of the fused argmax tail (4096 rows / 8 per block = 512)
-extern int g_opt_gemv_reg, g_opt_attn_v2, g_opt_cproj_b1, g_opt_prefetch_in, g_opt_mfma_batch, g_opt_fuse_argmax, g_opt_defer_select, g_opt_attn_depth, g_opt_attn_waves, g_opt_mfma_btile,
-    g_opt_fuse_mlp, g_opt_mfma_ln, g_opt_bt, g_opt_bt_rows, g_opt_bt_merge, g_opt_codec_g2, g_opt_codec_g2_min, g_opt_codec_xcd, g_opt_attn_blocks, g_opt_ln_stats, g_opt_codec_bm256, g_opt_b1_splits;  // A/B switches (lvx_set_option)
+extern int g_opt_defer_select, g_opt_fuse_mlp, g_opt_bt, g_opt_codec_g2;  // cross-check switches (lvx_set_option)
 
 // Device-resident AR weights. Matrices are [out][in] row-major (torch Linear layout),
 // in the context's weight dtype; vectors and gathered tables are fp32.

@@ -106,8 +106,8 @@ def eng_batched():
     e.close()
 
 
-@pytest.mark.parametrize("B,mode", [(3, 2), (4, 1), (8, 1), (32, 1), (48, 1)])
-def test_batched_deferred_select_matches_argmax_kernel(eng_batched, B, mode):
+@pytest.mark.parametrize("B", [4, 8, 32, 48])
+def test_batched_deferred_select_matches_argmax_kernel(eng_batched, B):
     """Batched steps (MFMA / v3 paths): the select runs in the next step's embedding rows kernel
     (ar_argmax_kernel after the last step). These paths have no arrival-order sums: bit-equal,
     with one idle row."""
@@ -136,7 +136,7 @@ def test_batched_deferred_select_matches_argmax_kernel(eng_batched, B, mode):
     e.set_option("defer_select", 0)
     try:
         ref = run()
-        e.set_option("defer_select", mode)  # 2: also B = 3
+        e.set_option("defer_select", 1)
         got = run()
     finally:
         e.set_option("defer_select", 1)

@@ -33,4 +33,4 @@ for spec in sys.argv[3:] or [""]:
     us = statistics.median(ts)
     print(f"B={B} P={P0}.. [{spec}]: {us:7.1f} us/step  {B / us * 1e6:9.0f} tok/s", flush=True)
     for k, v in opts:
-        e.set_option(k, {"bt": 1, "bt_rows": 16, "bt_merge": 0, "mfma_ln": 8, "attn_blocks": 256, "b1_splits": 16, "defer_select": 1, "attn_depth": 2, "attn_waves": 4, "mfma_btile": 0, "prefetch_in": 1, "fuse_mlp": 1}.get(k, 0))
+        e.set_option(k, {"bt": 1, "defer_select": 1, "fuse_mlp": 1, "codec_g2": 1}.get(k, 0))
