@@ -1717,7 +1717,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_bt_kernel(GemvArgs a) {
   }
 }
 
-// Measured (tools/bt_sweep.py, us per step at positions 256-511): v3 saves kernels but every block
+// Measured (round-1 sweep, us per step at positions 256-511): v3 saves kernels but every block
 // re-reads the fp32 x rows of its batch tile, and per-CU load bandwidth (not launch count) sets the
 // time of these short GEMMs: B = 8 / 16 / 32 v2 149 / 162 / 191 vs v3 172 / 181 / 203 (16-row
 // tiles, separate merge); a fused merge re-reads ns_max partials per row and block: 271 / 302 / 266.

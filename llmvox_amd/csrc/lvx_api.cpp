@@ -645,7 +645,7 @@ static int ar_step_impl(lvx_ctx* c, int n_steps, int B, const int32_t* slots, co
   hipStream_t s = (hipStream_t)stream;
   ar_launch_rowinfo_init(st, B, s);  // per-row control records, then advanced by every step
   // null-stream callers (torch's default stream) launch the steps one by one: replaying the same
-  // steps as graphs on a stream of their own measured no faster (tools/ab_graphs.sh)
+  // steps as graphs on a stream of their own measured no faster (round 1)
   if (!c->use_graphs || s == nullptr) {
     for (int i = 0; i < n_steps; ++i)
       ar_launch_step(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, 0, nullptr, 0, 0, nullptr, s);

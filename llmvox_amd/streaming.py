@@ -383,7 +383,7 @@ class FusedScheduler:
     ``run_until_idle`` and by an idle ``run_chunk``). Off by default: measured on MI355X, the
     latency-bound AR chain stalls while codec kernels from another queue are in flight, so the
     overlapped loop is slower than running the codec after the AR on one stream (25.5 vs
-    23.6 ms per 256-token chunk at 1 stream, 65.2 vs 64.4 ms at 32; tools/loop_probe.py).
+    23.6 ms per 256-token chunk at 1 stream, 65.2 vs 64.4 ms at 32; round 1).
     """
 
     def __init__(self, engine, max_chunk: int = 64, max_rows: Optional[int] = None, to_bytes: bool = True,
