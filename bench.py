@@ -5,9 +5,13 @@ Default workload (BASELINE.json configs[2], the largest single-GPU configuration
 bf16, 1xMI355X, 32 concurrent streams batched decode + vocoder". One bench STEP = one 256-token
 chunk of 32 utterance streams: 256 batched greedy AR decode steps of the speech-token GPT (B = 32
 rows per step) + the WavTokenizer decode of the 32 x 256 codes (one batched codec call, 2,621,440
-PCM samples at 24 kHz) + the PCM copy to the host. Steps continue the same streams (positions
-0..K*256-1). Synthetic input: stream 0 speaks the config's 64-char sentence, the others seeded
-random 64-char sentences (ByT5 ids, then PAD); seeded synthetic weights at the reference init
+PCM samples at 24 kHz) + the PCM copy to the host. Each stream speaks utterances of --utterance
+1024 tokens (N = 1024 per stream): four consecutive steps continue one utterance
+(KV positions 0..1023), then the stream starts its next utterance (a new sentence, its KV slot
+reset, as the reference resets it at every end of audio, streaming_server.py:406-417);
+--utterance 0 keeps one utterance per stream for the whole run. Synthetic input: stream 0's first
+utterance is the config's 64-char sentence, every other one a seeded random 64-char sentence
+(ByT5 ids, then PAD); seeded synthetic weights at the reference init
 scales (no checkpoints offline). p50 first-chunk latency is measured separately on one stream of
 the same engine through the service scheduler (FusedScheduler), from the first text word enqueued
 to the first 3,200-sample (10-token) dump as bytes on the host.
@@ -508,7 +512,10 @@ def first_chunk_latency(eng, reps=12):
 def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, world=1, codec_overlap=False):
     """W untimed then K timed bench steps (one step = `chunk` fused decode steps for the S streams,
     the batched codec decode of their codes, the PCM to the host; the PCM gathered to rank 0 when
-    distributed). Returns (seconds, last token buffer, codec stream, token buffers, PCM buffers)."""
+    distributed). With reset_every R, step c is chunk c % R of utterance c // R: the streams' KV
+    slots are reset at every utterance start and `mine` holds the utterances' text plans back to
+    back ([S][n_utterances * R * chunk]). Returns (seconds, last token buffer, codec stream, token
+    buffers, PCM buffers)."""
     from llmvox_amd.parallel import gather_pcm
     dev = eng.device
     slots = torch.arange(S, dtype=torch.int32, device=dev)
@@ -532,13 +539,11 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
         i = c & 1
         main = torch.cuda.current_stream(dev)
         main.wait_event(ev_codec[i])  # tok_bufs[i] is free again (its decode has read it)
-        cc = c
-        if reset_every:  # configs[4]: a new sentence every reset_every chunks, KV reset per sentence
-            cc = c % reset_every
-            if cc == 0:
-                for s_ in range(S):
-                    eng.reset_slot(s_)
-        text_plan.copy_(mine[:, cc * chunk:(cc + 1) * chunk])
+        col = c * chunk  # chunk c of the back-to-back utterance plans
+        if reset_every and c % reset_every == 0:  # a new utterance: KV slots reset (a new sentence)
+            for s_ in range(S):
+                eng.reset_slot(s_)
+        text_plan.copy_(mine[:, col:col + chunk])
         rowstep.zero_()
         eng.ar_steps(chunk, slots, text_plan, rowstep, tok_bufs[i])
         ev_ar[i].record(main)
@@ -633,8 +638,9 @@ def main():
                     help="BASELINE.json workload (2: default, 32 streams; 1: one stream; 3: scheduler replicas; 4: fp8)")
     ap.add_argument("--codec-dtype", default=None, choices=["fp8"], help="fp8 codec weights (configs[4])")
     ap.add_argument("--utt-tokens", type=int, default=2048, help="configs[3]: tokens per utterance (one step)")
-    ap.add_argument("--reset-every", type=int, default=4,
-                    help="configs[4]: chunks per sentence (KV reset at every sentence start)")
+    ap.add_argument("--utterance", type=int, default=1024,
+                    help="configs[1]/[2]/[4]: tokens per utterance (SURVEY 8(d) N = 1024; a multiple of --chunk): "
+                         "KV reset and a new sentence at every utterance start; 0 = one utterance for the whole run")
     ap.add_argument("--rehearse", action="store_true",
                     help="CPU-only rehearsal of the multi-rank skeleton (gloo; tests/test_bench_launcher.py)")
     args = ap.parse_args()
@@ -693,18 +699,24 @@ def main():
     if args.config == 3:
         return run_config3(args, eng, world, rank, local, dist)
 
-    # ---- text plans: stream 0 of rank 0 speaks the config sentence; others seeded sentences
-    n_pos = max(K, Wm) * chunk
+    # ---- text plans: stream 0 of rank 0 opens with the config sentence; every other utterance is a
+    # seeded random sentence; utterances back to back per stream
+    if args.utterance and args.utterance % chunk:
+        raise SystemExit("--utterance must be a multiple of --chunk")
+    reset_every = args.utterance // chunk if args.utterance else 0
+    utt = args.utterance or max(K, Wm) * chunk
+    n_utt = -(-max(K, Wm) * chunk // utt)
+    n_pos = n_utt * utt
     plans = np.zeros((world * S, n_pos), dtype=np.int32)
     rng = np.random.default_rng(1234)
     for g in range(world * S):
-        ids = sentence_ids(SENTENCE if g == 0 else random_sentence(rng))
-        plans[g] = plan_for(ids, 0, n_pos)
+        for u in range(n_utt):
+            ids = sentence_ids(SENTENCE if (g == 0 and u == 0) else random_sentence(rng))
+            plans[g, u * utt:(u + 1) * utt] = plan_for(ids, 0, utt)
     from llmvox_amd.parallel import scatter_plans
     # rank 0 scatters the text-id shards over RCCL (the path's inbound exchange)
     mine = scatter_plans(torch.from_numpy(plans), S, n_pos, dev, dist, rank)
 
-    reset_every = args.reset_every if args.config == 4 else 0
     dt, last_tok, codec_stream, tok_bufs, pcm_bufs = run_chunks(
         eng, mine, S, chunk, K, Wm, reset_every, dist, rank, world, args.codec_overlap)
     if dist is not None:
@@ -724,7 +736,7 @@ def main():
     if not args.no_probe:
         for s in range(S):
             eng.reset_slot(s)
-        span = (min(K, reset_every) if reset_every else K) * chunk
+        span = (min(K, reset_every) if reset_every else K) * chunk  # positions one utterance spans
         ppos = args.probe_pos or max(1, span // 2)
         for s in range(S):
             eng.set_slot(s, ppos - 1, 0)
@@ -783,8 +795,11 @@ def main():
                     "seeded synthetic weights at reference init scales)",
             "config": {"workload": f"configs[{args.config}]: 30M LLMVoX {args.dtype}, "
                                    f"{S} stream(s)/GPU, {chunk}-token chunk, greedy AR + WavTokenizer decode + PCM to host"
-                                   + (f", fp8 KV + fp8 codec weights, KV reset every {reset_every} chunks" if reset_every else ""),
-                       "streams_per_gpu": S, "chunk_tokens": chunk, "positions": K * chunk,
+                                   + (", fp8 KV + fp8 codec weights" if args.config == 4 else "")
+                                   + (f", utterances of {utt} tokens (KV reset + a new sentence per utterance)"
+                                      if reset_every else f", one {K * chunk}-token utterance per stream"),
+                       "streams_per_gpu": S, "chunk_tokens": chunk, "utterance_tokens": utt,
+                       "kv_positions": f"0..{min(K * chunk, utt) - 1}",
                        "parallelism": f"streams sharded over {world} GPU(s), RCCL scatter text / gather PCM"},
             "dist": dist_info or {"backend": None, "world_size": 1},
             "audio_samples_per_s": round(320 * value, 1),

@@ -774,54 +774,81 @@ __global__ __launch_bounds__(256) void gn_adaln_kernel(const float* __restrict__
   }
 }
 
-// ConvNeXt prologue (modules.py:45-50): depthwise conv k7 pad 3 (+bias) then AdaLN
-template <typename TO>
-__global__ __launch_bounds__(256) void dwconv_adaln_kernel(const float* __restrict__ x, int L, const float* __restrict__ dwt,
-                                                           const float* __restrict__ dwb, const float* __restrict__ scale,
-                                                           const float* __restrict__ shift, TO* __restrict__ y) {
-  // one frame per block, 3 channels per thread; the 7 taps of x and of the tap-major weights
-  // ([7][768], repacked at upload: coalesced) all issued up front and unconditionally (a tap
-  // outside [0, L) reads a clamped frame and is dropped by a select, in the guarded sum's order).
-  // (A 192-thread float4 variant measured slower: 5.0 vs 3.8 us at 256 frames, 27.2 vs 26.4 at
-  // 8,192.)
-  __shared__ float red[4];
-  const int m = blockIdx.x, tid = threadIdx.x, b = m / L, t = m - b * L;
-  float xv[3][7], wv[3][7], v[3], bb[3], sc[3], sh[3];
+// ConvNeXt prologue (modules.py:45-50): depthwise conv k7 pad 3 (+bias, tap-major weights [7][768]
+// repacked at upload) then AdaLN, over a tile of FT consecutive frames of one stream per block:
+// each thread owns 3 channels and slides the 7-tap window along the tile, so x is read
+// (FT + 6) / FT times instead of 7 and the tap weights once per tile instead of once per frame (the
+// round-1 one-frame-per-block form moved 43 KB through L2 per 1.5 KB written: 19.6 us at 8,192
+// frames = 1.9 TB/s). Taps outside [0, L) read a clamped frame and are dropped by a select, in the
+// guarded sum's order; the LayerNorm reductions follow row_ln's order (same bits as that form).
+// FT = 16 for large M, 4 when there are few frames.
+template <typename TO, int FT>
+__global__ __launch_bounds__(256) void dwconv_adaln_tile_kernel(const float* __restrict__ x, int L,
+                                                                const float* __restrict__ dwt,
+                                                                const float* __restrict__ dwb,
+                                                                const float* __restrict__ scale,
+                                                                const float* __restrict__ shift, TO* __restrict__ y) {
+  __shared__ float red[2][4][FT];
+  const int b = blockIdx.y, t0 = blockIdx.x * FT, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  float v[3][FT], sc[3], sh[3];
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {  // bias and the AdaLN affine with the taps, not behind the reductions
+  for (int j = 0; j < 3; ++j) {
     const int c = tid + 256 * j;
-    bb[j] = dwb[c];
+    float w[7], xs[FT + 6];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) w[k] = dwt[k * CD + c];
+#pragma unroll
+    for (int i = 0; i < FT + 6; ++i) xs[i] = x[((size_t)b * L + min(max(t0 + i - 3, 0), L - 1)) * CD + c];
+    const float bb = dwb[c];
     sc[j] = scale[c];
     sh[j] = shift[c];
-  }
 #pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    const int tt = min(max(t + k - 3, 0), L - 1);
+    for (int f = 0; f < FT; ++f) {
+      float a = 0.f;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int c = tid + 256 * j;
-      xv[j][k] = x[((size_t)b * L + tt) * CD + c];
-      wv[j][k] = dwt[k * CD + c];
+      for (int k = 0; k < 7; ++k) {
+        const int tt = t0 + f + k - 3;
+        const float na = a + w[k] * xs[f + k];
+        a = (tt >= 0 && tt < L) ? na : a;
+      }
+      v[j][f] = a + bb;
     }
   }
+  // AdaLayerNorm (modules.py:81-86) per frame: block_sum's order (wave DPP sum, then waves 0..3)
+  float mean[FT];
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int c = tid + 256 * j;
-    float a = 0.f;
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      const int tt = t + k - 3;
-      const float na = a + wv[j][k] * xv[j][k];
-      a = (tt >= 0 && tt < L) ? na : a;
-    }
-    v[j] = a + bb[j];
-    (void)c;
+  for (int f = 0; f < FT; ++f) {
+    const float s = wave_sum(v[0][f] + v[1][f] + v[2][f]);
+    if (lane == 0) red[0][wave][f] = s;
   }
-  row_ln(v, 1e-6f, red);  // AdaLayerNorm (modules.py:81-86): no affine, eps 1e-6, then scale / shift
+  __syncthreads();
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int c = tid + 256 * j;
-    store_out<TO>(y + (size_t)m * CD + c, v[j] * sc[j] + sh[j]);
+  for (int f = 0; f < FT; ++f) {
+    float r = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r += red[0][i][f];
+    mean[f] = r * (1.0f / CD);
+  }
+#pragma unroll
+  for (int f = 0; f < FT; ++f) {
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { v[j][f] -= mean[f]; q += v[j][f] * v[j][f]; }
+    q = wave_sum(q);
+    if (lane == 0) red[1][wave][f] = q;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int f = 0; f < FT; ++f) {
+    float r = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r += red[1][i][f];
+    const float rstd = 1.0f / sqrtf(r * (1.0f / CD) + 1e-6f);
+    if (t0 + f < L) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        store_out<TO>(y + ((size_t)b * L + t0 + f) * CD + tid + 256 * j, v[j][f] * rstd * sc[j] + sh[j]);
+    }
   }
 }
 
@@ -1138,8 +1165,12 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
   hipLaunchKernelGGL(gn_adaln_kernel, dim3(M), dim3(256), 0, s, x, L, sc.stats, w.pn_w, w.pn_b,
                      w.ada_scale + (size_t)bw * CD, w.ada_shift + (size_t)bw * CD, x);
   for (int i = 0; i < 12; ++i) {  // ConvNeXt blocks (modules.py:43-60)
-    hipLaunchKernelGGL(dwconv_adaln_kernel<TAct>, dim3(M), dim3(256), 0, s, x, L, w.dw_w[i], w.dw_b[i],
-                       w.cn_scale[i] + (size_t)bw * CD, w.cn_shift[i] + (size_t)bw * CD, t2a);
+    if (M >= 2048)
+      hipLaunchKernelGGL((dwconv_adaln_tile_kernel<TAct, 16>), dim3((L + 15) / 16, B), dim3(256), 0, s, x, L, w.dw_w[i],
+                         w.dw_b[i], w.cn_scale[i] + (size_t)bw * CD, w.cn_shift[i] + (size_t)bw * CD, t2a);
+    else
+      hipLaunchKernelGGL((dwconv_adaln_tile_kernel<TAct, 4>), dim3((L + 3) / 4, B), dim3(256), 0, s, x, L, w.dw_w[i],
+                         w.dw_b[i], w.cn_scale[i] + (size_t)bw * CD, w.cn_shift[i] + (size_t)bw * CD, t2a);
     GemmArgs c{};
     c.ws = sc.ws;
     c.M = M; c.L = L; c.N = CFF; c.K = CD; c.ldw = CD;

@@ -10,7 +10,7 @@ export PYTHONPATH=.
 TAG=${TAG:-r02}
 O=gpurun_out/$TAG; mkdir -p $O
 ARGS=${ARGS:-"--steps 20 --warmup 0 --no-cpu-baseline --no-parity-line"}
-KEY=${KEY:-bf16/kvbf16/B32/P2560}
+KEY=${KEY:-bf16/kvbf16/B32/P512}
 CKEY=${CKEY:-bf16/F8192/L256}
 run() { # tag, timeout, rocprof args..., -- cmd
   local tag=$1 t=$2; shift 2
