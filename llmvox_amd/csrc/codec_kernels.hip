@@ -27,6 +27,8 @@ constexpr int CD = 768, CFF = 2304, CIN = 512, NFFT = 1280, HOPL = 320, NB = 641
 enum { A_PLAIN = 0, A_CONV = 1 };
 enum { E_BIAS = 0, E_BIAS_GELU = 1, E_BIAS_GAMMA_RES = 2, E_BIAS_RES = 3, E_SCALE = 4 };
 
+typedef __attribute__((address_space(1))) unsigned gu32;
+
 struct GemmArgs {
   const void* A; int lda;    // fp32 or bf16 activations (kernel template TA)
   const void* W; int ldw;
@@ -41,6 +43,9 @@ struct GemmArgs {
   int xcd_remap;             // gemm_bf16_kernel: XCD-aware tile order (option codec_xcd)
   const float* wscale;       // fp8 weights: per-output-column scale (w = q * s), else null
   float* ws;
+  uint32_t* tick;            // gemm_mfma_kernel split-K: per-tile arrival counters of the in-launch
+                             // combine (zero between launches: the last arriver resets its own), or
+                             // null for the separate reduce kernel
 };
 
 template <typename T> __device__ __forceinline__ void load8(const T* p, float* v);
@@ -88,6 +93,8 @@ __device__ __forceinline__ float gemm_epi(const GemmArgs& g, const float* R, int
 // grid.z = batch x ksplit; with ksplit > 1 every split writes its raw partial tile to ws and
 // gemm_splitk_reduce applies the epilogue (fixed summation order: deterministic).
 constexpr int BM = 64, BN = 64, BK = 32;
+constexpr int KS_INLAUNCH = 16;    // most K splits of an in-launch combined GEMM
+constexpr int M_INLAUNCH = 16;     // in-launch split-K combine for M <= this (the first dumps)
 constexpr int LDF = BK + 1;  // fp32 LDS row (conflict-free b32 column reads)
 constexpr int LDH = BK + 8;  // bf16 LDS row (80 B)
 
@@ -266,16 +273,63 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(GemmArgs g) {
       rv[r] = (g.ksplit > 1) ? 0.f : R[(size_t)row * g.ldr + colc];
     }
   }
-  if (col >= g.N) return;
   if (g.ksplit > 1) {  // raw partial tile -> ws[ks][zb][M][N]
-    float* P = g.ws + ((size_t)ks * gridDim.z / g.ksplit + zb) * (size_t)g.M * g.N;
+    const int batch = gridDim.z / g.ksplit;
+    float* P = g.ws + ((size_t)ks * batch + zb) * (size_t)g.M * g.N;
+    if (!g.tick) {  // reduced by gemm_splitk_reduce
+      if (col >= g.N) return;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row < g.M) P[(size_t)row * g.N + col] = acc[r];
+      }
+      return;
+    }
+    // In-launch combine (cdna_hip_programming.md G16, counter form with write-through slabs): every
+    // wave stores its partial with sc1 stores and drains them, one relaxed agent ticket per block;
+    // the tile's last arriving slice reads every slab with sc1 loads (no fences), sums them in
+    // split order and applies the epilogue -- the same arithmetic as gemm_splitk_reduce, one
+    // launch fewer per GEMM.
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      if (row < g.M) P[(size_t)row * g.N + col] = acc[r];
+      if (row < g.M && col < g.N)
+        __hip_atomic_store((gu32*)(P + (size_t)row * g.N + col), __float_as_uint(acc[r]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int tile = (zb * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    if (tid == 0) {
+      const unsigned tk = __hip_atomic_fetch_add((gu32*)(g.tick + tile), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool last = tk == (unsigned)g.ksplit - 1;
+      if (last) __hip_atomic_store((gu32*)(g.tick + tile), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      As_[0] = last ? 1.f : 0.f;
+    }
+    __syncthreads();
+    if (As_[0] == 0.f) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below here
+    const size_t MN = (size_t)g.M * g.N;
+    TC* C = reinterpret_cast<TC*>(g.C) + zb * g.sC;
+    const int rows = min(BM, g.M - m0), cols = min(BN, g.N - n0);  // launched for M <= 16: <= 4 per thread
+    for (int e = tid; e < rows * cols; e += 256) {
+      const int row = m0 + e / cols, cc = n0 + e % cols;
+      const size_t off = (size_t)zb * MN + (size_t)row * g.N + cc;
+      float p[KS_INLAUNCH];  // every slab load in flight at once (index clamped, no load under a branch)
+#pragma unroll
+      for (int k = 0; k < KS_INLAUNCH; ++k)
+        p[k] = __uint_as_float(__hip_atomic_load((gu32*)(g.ws + (size_t)min(k, g.ksplit - 1) * batch * MN + off),
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < KS_INLAUNCH; ++k) v = k < g.ksplit ? v + p[k] : v;  // split order, as the reduce kernel
+      const float bb = (EPI != E_SCALE && g.bias) ? g.bias[cc] : 0.f;
+      const float gm = (EPI == E_BIAS_GAMMA_RES) ? g.gamma[cc] : 0.f;
+      store_out<TC>(C + (size_t)row * g.ldc + cc, gemm_epi<EPI>(g, R, row, cc, v, bb, gm));
     }
     return;
   }
+  if (col >= g.N) return;
   TC* C = reinterpret_cast<TC*>(g.C) + zb * g.sC;
   // outputs computed before any row guard: the empty asm takes them as inputs, so the waits for
   // the epilogue loads happen once here. Computed inside each guarded store, every store block
@@ -316,6 +370,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmArgs g, int batch)
 }
 
 static size_t g_ws_floats = 0;  // capacity of the split-K workspace (set by the front end)
+static uint32_t* g_tick = nullptr;  // per-tile counters of the in-launch combine (set by the front end)
 
 template <bool BF, typename TA, typename TB, int AMODE, int EPI, typename TC>
 static void gemm_launch(GemmArgs g, int batch, hipStream_t s) {
@@ -324,12 +379,19 @@ static void gemm_launch(GemmArgs g, int batch, hipStream_t s) {
   int ks = 1;
   // split K until the grid covers the chip (>= ~256 blocks), >= 4 k-tiles per split,
   // and the partials fit the workspace
+  // (measured, tools/codec_probe.py, 1 x 10 / 1 x 256 frames: no split 1.05 / 1.15 ms, at most 2
+  // splits 0.75 / 0.85, at most 4 0.56 / 0.74, this rule 0.51 / 0.70; a 160-block target the same,
+  // 640 slower at 32 x 256 frames)
   while (tiles * ks * 2 <= 320 && nkt / (ks * 2) >= 4 && (size_t)(ks * 2) * g.M * g.N * batch <= g_ws_floats) ks *= 2;
+  // in-launch combine for the first dumps (1 x 10 frames: 0.502 -> 0.442 ms)
+  const bool inl = g_tick && batch == 1 && g.M <= M_INLAUNCH && tiles <= 4096;
+  if (inl) ks = std::min(ks, KS_INLAUNCH);
   g.ksplit = ks;
+  g.tick = (inl && ks > 1) ? g_tick : nullptr;
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, batch * ks);
   if (g.K % BK == 0) hipLaunchKernelGGL((gemm_mfma_kernel<BF, TA, TB, AMODE, EPI, TC, true>), grid, dim3(256), 0, s, g);
   else hipLaunchKernelGGL((gemm_mfma_kernel<BF, TA, TB, AMODE, EPI, TC, false>), grid, dim3(256), 0, s, g);
-  if (ks > 1) {
+  if (ks > 1 && !g.tick) {
     const size_t total = (size_t)g.M * g.N * batch;
     const int blocks = (int)std::min<size_t>((total + 255) / 256, 2048);
     hipLaunchKernelGGL((gemm_splitk_reduce<EPI, TC>), dim3(blocks), dim3(256), 0, s, g, batch);
@@ -1092,6 +1154,7 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
   }
 
   g_ws_floats = sc.ws_floats;
+  g_tick = sc.tick;
   GemmArgs g{};
   g.ws = sc.ws;
   g.L = L;

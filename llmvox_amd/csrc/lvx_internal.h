@@ -134,6 +134,7 @@ struct CodecScratch {
   float* gn = nullptr;     // [M][768] GroupNorm(+swish) output
   float* ws = nullptr;     // split-K partials
   size_t ws_floats = 0;
+  uint32_t* tick = nullptr;  // [4096] per-tile arrival counters of the in-launch split-K combine (zero)
   float* att = nullptr;    // [sum_b L_b^2] scores
   float* stats = nullptr;  // [B][32][2]
   float* spec = nullptr;   // [M][1282]
