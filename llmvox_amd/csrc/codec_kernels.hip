@@ -971,148 +971,6 @@ __global__ void codes_gather_bf16_kernel(const float* __restrict__ cb, const int
                  (uint32_t)f32_to_bf16(v.z) | ((uint32_t)f32_to_bf16(v.w) << 16));
 }
 
-// ---------------------------------------------------------------------------------
-// AttnBlock core in one kernel (bf16 mode; decoder/models.py:107-127: single head, 768-dim,
-// non-causal over the whole dump): h = softmax(q k^T * 768^-0.5) v for one stream and a tile of 32
-// query frames per block, streaming 32-key tiles with an online softmax, so the L x L scores never
-// reach HBM (the unfused path: v transpose, scores GEMM, row softmax, P.V GEMM -- four launches
-// and 8 L^2 bytes per stream through HBM). q / k / v are the fp32 columns of the qkv GEMM output
-// [M][2304]; operands are rounded to bf16 as the unfused path's GEMMs round them (scores from bf16
-// q, k; P and v in bf16 for P.V; fp32 accumulation), the softmax is fp32. 4 waves: each owns a
-// 192-wide slice of the q.k dot products (partials summed through LDS) and of the 768 outputs.
-// ---------------------------------------------------------------------------------
-constexpr int FA_Q = 32, FA_K = 32;       // query rows per block, keys per tile
-constexpr int FA_LD = CD + 8;             // bf16 row stride of the Q / K tiles (16-B pad)
-constexpr int FA_VLD = FA_K + 8;          // bf16 row stride of the transposed V tile (channel rows)
-__global__ __launch_bounds__(256) void attn_fused_kernel(const float* __restrict__ qkv, int L,
-                                                         bf16_t* __restrict__ out, float scale) {
-  __shared__ __attribute__((aligned(16))) bf16_t Qs[FA_Q * FA_LD];
-  __shared__ __attribute__((aligned(16))) bf16_t KVs[CD * FA_VLD > FA_K * FA_LD ? CD * FA_VLD : FA_K * FA_LD];
-  __shared__ float Sred[4][FA_Q * FA_K];
-  __shared__ __attribute__((aligned(16))) bf16_t Ps[FA_Q * FA_VLD];
-  __shared__ float rowf[2][FA_Q];  // per query row: rescale factor of this tile, final 1 / l
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int b = blockIdx.y, q0 = blockIdx.x * FA_Q;
-  const float* base = qkv + (size_t)b * L * (3 * CD);
-  // Q tile -> bf16 LDS (rows past L: zeros, never stored)
-  for (int e = tid; e < FA_Q * (CD / 4); e += 256) {
-    const int r = e / (CD / 4), c4 = (e - r * (CD / 4)) * 4;
-    const int q = min(q0 + r, L - 1);
-    const float4 v = *reinterpret_cast<const float4*>(base + (size_t)q * (3 * CD) + c4);
-    *reinterpret_cast<uint2*>(Qs + r * FA_LD + c4) =
-        make_uint2((uint32_t)f32_to_bf16(v.x) | ((uint32_t)f32_to_bf16(v.y) << 16),
-                   (uint32_t)f32_to_bf16(v.z) | ((uint32_t)f32_to_bf16(v.w) << 16));
-  }
-  // softmax state of row r = tid / 8 (8 threads per row, 4 keys each)
-  const int sr = tid >> 3, sk = (tid & 7) * 4;
-  float m_run = -INFINITY, l_run = 0.f;
-  f32x16 acc[6];
-#pragma unroll
-  for (int t = 0; t < 6; ++t)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
-  for (int k0 = 0; k0 < L; k0 += FA_K) {
-    __syncthreads();  // Q staged / the previous tile's V reads done
-    for (int e = tid; e < FA_K * (CD / 4); e += 256) {  // K tile -> bf16 LDS
-      const int r = e / (CD / 4), c4 = (e - r * (CD / 4)) * 4;
-      const int kk = min(k0 + r, L - 1);
-      const float4 v = *reinterpret_cast<const float4*>(base + (size_t)kk * (3 * CD) + CD + c4);
-      *reinterpret_cast<uint2*>(KVs + r * FA_LD + c4) =
-          make_uint2((uint32_t)f32_to_bf16(v.x) | ((uint32_t)f32_to_bf16(v.y) << 16),
-                     (uint32_t)f32_to_bf16(v.z) | ((uint32_t)f32_to_bf16(v.w) << 16));
-    }
-    __syncthreads();
-    {  // partial scores over this wave's 192 dims: S[q][key], q = lane & 31 rows of the A operand
-      f32x16 sp;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) sp[e] = 0.f;
-#pragma unroll
-      for (int kk = 0; kk < 192; kk += 16) {
-        const int kc = wave * 192 + kk + 8 * (lane >> 5);
-        const bf16x8 fa = *reinterpret_cast<const bf16x8*>(Qs + (lane & 31) * FA_LD + kc);
-        const bf16x8 fb = *reinterpret_cast<const bf16x8*>(KVs + (lane & 31) * FA_LD + kc);
-        sp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, sp, 0, 0, 0);
-      }
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {  // acc element e: row (e & 3) + 8 (e >> 2) + 4 (lane >> 5), col lane & 31
-        const int r = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-        Sred[wave][r * FA_K + (lane & 31)] = sp[e];
-      }
-    }
-    __syncthreads();
-    {  // online softmax of row sr over keys sk..sk+3 (8 threads per row, xor-shuffles within them)
-      float sv[4], mx = -INFINITY;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int idx = sr * FA_K + sk + j;
-        const float v = ((Sred[0][idx] + Sred[1][idx]) + (Sred[2][idx] + Sred[3][idx])) * scale;
-        sv[j] = (k0 + sk + j < L) ? v : -INFINITY;
-        mx = fmaxf(mx, sv[j]);
-      }
-#pragma unroll
-      for (int o = 1; o < 8; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-      const float mn = fmaxf(m_run, mx);
-      const float alpha = (m_run == -INFINITY) ? 0.f : expf(m_run - mn);
-      float ps = 0.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float pv = (sv[j] == -INFINITY) ? 0.f : expf(sv[j] - mn);
-        const bf16_t pb = f32_to_bf16(pv);
-        Ps[sr * FA_VLD + sk + j] = pb;
-        ps += __uint_as_float((uint32_t)pb << 16);  // l sums the bf16 P the P.V product uses
-      }
-#pragma unroll
-      for (int o = 1; o < 8; o <<= 1) ps += __shfl_xor(ps, o);
-      l_run = l_run * alpha + ps;
-      m_run = mn;
-      if ((tid & 7) == 0) rowf[0][sr] = alpha;
-    }
-    // V tile transposed into the K buffer: Vt[channel][key] (the B operand of P.V reads 8 keys of
-    // one channel contiguously)
-    __syncthreads();
-    for (int e = tid; e < FA_K * (CD / 4); e += 256) {
-      const int r = e / (CD / 4), c4 = (e - r * (CD / 4)) * 4;
-      const int kk = min(k0 + r, L - 1);
-      const float4 v = *reinterpret_cast<const float4*>(base + (size_t)kk * (3 * CD) + 2 * CD + c4);
-      KVs[(c4 + 0) * FA_VLD + r] = f32_to_bf16(v.x);
-      KVs[(c4 + 1) * FA_VLD + r] = f32_to_bf16(v.y);
-      KVs[(c4 + 2) * FA_VLD + r] = f32_to_bf16(v.z);
-      KVs[(c4 + 3) * FA_VLD + r] = f32_to_bf16(v.w);
-    }
-    __syncthreads();
-    // O[q][c] = O * alpha[q] + P[q][keys] . V[keys][c] over this wave's 6 column tiles
-    float al[16];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) al[e] = rowf[0][(e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)];
-    bf16x8 fp[2];
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-      fp[kk] = *reinterpret_cast<const bf16x8*>(Ps + (lane & 31) * FA_VLD + kk * 16 + 8 * (lane >> 5));
-#pragma unroll
-    for (int t = 0; t < 6; ++t) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[t][e] *= al[e];
-      const int c = wave * 192 + t * 32 + (lane & 31);
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const bf16x8 fv = *reinterpret_cast<const bf16x8*>(KVs + c * FA_VLD + kk * 16 + 8 * (lane >> 5));
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fp[kk], fv, acc[t], 0, 0, 0);
-      }
-    }
-  }
-  if ((tid & 7) == 0) rowf[1][sr] = 1.0f / l_run;
-  __syncthreads();
-#pragma unroll
-  for (int t = 0; t < 6; ++t) {
-    const int c = wave * 192 + t * 32 + (lane & 31);
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int r = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-      if (q0 + r < L) out[((size_t)b * L + q0 + r) * CD + c] = f32_to_bf16(acc[t][e] * rowf[1][r]);
-    }
-  }
-}
-
 // v rows of qkv [B*L][2304] (cols 1536..2303) -> Vt [B][768][ldv]
 __global__ void v_transpose_kernel(const float* __restrict__ qkv, int L, int ldv, float* __restrict__ vt) {
   __shared__ float tile[32][33];
@@ -1329,16 +1187,6 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
     c.A = gn; c.lda = CD;
     c.W = w.at_qkv_w; c.wscale = w.at_qkv_s; c.bias = w.at_qkv_b; c.C = t1; c.ldc = CFF;
     gemm_w<TW, TAct, A_PLAIN, E_BIAS>(c, s);
-    if constexpr (sizeof(TAct) == 2) {  // fused: scores never leave the chip
-      hipLaunchKernelGGL(attn_fused_kernel, dim3((L + FA_Q - 1) / FA_Q, B), dim3(256), 0, s, t1, L,
-                         reinterpret_cast<bf16_t*>(gn), 0.036084391824351615f);
-      GemmArgs o{};
-      o.ws = sc.ws;
-      o.M = M; o.N = CD; o.K = CD; o.L = L;
-      o.A = gn; o.lda = CD; o.W = w.at_proj_w; o.wscale = w.at_proj_s; o.ldw = CD; o.bias = w.at_proj_b;
-      o.C = x; o.ldc = CD; o.res = x; o.ldr = CD;
-      gemm_w<TW, TAct, A_PLAIN, E_BIAS_RES>(o, s);
-    } else {
     const int ldS = (L + 3) & ~3;
     float* S = sc.att;            // [B][L][ldS]
     float* Vt = t2;               // [B][768][ldS]
@@ -1372,7 +1220,6 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
     o.A = p.C; o.lda = p.ldc; o.W = w.at_proj_w; o.wscale = w.at_proj_s; o.ldw = CD; o.bias = w.at_proj_b;
     o.C = x; o.ldc = CD; o.res = x; o.ldr = CD;
     gemm_w<TW, TAct, A_PLAIN, E_BIAS_RES>(o, s);
-    }
   }
   resnet(2);
   resnet(3);
