@@ -776,7 +776,8 @@ def main():
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(K, chunk)
+        # the same utterance length as the timed run (one stream: the oracle is B = 1)
+        cpu = cpu_baseline(min(K, reset_every) if reset_every else K, chunk)
 
     if rank == 0:
         out = {
