@@ -115,9 +115,12 @@ int lvx_ar_steps(lvx_ctx* ctx, int n_steps, int B, const int32_t* slots_dev, con
                  void* stream);
 /* Copy the logits [B][4096] of the last lvx_ar_step(s) call (diagnostics / tests). */
 int lvx_ar_logits(lvx_ctx* ctx, int B, float* dst_dev, void* stream);
-/* Synchronises the stream and reports (then clears) device-side errors: an embedding id out of
- * range (LVX_E_INDEX), a slot past max_positions (LVX_E_CAPACITY; reference: the block_size
- * AssertionError, src/model.py:205) or a row past the end of its plan (LVX_E_CAPACITY). */
+/* Synchronises the stream and reports (then clears) device-side errors: an embedding id or codec
+ * code out of range (LVX_E_INDEX), the ISTFT window envelope <= 1e-11 (LVX_E_STATE; reference:
+ * the assertion of decoder/spectral_ops.py:72 -- the fixed periodic Hann envelope is >= 0.72 on the
+ * trimmed span, so this is a self-check), a slot past max_positions (LVX_E_CAPACITY; reference:
+ * the block_size AssertionError, src/model.py:205) or a row past the end of its plan
+ * (LVX_E_CAPACITY). */
 int lvx_check_errors(lvx_ctx* ctx, void* stream);
 /* Set a slot's position and previous token (rewind after a speculative run-ahead, or jump). */
 int lvx_stream_set(lvx_ctx* ctx, int slot, int pos, int prev_token, void* stream);
@@ -167,7 +170,8 @@ int lvx_device_cus(lvx_ctx* ctx, int* cus_out);
  * decoded independently (each one exactly as a separate reference call with its own L). */
 int lvx_codec_decode_features(lvx_ctx* ctx, const float* feats_dev, int B, int L, int bandwidth_id,
                               float* pcm_dev, void* stream);
-/* codes_to_features + decode fused: codes int32 [B,L] -> pcm float32 [B,320*L] */
+/* codes_to_features + decode fused: codes int32 [B,L] -> pcm float32 [B,320*L]. A code outside
+ * [0, 4096) is clamped for the gather and flagged (the next lvx_check_errors: LVX_E_INDEX). */
 int lvx_codec_decode_codes(lvx_ctx* ctx, const int32_t* codes_dev, int B, int L, int bandwidth_id,
                            float* pcm_dev, void* stream);
 

@@ -954,17 +954,21 @@ __global__ void feats_transpose_kernel(const float* __restrict__ f, int L, TO* _
 }
 
 // codes [B*L] -> [B*L][512]
-__global__ void codes_gather_kernel(const float* __restrict__ cb, const int32_t* __restrict__ codes, float* __restrict__ out) {
+__global__ void codes_gather_kernel(const float* __restrict__ cb, const int32_t* __restrict__ codes, float* __restrict__ out, int32_t* __restrict__ err) {
   const int m = blockIdx.x;
-  const int code = min(max(codes[m], 0), 4095);
+  const int raw = codes[m];
+  const int code = min(max(raw, 0), 4095);  // clamped for the load; flagged (lvx_check_errors -> LVX_E_INDEX)
+  if (threadIdx.x == 0 && raw != code) atomicOr(err, 4);
   const float4 v = reinterpret_cast<const float4*>(cb + (size_t)code * CIN)[threadIdx.x];
   reinterpret_cast<float4*>(out + (size_t)m * CIN)[threadIdx.x] = v;
 }
 // bf16 mode: the rows as the embed conv's bf16 operand
 __global__ void codes_gather_bf16_kernel(const float* __restrict__ cb, const int32_t* __restrict__ codes,
-                                         bf16_t* __restrict__ out) {
+                                         bf16_t* __restrict__ out, int32_t* __restrict__ err) {
   const int m = blockIdx.x;
-  const int code = min(max(codes[m], 0), 4095);
+  const int raw = codes[m];
+  const int code = min(max(raw, 0), 4095);  // clamped for the load; flagged (lvx_check_errors -> LVX_E_INDEX)
+  if (threadIdx.x == 0 && raw != code) atomicOr(err, 4);
   const float4 v = reinterpret_cast<const float4*>(cb + (size_t)code * CIN)[threadIdx.x];
   reinterpret_cast<uint2*>(out + (size_t)m * CIN)[threadIdx.x] =
       make_uint2((uint32_t)f32_to_bf16(v.x) | ((uint32_t)f32_to_bf16(v.y) << 16),
@@ -1109,7 +1113,7 @@ __global__ __launch_bounds__(256) void istft_frames_kernel(const float* __restri
 
 // overlap-add (fold, hop 320) + trim 480 + divide by the window-square envelope
 __global__ void istft_ola_kernel(const float* __restrict__ frames, const float* __restrict__ window, int L,
-                                 float* __restrict__ pcm) {
+                                 float* __restrict__ pcm, int32_t* __restrict__ err) {
   const int b = blockIdx.y;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   const int T = HOPL * L;
@@ -1125,6 +1129,7 @@ __global__ void istft_ola_kernel(const float* __restrict__ frames, const float* 
     y += frames[((size_t)b * L + f) * NFFT + o];
     env += window[o] * window[o];
   }
+  if (!(env > 1e-11f)) atomicOr(err, 8);  // spectral_ops.py:72 `assert (window_envelope > 1e-11).all()`
   pcm[(size_t)b * T + j] = y / env;
 }
 
@@ -1147,8 +1152,8 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
   // a3: features, time-major [M][512]
   TAct* feats = reinterpret_cast<TAct*>(sc.feats);
   if (codes) {
-    if constexpr (sizeof(TAct) == 2) hipLaunchKernelGGL(codes_gather_bf16_kernel, dim3(M), dim3(CIN / 4), 0, s, w.codebook, codes, feats);
-    else hipLaunchKernelGGL(codes_gather_kernel, dim3(M), dim3(CIN / 4), 0, s, w.codebook, codes, feats);
+    if constexpr (sizeof(TAct) == 2) hipLaunchKernelGGL(codes_gather_bf16_kernel, dim3(M), dim3(CIN / 4), 0, s, w.codebook, codes, feats, sc.err);
+    else hipLaunchKernelGGL(codes_gather_kernel, dim3(M), dim3(CIN / 4), 0, s, w.codebook, codes, feats, sc.err);
   } else {
     hipLaunchKernelGGL(feats_transpose_kernel<TAct>, dim3((L + 31) / 32, CIN / 32, B), dim3(256), 0, s, feats_in, L, feats);
   }
@@ -1256,7 +1261,7 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
   }
   hipLaunchKernelGGL(istft_frames_kernel, dim3(M), dim3(256), 0, s, sc.spec,
                      reinterpret_cast<const float2*>(w.twiddle), w.window, sc.frames);
-  hipLaunchKernelGGL(istft_ola_kernel, dim3((HOPL * L + 255) / 256, B), dim3(256), 0, s, sc.frames, w.window, L, pcm);
+  hipLaunchKernelGGL(istft_ola_kernel, dim3((HOPL * L + 255) / 256, B), dim3(256), 0, s, sc.frames, w.window, L, pcm, sc.err);
 }
 
 void codec_launch_decode(const CodecWeights& w, const CodecScratch& sc, int wdtype, const float* feats_in,

@@ -432,14 +432,11 @@ int lvx_finalize(lvx_ctx* c) {
       (r = c->dalloc(&st.selp, 4)) || (r = c->dalloc(&st.selrow, S)) ||
       (r = c->dalloc(&st.xn, (size_t)S * D)) || (r = c->dalloc(&st.hb, (size_t)S * DFF)) ||
       (r = c->dalloc(&st.xb, (size_t)S * D)) || (r = c->dalloc(&st.xstat, (size_t)(D / 16) * S * 2)) ||
-      (r = c->dalloc(&st.tick, (size_t)(D / 16))) ||
-      (r = c->dalloc(&st.lmbest, (size_t)LM_MAX_BLOCKS * 4 * 2)) || (r = c->dalloc(&st.ticket, 4)) ||
+      (r = c->dalloc(&st.lmbest, (size_t)LM_MAX_BLOCKS * 4 * 2)) ||
       (r = c->dalloc(&st.yacc, (size_t)YCOPIES * S * D)))
     return r;
   HIP_TRY(hipMemset(st.yacc, 0, (size_t)YCOPIES * S * D * 4));
-  HIP_TRY(hipMemset(st.ticket, 0, 16));
   HIP_TRY(hipMemset(st.selp, 0, 16));
-  HIP_TRY(hipMemset(st.tick, 0, (D / 16) * 4));
   HIP_TRY(hipMemset(st.part_o, 0, (size_t)S * N_HEAD * NSPLIT * HD * 4));
   HIP_TRY(hipMemset(st.part_ml, 0, (size_t)S * N_HEAD * NSPLIT * 2 * 4));
   HIP_TRY(hipMemset(st.pos, 0, S * 4));
@@ -468,6 +465,7 @@ int lvx_finalize(lvx_ctx* c) {
       (r = c->dalloc(&cs.frames, (size_t)M * 1280)) || (r = c->dalloc(&cs.tick, 4096)))
     return r;
   HIP_TRY(hipMemset(cs.tick, 0, 4096 * 4));
+  cs.err = st.err;
   HIP_TRY(hipDeviceSynchronize());
   c->host.clear();
   c->finalized = true;
@@ -706,7 +704,8 @@ int lvx_check_errors(lvx_ctx* c, void* stream) {
   if (v) {
     (void)hipMemsetAsync(c->st.err, 0, 4, (hipStream_t)stream);
     if (v & 4) return fail(LVX_E_INDEX, "index out of range in self (a text id outside [0, 386) or a code "
-                                         "outside [0, 4096) given to lvx_text_embed / lvx_codes_to_features)");
+                                         "outside [0, 4096) given to lvx_text_embed / lvx_codes_to_features / lvx_codec_decode_codes)");
+    if (v & 8) return fail(LVX_E_STATE, "ISTFT window envelope <= 1e-11 (spectral_ops.py:72 assertion)");
     if (v & 1) return fail(LVX_E_CAPACITY, "a stream exceeded its KV capacity (max_positions)");
     return fail(LVX_E_CAPACITY, "a batch row ran past the end of its text plan (plan_stride)");
   }

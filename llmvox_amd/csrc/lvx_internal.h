@@ -60,12 +60,10 @@ struct ArState {
   float* h = nullptr;           // [B][3072]
   bf16_t* xn = nullptr;         // [B][768] bf16 operand rows (batched path)
   bf16_t* hb = nullptr;         // [B][3072] bf16 h (batched path)
-  bf16_t* xb = nullptr;         // [B][768] bf16 copy of x after c_proj (batched path, option ln_stats)
+  bf16_t* xb = nullptr;         // [B][768] bf16 copy of x after c_proj (batched path: c_fc's operand, normalised from xstat)
   float* xstat = nullptr;       // [max_streams][48 column blocks][2] (mean, M2) of x over 16 columns
-  uint32_t* tick = nullptr;     // [48] arrival tickets of the split mlp c_proj's in-launch combine (reset by the last arriver)
   float* logits = nullptr;      // [B][4096]
-  uint64_t* lmbest = nullptr;   // [LM_MAX_BLOCKS][4][2] per-block top1/top2 granules (fused lm_head + argmax)
-  uint32_t* ticket = nullptr;   // [4] arrival counter of the fused lm_head (reset by its last block)
+  uint64_t* lmbest = nullptr;   // [LM_MAX_BLOCKS][4][2] per-block top1/top2 granules of lm_head (deferred select, B <= 2)
   float* yacc = nullptr;        // [max_streams][YCOPIES][768] fused-MLP output accumulators (fp32 atomics);
                                 // a row's copies adjacent: spaced by max_streams rows they shared
                                 // L2 channels (B = 1: 82.6 vs 69.6 us/step at max_streams 32)
@@ -139,6 +137,7 @@ struct CodecScratch {
   float* stats = nullptr;  // [B][32][2]
   float* spec = nullptr;   // [M][1282]
   float* frames = nullptr; // [M][1280]
+  int32_t* err = nullptr;  // = ArState.err: bit 4 a code outside [0, 4096), bit 8 the ISTFT envelope <= 1e-11
   int max_frames = 0;
 };
 

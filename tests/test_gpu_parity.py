@@ -130,3 +130,24 @@ def test_codec_batched_equals_single(eng):
     for b in range(3):
         single = eng.decode_codes(codes[b:b + 1]).cpu()
         assert torch.allclose(batched[b:b + 1], single, atol=1e-6, rtol=0)
+
+
+@pytest.mark.parametrize("what", ["text_embed", "codes_to_features", "decode_codes"])
+def test_out_of_range_ids_raise_index_error(eng, what):
+    """The reference raises IndexError for an embedding / codebook id out of range (nn.Embedding,
+    decoder/pretrained.py:209-239); the device path clamps the load, flags it, and the next
+    check_errors raises LvxIndexError (an IndexError). The flag is cleared by the report."""
+    from llmvox_amd._lib import LvxIndexError
+    for bad in (-1, {"text_embed": 386}.get(what, 4096)):
+        if what == "text_embed":
+            eng.text_embed(torch.tensor([5, bad, 7], dtype=torch.int64, device=eng.device))
+        elif what == "codes_to_features":
+            eng.codes_to_features(torch.tensor([[1, 2, bad]], dtype=torch.int64, device=eng.device))
+        else:
+            eng.decode_codes(torch.tensor([[1, bad, 3]], dtype=torch.int32, device=eng.device))
+        with pytest.raises(IndexError) as ei:
+            eng.check_errors()
+        assert isinstance(ei.value, LvxIndexError)
+        eng.check_errors()  # cleared
+    eng.decode_codes(torch.tensor([[0, 4095, 3]], dtype=torch.int32, device=eng.device))
+    eng.check_errors()  # the envelope self-check holds and in-range codes raise nothing
