@@ -670,12 +670,151 @@ static void gemm2_launch(GemmArgs g, hipStream_t s) {
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Skinny weight GEMM for the small decodes (bf16 mode, M <= SKINNY_MAX_M frames: the first dumps
+// and short single-stream chunks). C[M][N] = epi(A[M][K] . W[N][K]^T). One block owns 16 x NJ
+// weight rows and 16 x MI frames; its NWV waves take K in NWV slices, so a block's whole operand
+// volume is in flight at once instead of a k-loop of dependent round trips (the 64 x 64 tile ran
+// 3 k-tiles per split + a split-K combine). Operands go global -> registers directly in
+// v_mfma_f32_16x16x32_bf16 layout (A-operand = 16 weight rows, B-operand = 16 frames; lane l: row
+// l & 15, k + 8 (l >> 4)); KC 32-wide k-steps per register set, two sets in flight. The k-steps
+// per wave (S) are a template constant: the pipeline unrolls completely, no load is issued past
+// the slice and no load sits under a branch. The NWV wave partials are summed through LDS in wave
+// order (deterministic), then the epilogue.
+// ---------------------------------------------------------------------------------
+constexpr int SKINNY_MAX_M = 384;
+typedef float f32x4s __attribute__((ext_vector_type(4)));
+template <int AMODE, int EPI, typename TC, int MI, int NJ, int S, int NWV>
+__global__ __launch_bounds__(NWV * 64) void gemm_skinny_kernel(GemmArgs g) {
+  constexpr int KC = MI + NJ <= 2 ? 6 : 4;  // k-steps per register set (2 sets: <= 96 VGPRs of operands)
+  __shared__ float red[NWV][MI][16][16 * NJ + 1];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int n0 = blockIdx.x * 16 * NJ, m0 = blockIdx.y * 16 * MI;
+  const bf16_t* __restrict__ A = reinterpret_cast<const bf16_t*>(g.A);
+  const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(g.W);
+  const int kw0 = wave * S * 32;                 // first k of this wave's slice
+  const int kl = kw0 + 8 * (lane >> 4);          // + this lane's 8-element chunk
+  // this lane's weight rows and frames (clamped: rows past N / M are computed, never stored)
+  const bf16_t* wrow[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) wrow[j] = W + (size_t)min(n0 + j * 16 + (lane & 15), g.N - 1) * g.ldw + kl;
+  int fb[MI], ft[MI];  // A_CONV: (stream, frame) of the lane's frames; A_PLAIN: row
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int mc = min(m0 + i * 16 + (lane & 15), g.M - 1);
+    if (AMODE == A_CONV) { fb[i] = mc / g.L; ft[i] = mc - fb[i] * g.L; }
+    else { fb[i] = mc; ft[i] = 0; }
+  }
+  u32x4 wv[2][KC][NJ], av[2][KC][MI];
+  auto issue = [&](int set, int s0) {
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      const int st = s0 + c;
+      if (st >= S) break;  // compile-time after unrolling
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) g2_ldb(wv[set][c][j], wrow[j] + st * 32);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        if (AMODE == A_PLAIN) {
+          g2_ld(av[set][c][i], A + (size_t)fb[i] * g.lda + kl + st * 32, true);
+        } else {
+          const int kb = kw0 + st * 32;  // k of this step (uniform); a 32-wide step lies in one tap
+          const int tap = kb / g.cin, cc = kb - tap * g.cin + 8 * (lane >> 4);
+          const int tt = ft[i] + tap - (g.taps - 1) / 2;
+          g2_ld(av[set][c][i], A + ((size_t)fb[i] * g.L + min(max(tt, 0), g.L - 1)) * g.cin + cc, tt >= 0 && tt < g.L);
+        }
+      }
+    }
+  };
+  f32x4s acc[NJ][MI];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int i = 0; i < MI; ++i) acc[j][i] = f32x4s{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](int set, int s0) {
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      if (s0 + c >= S) break;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wv[set][c][j]),
+                                                              __builtin_bit_cast(bf16x8, av[set][c][i]), acc[j][i], 0, 0, 0);
+    }
+  };
+  issue(0, 0);
+  issue(1, KC);
+#pragma unroll
+  for (int s0 = 0; s0 < S; s0 += 2 * KC) {
+    mma(0, s0);
+    issue(0, s0 + 2 * KC);
+    mma(1, s0 + KC);
+    issue(1, s0 + 3 * KC);
+  }
+  // wave partials -> LDS: lane holds weight rows 4 (lane >> 4) + r of tile j, frame lane & 15
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wave][i][lane & 15][j * 16 + 4 * (lane >> 4) + r] = acc[j][i][r];
+  __syncthreads();
+  constexpr int NW = 16 * NJ;  // output columns per block
+#pragma unroll
+  for (int e0 = 0; e0 < MI * 16 * NW; e0 += NWV * 64) {
+    const int e = e0 + tid;
+    if (MI * 16 * NW % (NWV * 64) != 0 && e >= MI * 16 * NW) break;
+    const int i = e / (16 * NW), rm = (e / NW) % 16, cn = e % NW;
+    const int row = m0 + i * 16 + rm, col = n0 + cn;
+    const int rowc = min(row, g.M - 1), colc = min(col, g.N - 1);
+    float v = red[0][i][rm][cn];
+#pragma unroll
+    for (int w = 1; w < NWV; ++w) v += red[w][i][rm][cn];
+    const float bias = (EPI != E_SCALE && g.bias) ? g.bias[colc] : 0.f;
+    const float gam = (EPI == E_BIAS_GAMMA_RES) ? g.gamma[colc] : 0.f;
+    const float o = gemm_epi<EPI>(g, g.res, rowc, colc, v, bias, gam);
+    if (row < g.M && col < g.N) store_out<TC>(reinterpret_cast<TC*>(g.C) + (size_t)row * g.ldc + col, o);
+  }
+}
+
+template <int AMODE, int EPI, typename TC, int MI, int NJ, int NWV>
+static bool skinny_go(const GemmArgs& g, hipStream_t s) {
+  const dim3 grid((g.N + 16 * NJ - 1) / (16 * NJ), (g.M + 16 * MI - 1) / (16 * MI));
+  const int S = g.K / (32 * NWV);
+  if (g.K % (32 * NWV)) return false;
+  switch (S) {  // the codec's K: 768 (1x1 convs, head), 2,304 (pwconv2, k3 convs), 3,584 (embed k7)
+    case 3: hipLaunchKernelGGL((gemm_skinny_kernel<AMODE, EPI, TC, MI, NJ, 3, NWV>), grid, dim3(NWV * 64), 0, s, g); return true;
+    case 6: hipLaunchKernelGGL((gemm_skinny_kernel<AMODE, EPI, TC, MI, NJ, 6, NWV>), grid, dim3(NWV * 64), 0, s, g); return true;
+    case 9: hipLaunchKernelGGL((gemm_skinny_kernel<AMODE, EPI, TC, MI, NJ, 9, NWV>), grid, dim3(NWV * 64), 0, s, g); return true;
+    case 14: hipLaunchKernelGGL((gemm_skinny_kernel<AMODE, EPI, TC, MI, NJ, 14, NWV>), grid, dim3(NWV * 64), 0, s, g); return true;
+    case 18: hipLaunchKernelGGL((gemm_skinny_kernel<AMODE, EPI, TC, MI, NJ, 18, NWV>), grid, dim3(NWV * 64), 0, s, g); return true;
+    case 28: hipLaunchKernelGGL((gemm_skinny_kernel<AMODE, EPI, TC, MI, NJ, 28, NWV>), grid, dim3(NWV * 64), 0, s, g); return true;
+  }
+  return false;
+}
+// Tile shape by M, waves by K (tools/codec_probe.py, decode ms, skinny vs the 64 x 64 split-K /
+// 128 x 128 kernels it replaces): 1 x 10 frames 0.29 vs 0.45, 1 x 30 0.37 vs 0.53, 1 x 90 0.41 vs
+// 0.58, 1 x 256 0.56 vs 0.71, 2 x 160 0.57 vs 0.74; 1 x 480 0.87 vs 0.84 (the limit below).
+// 8 waves for K > 1,024 (a shorter chain per wave), 4 otherwise; 16 x 16 tiles at M <= 16, 32 x 16
+// up to 128, 32 x 32 above (measured at 90 and 256 against the other two and 64 x 32 / 32 x 64).
+template <int AMODE, int EPI, typename TC>
+static bool skinny_launch(const GemmArgs& g, hipStream_t s) {
+  const bool w8 = g.K > 1024;
+  if (g.M <= 16) return w8 ? skinny_go<AMODE, EPI, TC, 1, 1, 8>(g, s) : skinny_go<AMODE, EPI, TC, 1, 1, 4>(g, s);
+  if (g.M <= 128) return w8 ? skinny_go<AMODE, EPI, TC, 2, 1, 8>(g, s) : skinny_go<AMODE, EPI, TC, 2, 1, 4>(g, s);
+  return w8 ? skinny_go<AMODE, EPI, TC, 2, 2, 8>(g, s) : skinny_go<AMODE, EPI, TC, 2, 2, 4>(g, s);
+}
+int g_opt_codec_skinny = 1;  // 1: bf16 weight GEMMs with M <= SKINNY_MAX_M on gemm_skinny_kernel; 0: off (cross-check)
+
 // weight GEMMs: bf16 weights -> bf16 MFMA (gemm_bf16_kernel for large M); fp32 weights -> exact
 // fp32 MFMA (parity mode). TA / TC: activation types of the operand / output (bf16 only in bf16 mode)
 template <typename TW, typename TA, int AMODE, int EPI, typename TC = float>
 static void gemm_w(const GemmArgs& g, hipStream_t s) {
   if constexpr (sizeof(TW) == 2) {
     if (g.wscale) gemm2_launch<TA, fp8_t, AMODE, EPI, TC>(g, s);  // fp8 codec weights: any M
+    else if (sizeof(TA) == 2 && g_opt_codec_skinny && g.M <= SKINNY_MAX_M && skinny_launch<AMODE, EPI, TC>(g, s))
+      return;
     else if (g_opt_codec_g2 && g.M >= CODEC_G2_MIN_M) gemm2_launch<TA, bf16_t, AMODE, EPI, TC>(g, s);
     else gemm_launch<true, TA, bf16_t, AMODE, EPI, TC>(g, 1, s);
   } else {

@@ -2,8 +2,8 @@
 residual stream). No bit-exactness claim against the fp32 reference; the bar is a relative RMS
 error of the waveform, measured against the fp32 parity-mode engine (itself pinned to the
 reference's golden PCM by test_gpu_parity.py) and against the golden PCM directly. The large-M
-GEMM (gemm_bf16_kernel, 128x128 tiles) and the small-M GEMM must agree to bf16 summation-order
-noise.
+GEMM (gemm_bf16_kernel, 128x128 tiles), the small-M tile GEMM and the skinny GEMM (M <= 384)
+must agree to bf16 summation-order noise.
 """
 import os
 
@@ -64,6 +64,45 @@ def test_large_m_gemm_agrees_with_small_m_gemm(engs):
     finally:
         e16.set_option("codec_g2", 1)
     assert _rel_rms(big, small) < 5e-3
+
+
+@pytest.mark.parametrize("S,L", [(1, 10), (1, 30), (1, 90), (1, 256), (2, 160), (3, 100)])
+def test_skinny_gemm_close_to_fp32(engs, S, L):
+    """M = S x L <= 384: the codec's weight GEMMs run on gemm_skinny_kernel (K split over the
+    block's waves, A_CONV windows crossing stream boundaries at S > 1)"""
+    e16, e32 = engs
+    g = torch.Generator().manual_seed(S * 7 + L)
+    codes = torch.randint(0, 4096, (S, L), generator=g).to(e16.device)
+    p16 = e16.decode_codes(codes).cpu().numpy()
+    p32 = e32.decode_codes(codes).cpu().numpy()
+    for b in range(S):
+        assert _rel_rms(p16[b], p32[b]) < 0.02, b
+
+
+@pytest.mark.parametrize("S,L", [(1, 10), (1, 90), (2, 160)])
+def test_skinny_gemm_agrees_with_tile_kernels(engs, S, L):
+    e16, _ = engs
+    g = torch.Generator().manual_seed(11 + L)
+    codes = torch.randint(0, 4096, (S, L), generator=g).to(e16.device)
+    sk = e16.decode_codes(codes).cpu().numpy()
+    e16.set_option("codec_skinny", 0)
+    try:
+        tile = e16.decode_codes(codes).cpu().numpy()
+    finally:
+        e16.set_option("codec_skinny", 1)
+    assert _rel_rms(sk, tile) < 5e-3
+
+
+def test_bf16_streams_independent_small_m(engs):
+    """as below, on the skinny-GEMM path (M = 300: 32-frame tiles straddle the streams)"""
+    e16, _ = engs
+    g = torch.Generator().manual_seed(19)
+    codes = torch.randint(0, 4096, (3, 100), generator=g).to(e16.device)
+    a = e16.decode_codes(codes).cpu().numpy()
+    perm = [2, 0, 1]
+    b = e16.decode_codes(codes[perm]).cpu().numpy()
+    for i, p in enumerate(perm):
+        np.testing.assert_array_equal(b[i], a[p])
 
 
 def test_bf16_streams_independent(engs):
