@@ -24,6 +24,31 @@
 
 namespace lvx {
 
+// Development timeline of the batched step (tools/step_timeline.py; built only into the
+// LVX_TIMING library variant, `make timing`): thread 0 of every block of the instrumented
+// kernels records the 100 MHz real-time counter at entry, after its operands landed, and at
+// exit, plus the XCC / hardware-id registers, under (tag, layer, block).
+#ifdef LVX_TIMING
+constexpr int TS_BLOCKS = 1024;
+__device__ uint64_t g_lvx_ts[16 * 4 * TS_BLOCKS * 4];
+#define TS_DECL uint64_t ts_[2] = {0, 0}
+#define TS_MARK(i) do { if (threadIdx.x == 0) ts_[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define TS_SAVE(tag, layer, blk)                                                                    \
+  do {                                                                                               \
+    if (threadIdx.x == 0) {                                                                          \
+      const uint64_t te_ = __builtin_amdgcn_s_memrealtime();                                         \
+      const uint64_t hw_ = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |                    \
+                           ((uint64_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32);              \
+      uint64_t* p_ = g_lvx_ts + ((size_t)(((tag) * 4 + (layer)) * TS_BLOCKS + min((int)(blk), TS_BLOCKS - 1))) * 4; \
+      p_[0] = ts_[0]; p_[1] = ts_[1]; p_[2] = te_; p_[3] = hw_;                                      \
+    }                                                                                                \
+  } while (0)
+#else
+#define TS_DECL do {} while (0)
+#define TS_MARK(i) do {} while (0)
+#define TS_SAVE(tag, layer, blk) do {} while (0)
+#endif
+
 // ---------------------------------------------------------------------------------
 // GEMV family: out[b][n] = sum_k W[n][k] * in[b][k]   (W row-major [N][K], TW in {f32,bf16})
 //   IN  0: in = LayerNorm(x[b]) * ln_w            (eps 1e-5, no bias; src/model.py:37-38)
@@ -58,6 +83,7 @@ struct GemvArgs {
   const float* emb_row;  // drop-in row mode when non-null
   // fused MLP (ar_mlp_fused_kernel): its output sits in YCOPIES accumulators until c_proj folds it in
   float* yacc;           // non-null when the step runs the fused MLP
+  const float* gsum;     // batched c_fc (ar_mfma2_kernel XM 1): ArWeights::fc_gsum of the layer
   int add_y;             // c_proj: fold the accumulators into x (layers >= 1; 0 at layer 0 = just clear)
   int defer_sel;         // deferred greedy select (option "defer_select"). 1: B <= 2 GEMV step, lm_head
                          // publishes per-block granules, the next step's c_attn layer 0 reduces them;
@@ -871,7 +897,15 @@ template <> struct KvPiece<float> {
 };
 template <> struct KvPiece<bf16_t> {
   uint4 u;
-  __device__ __forceinline__ void load(const bf16_t* p) { u = *reinterpret_cast<const uint4*>(p); }
+  __device__ __forceinline__ void load(const bf16_t* p) {
+#ifdef LVX_KV_NT
+    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+    u = make_uint4(v.x, v.y, v.z, v.w);
+#else
+    u = *reinterpret_cast<const uint4*>(p);
+#endif
+  }
   __device__ __forceinline__ void get(float* v) const {
     v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
     v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
@@ -908,6 +942,8 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
   __shared__ float wo_s[NW][4][HD];  // [wave][16-lane row][part * 24 + i]
   const int sp = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  TS_DECL;
+  TS_MARK(0);
   // selcopy (layer 0 of a deferred-select step): the records c_attn just built are in the shadow
   // arrays; one block per row copies them back for the rest of the step and clears the flag
   // (the next text id, a dependent plan load, is looked up at the end of the block, when every
@@ -1012,8 +1048,10 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
 #pragma unroll
     for (int i = 0; i < 24; ++i) wo_s[wave][lane >> 4][(lane & 3) * 24 + i] = o[i];
   }
+  TS_MARK(1);
   if (lane == 0) { wm_s[wave] = m; wl_s[wave] = l; }
   __syncthreads();
+  TS_SAVE(2, layer, sp + gridDim.x * (head + N_HEAD * b));
   copy_tail();
   if (tid < HD) {
     float M = wm_s[0];
@@ -1165,6 +1203,8 @@ __global__ __launch_bounds__(256) void ar_rows_kernel(GemvArgs a) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int b = blockIdx.x * (blockDim.x >> 6) + wave;
   if (b >= a.B) return;
+  TS_DECL;
+  TS_MARK(0);
   float4 g[3], v[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) g[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
@@ -1183,10 +1223,12 @@ __global__ __launch_bounds__(256) void ar_rows_kernel(GemvArgs a) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = v[j];
   }
+  TS_MARK(1);
   wave_ln_regs(v, g);
   uint2* dst = reinterpret_cast<uint2*>(a.st.xn + (size_t)b * D);
 #pragma unroll
   for (int j = 0; j < 3; ++j) dst[j * 64 + lane] = pack4_bf16(v[j]);
+  TS_SAVE(a.N == VOCAB ? 8 : 0, a.layer, blockIdx.x);
 }
 
 // Batched deferred select (defer_sel 2): the previous step's greedy select of row b (the
@@ -1197,6 +1239,8 @@ __global__ __launch_bounds__(256) void ar_embed_select_kernel(GemvArgs a) {
   __shared__ float sv[4], sv2[4];
   __shared__ int si[4];
   const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  TS_DECL;
+  TS_MARK(0);
   int4 ri = a.st.rowinfo[b];
   const int2 rx = a.st.rowx[b];  // {plan step j, text id of step j + 1}
   const unsigned pend = a.st.selrow[b];
@@ -1217,6 +1261,7 @@ __global__ __launch_bounds__(256) void ar_embed_select_kernel(GemvArgs a) {
     bt = best_merge(bt, Best{lv[k].w, -INFINITY, i0 + 3});
   }
   bt = best_wave(bt);
+  TS_MARK(1);
   if (lane == 0) { sv[wave] = bt.v; sv2[wave] = bt.v2; si[wave] = bt.i; }
   __syncthreads();
   if (wave != 0) return;
@@ -1252,6 +1297,7 @@ __global__ __launch_bounds__(256) void ar_embed_select_kernel(GemvArgs a) {
   for (int j = 0; j < 3; ++j) dst[j * 64 + lane] = pack4_bf16(v[j]);
   // the plan load for the next text id last: waiting for it earlier held the embedding loads
   if (take && lane == 0) a.st.rowx[b] = make_int2(rx.x + 1, plan_tok(a.st, b, rx.x + 2));
+  TS_SAVE(7, 0, b);
 }
 
 // split-KV merge for the batched path: y[b] (bf16) into st.xn. NS = ns_max (the attention's split
@@ -1302,10 +1348,14 @@ static void launch_merge_bf16(const ArState& st, int B, int nsm, hipStream_t s) 
 
 // OUT as gemv_store, plus OUT 5: h (bf16) = gelu_tanh(v) for the batched mlp c_proj. A block
 // covers K columns starting at blockIdx.y * K of rows of length KTOT (KTOT > K: split K, OUT 6).
-// XM 1 (c_fc, option ln_stats): the operand is LayerNorm(x) built on the fly from the bf16 copy of
-// x and the per-row statistics the previous c_proj (OUT 7) left in 48 column-block partials
-// (mean, M2 over 16 columns each, combined here with Chan's formula): no separate rows kernel.
-// OUT 7 (c_proj): x += v, plus that bf16 copy and this block's (mean, M2) of its 16 columns.
+// XM 1 (c_fc): LayerNorm applied after the GEMM. The operand is the bf16 copy of x * ln_2.weight
+// the previous c_proj (OUT 7) left, multiplied as it is; the epilogue centres and scales:
+// LN2(x) . W^T = rstd * ((x * g) . W^T - mean * G[n]), G = ArWeights::fc_gsum, with (mean, rstd)
+// from the per-row statistics c_proj left in 48 column-block partials (mean, M2 over 16 columns
+// each, combined here with Chan's formula while the operands load): no rows kernel and no
+// per-element normalisation on the operand path (round 2: 4.1 -> ~2.7 us from entry to MFMA).
+// OUT 7 (c_proj): x += v, plus that bf16 copy (x * ln_2.weight) and this block's (mean, M2) of its
+// 16 columns.
 template <int K, int NT, int OUT, int KTOT = K, int XM = 0>
 __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   constexpr int NW = K / 192;  // waves per block, each a 192-wide K slice (6 MFMA k-steps)
@@ -1316,6 +1366,8 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   const int n0 = blockIdx.x * 16;
   const int r0 = blockIdx.z * (NT * 16);  // first batch row of this block's tile (grid.z batch tiles)
   const int B = a.B;
+  TS_DECL;
+  TS_MARK(0);
   const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(a.W);
   const bf16_t* __restrict__ X = XM == 1 ? a.st.xb : ((KTOT == 768) ? a.st.xn : a.st.hb);
   const int wrow = min(n0 + (lane & 15), a.N - 1);
@@ -1327,12 +1379,15 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   static_assert((NW * 64) % (NT * 16) == 0, "one batch row per thread in the epilogue");
   int4 ripre = make_int4(-1, 0, 0, 0);
   float xpre[OUT == 7 ? EPT : 1];
+  float gpre[(OUT == 7 || XM == 1) ? EPT : 1];  // OUT 7: ln_2.weight[n]; XM 1: G[n]
   if constexpr (OUT == 0) ripre = a.st.rowinfo[min(r0 + tid % (NT * 16), B - 1)];
-  if constexpr (OUT == 7) {
+  if constexpr (OUT == 7 || XM == 1) {
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
       const int e = min(tid + k * NW * 64, 16 * NT * 16 - 1), r = e / (NT * 16), b = e - r * (NT * 16);
-      xpre[k] = a.st.x[(size_t)min(r0 + b, B - 1) * D + min(n0 + r, a.N - 1)];
+      const int n = min(n0 + r, a.N - 1);
+      if constexpr (OUT == 7) xpre[k] = a.st.x[(size_t)min(r0 + b, B - 1) * D + n];
+      gpre[k] = OUT == 7 ? a.ln_w[n] : a.gsum[n];
     }
   }
   // XM 1: the row statistics partials first (vmcnt retires in issue order, so the Chan combine
@@ -1358,13 +1413,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   // every operand load in flight before the first MFMA (left to itself the scheduler interleaves
   // them with the MFMAs: ~7 KB in flight per wave instead of (6 + 6 NT) KB)
   __builtin_amdgcn_sched_barrier(0);
-  if constexpr (XM == 1) {
-    float4 g[6][2];
-#pragma unroll
-    for (int kk = 0; kk < 6; ++kk) {
-      g[kk][0] = *reinterpret_cast<const float4*>(a.ln_w + k0 + kk * 32);
-      g[kk][1] = *reinterpret_cast<const float4*>(a.ln_w + k0 + kk * 32 + 4);
-    }
+  if constexpr (XM == 1) {  // (mean, rstd) per batch row into rs (read in the epilogue)
     if (tid < NT * 16 * 4) {  // 4 lanes per row, 12 column blocks each (loaded above)
       const int rr = tid >> 2, q = tid & 3;
       const float2 (&p)[12] = sp;
@@ -1387,25 +1436,6 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
       }
       if (q == 0) rs[rr] = make_float2(mean, 1.0f / sqrtf(m2 * (1.0f / D) + 1e-5f));
     }
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const float2 st = rs[t * 16 + (lane & 15)];
-#pragma unroll
-      for (int kk = 0; kk < 6; ++kk) {
-        const uint4 u = xf[t][kk];
-        const float gv[8] = {g[kk][0].x, g[kk][0].y, g[kk][0].z, g[kk][0].w, g[kk][1].x, g[kk][1].y, g[kk][1].z, g[kk][1].w};
-        const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
-        uint32_t o4[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float lo = (__uint_as_float(w4[q] << 16) - st.x) * st.y * gv[2 * q];
-          const float hi = (__uint_as_float(w4[q] & 0xffff0000u) - st.x) * st.y * gv[2 * q + 1];
-          o4[q] = (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
-        }
-        xf[t][kk] = make_uint4(o4[0], o4[1], o4[2], o4[3]);
-      }
-    }
   }
   f32x4_t acc[NT];
 #pragma unroll
@@ -1416,6 +1446,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
     for (int t = 0; t < NT; ++t)
       acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[kk]),
                                                        __builtin_bit_cast(bf16x8_t, xf[t][kk]), acc[t], 0, 0, 0);
+  TS_MARK(1);
   // partial 16 x (NT*16) tiles -> LDS, element (row r, col c) at r * (NT*16) + c
 #pragma unroll
   for (int t = 0; t < NT; ++t)
@@ -1438,11 +1469,15 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
       const size_t idx = ((((size_t)a.layer * a.st.max_streams + ripre.x) * N_HEAD + head) * a.st.max_pos + ripre.y) * HD + d;
       store_kv(a, which, idx, v);
     } else if (OUT == 5) {
+      if constexpr (XM == 1) {  // LayerNorm after the GEMM: rstd * (v - mean * G[n])
+        const float2 st = rs[b - r0];
+        v = (v - st.x * gpre[k]) * st.y;
+      }
       a.st.hb[(size_t)b * DFF + n] = f32_to_bf16(gelu_tanh(v));
     } else if (OUT == 7) {
       const float xn = xpre[k] + v;
       a.st.x[(size_t)b * D + n] = xn;
-      a.st.xb[(size_t)b * D + n] = f32_to_bf16(xn);
+      a.st.xb[(size_t)b * D + n] = f32_to_bf16(xn * gpre[k]);
       xo[e] = xn;
     } else {
       gemv_store<OUT>(a, n, b, v);
@@ -1464,6 +1499,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
       reinterpret_cast<float2*>(a.st.xstat)[(size_t)(r0 + tid) * (D / 16) + blockIdx.x] = make_float2(mean, m2);
     }
   }
+  TS_SAVE(OUT == 0 ? 1 : OUT == 7 ? 3 : OUT == 5 ? 4 : OUT == 6 ? 5 : 6, a.layer, blockIdx.x + gridDim.x * blockIdx.y);
 }
 
 // measured alternatives to the batched v2 layout (round 1/2, us/step at B = 32, t = 256-512), removed:
@@ -1859,6 +1895,7 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       if (mf) {
         if (B > MFMA_LN_MAX) a.add_y = 0;  // ar_rows_kernel<4> of this layer's c_attn folded them
         if (nsm > 1) launch_merge_bf16(a.st, B, nsm, s);  // nsm == 1: the attention wrote xn itself
+        a.ln_w = w.ln2[l];  // OUT 7: the bf16 copy is x * ln_2.weight (c_fc's operand)
         if (B > MFMA_LN_MAX) launch_mfma2<768, 7>(a, s);  // + bf16 x and row statistics for c_fc
         else launch_mfma2<768, 1>(a, s);
       } else {
@@ -1875,7 +1912,8 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       } else if (mf && B <= MFMA_LN_MAX) {
         launch_mfma_ln<5, 0>(a, s);
       } else if (mf) {
-        launch_mfma2<768, 5, 1>(a, s);  // LayerNorm from c_proj's row statistics in the prologue
+        a.gsum = w.fc_gsum[l];
+        launch_mfma2<768, 5, 1>(a, s);  // LayerNorm from c_proj's row statistics, after the GEMM
       } else {
         launch_gemv<TW, 768, 1, 2, 0, 2>(a, s);
       }
@@ -2079,3 +2117,17 @@ void launch_codes_to_features(const float* codebook, const int64_t* codes, int B
 }
 
 }  // namespace lvx
+
+#ifdef LVX_TIMING
+// timing build only (tools/step_timeline.py): copy / clear the step timeline records
+extern "C" int lvx_debug_timeline(void* dst, size_t bytes, int clear) {
+  if (bytes > sizeof(lvx::g_lvx_ts)) bytes = sizeof(lvx::g_lvx_ts);
+  if (dst && hipMemcpyFromSymbol(dst, HIP_SYMBOL(lvx::g_lvx_ts), bytes) != hipSuccess) return -3;
+  if (clear) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(lvx::g_lvx_ts)) != hipSuccess) return -3;
+    if (hipMemset(p, 0, sizeof(lvx::g_lvx_ts)) != hipSuccess) return -3;
+  }
+  return (int)bytes;
+}
+#endif

@@ -334,8 +334,25 @@ int lvx_finalize(lvx_ctx* c) {
     UP_W(c->H(p + "attn.c_proj.weight"), w.w_aproj[i]);
     UP_W(c->H(p + "mlp.c_fc.weight"), w.w_fc[i]);
     UP_W(c->H(p + "mlp.c_proj.weight"), w.w_mproj[i]);
-    if (c->cfg.weight_dtype == LVX_DTYPE_BF16)  // thread-packed copy for the fused MLP (ar_mlp_fused_kernel)
+    if (c->cfg.weight_dtype == LVX_DTYPE_BF16) {  // thread-packed copy for the fused MLP (ar_mlp_fused_kernel)
       UP_W(pack_mproj(c->H(p + "mlp.c_proj.weight")), w.w_mproj_pk[i]);
+      // batched c_fc: LN2(x) . W^T = rstd * ((x * g) . W^T - mean * G), G[n] = sum_k g[k] W[n][k]
+      // over the bf16 weights the GEMM multiplies (double accumulation, rounded once)
+      const std::vector<float>& wf = c->H(p + "mlp.c_fc.weight");
+      const std::vector<float>& g2 = c->H(p + "ln_2.weight");
+      std::vector<float> gs(DFF);
+      for (int n = 0; n < DFF; ++n) {
+        double acc = 0.0;
+        for (int k = 0; k < D; ++k) {
+          const uint32_t hb = (uint32_t)f32_to_bf16(wf[(size_t)n * D + k]) << 16;
+          float wv;
+          std::memcpy(&wv, &hb, 4);
+          acc += (double)g2[k] * (double)wv;
+        }
+        gs[n] = (float)acc;
+      }
+      if ((r = c->upload_f32(gs, &w.fc_gsum[i]))) return r;
+    }
   }
   UP_F("transformer.ln_f.weight", w.lnf);
   UP_W(c->H("lm_head.weight"), w.w_lm);

@@ -33,6 +33,8 @@ struct ArWeights {
   const void* w_fc[N_LAYER] = {};     // [3072][768]
   const void* w_mproj[N_LAYER] = {};  // [768][3072]
   const void* w_mproj_pk[N_LAYER] = {};  // bf16 only: thread-packed copy for the fused MLP (pack_mproj)
+  const float* fc_gsum[N_LAYER] = {};    // bf16 only: G[n] = sum_k ln_2.weight[k] * bf16(c_fc W[n][k]) (batched
+                                         // c_fc: LayerNorm applied after the GEMM, ar_mfma2_kernel XM 1)
   const void* w_lm = nullptr;         // [4096][768]
 };
 

@@ -21,33 +21,41 @@ GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 BOUNDS = {("bf16", "bf16"): 0.03, ("bf16", "fp8"): 0.15}
 
 
-@pytest.mark.parametrize("wd,kvd", list(BOUNDS), ids=["bf16", "bf16-kvfp8"])
-def test_teacher_forced_256_steps(wd, kvd):
+# B: rows per step. B = 1 runs the single-stream kernels (configs[1]); B = 32 the batched MFMA path
+# of the bench's default workload (configs[2]); B = 8 the fp8-KV batched path of configs[4]. Every
+# row of a step gets the same teacher-forced history (its own slot), so all rows must also agree.
+@pytest.mark.parametrize("wd,kvd,B", [("bf16", "bf16", 1), ("bf16", "bf16", 32), ("bf16", "fp8", 1), ("bf16", "fp8", 8)],
+                         ids=["bf16-B1", "bf16-B32", "bf16-kvfp8-B1", "bf16-kvfp8-B8"])
+def test_teacher_forced_256_steps(wd, kvd, B):
     from llmvox_amd.engine import build_engine
     g = np.load(os.path.join(GOLDEN, "ar_golden.npz"))
     ids, margins, text = g["ids"], g["margins"], g["text_ids"].tolist()
     n = len(ids)
-    e = build_engine(0, wd, kvd, max_streams=1, max_positions=512, max_codec_frames=16)
+    e = build_engine(0, wd, kvd, max_streams=B, max_positions=512, max_codec_frames=16)
     dev = e.device
     try:
-        slots = torch.zeros(1, dtype=torch.int32, device=dev)
-        plan = torch.zeros(1, 2, dtype=torch.int32, device=dev)
-        rowstep = torch.zeros(1, dtype=torch.int32, device=dev)
-        tok = torch.zeros(1, 2, dtype=torch.int32, device=dev)
-        marg = torch.zeros(1, 2, dtype=torch.float32, device=dev)
-        picks, gm, kept = [], [], {}
+        slots = torch.arange(B, dtype=torch.int32, device=dev)
+        plan = torch.zeros(B, 2, dtype=torch.int32, device=dev)
+        rowstep = torch.zeros(B, dtype=torch.int32, device=dev)
+        tok = torch.zeros(B, 2, dtype=torch.int32, device=dev)
+        marg = torch.zeros(B, 2, dtype=torch.float32, device=dev)
+        picks, gm, kept, rows_ok = [], [], {}, True
         keep = g["logit_steps"].tolist()
         for i in range(n):
-            e.set_slot(0, i, int(ids[i - 1]) if i > 0 else 0)
+            for b in range(B):
+                e.set_slot(b, i, int(ids[i - 1]) if i > 0 else 0)
             plan.fill_(text[i] if i < len(text) else 384)
             rowstep.zero_()
             e.ar_steps(1, slots, plan, rowstep, tok, marg)
             if i in keep:
-                kept[i] = e.last_logits(1)[0].cpu().numpy()
-            picks.append(tok[0, 0].clone())
+                lg = e.last_logits(B).cpu().numpy()
+                kept[i] = lg[0]
+                rows_ok &= bool(np.abs(lg - lg[0]).max() < 1e-5)
+            picks.append(tok[:, 0].clone())
             gm.append(marg[0, 0].clone())
         e.check_errors()
-        picks = torch.stack(picks).cpu().numpy()
+        allp = torch.stack(picks).cpu().numpy()  # [n][B]
+        picks = allp[:, 0]
         gm = torch.stack(gm).cpu().numpy()
     finally:
         e.close()
@@ -55,11 +63,12 @@ def test_teacher_forced_256_steps(wd, kvd):
     err = max(float(np.abs(kept[s] - g["logits"][k]).max()) for k, s in enumerate(keep))
     agree = float((picks == ids).mean())
     must = margins > 2 * bound
-    print(f"\n[teacher-forced {wd}/kv {kvd}] agreement {agree:.4f} over {n} steps; "
+    print(f"\n[teacher-forced {wd}/kv {kvd} B={B}] agreement {agree:.4f} over {n} steps; "
           f"max |dlogit| at recorded steps {err:.4g} (bound {bound}); steps with margin > {2 * bound}: "
           f"{int(must.sum())}, mismatches there: {int((picks != ids)[must].sum())}; "
           f"mismatch steps {np.nonzero(picks != ids)[0].tolist()} (golden margins "
           f"{[round(float(margins[k]), 4) for k in np.nonzero(picks != ids)[0]]})")
     assert err < bound
+    assert rows_ok and (allp == allp[:, :1]).all(), "rows with the same history disagree"
     np.testing.assert_array_equal(picks[must], ids[must])
     assert agree >= 0.95
