@@ -924,6 +924,10 @@ template <> struct KvPiece<fp8_t> {
   }
 };
 
+// (round 2, measured slower: keys stored in piece-major groups of 16 so that a 16-lane row reads
+// one piece of 16 consecutive keys, 256 B contiguous per row and 8 lines per wave-instruction
+// instead of 24: B = 32 10.83 vs 10.22 us at t = 512, 30.9 vs 29.95 at t = 2,048; every line of a
+// wave's 3 KB key run is requested by its first load either way)
 // No LDS in the key loop: a block walks its key range in 64-key
 // tiles; lane quad (tid/4) owns one key per tile and lane tid%4 owns 24 of its 96 dims: the K and
 // V pieces (48 B bf16 each) load straight to registers, the score needs two quad shuffles, and
@@ -1508,9 +1512,12 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
 // the split mlp c_proj combined in-launch by each column tile's last arriving slice (release /
 // acquire fences: 182 vs 157; write-through slabs and sc1 loads, no fences: 171.9 vs 162-168)
 template <int K, int OUT, int XM = 0>
-static void launch_mfma2(const GemvArgs& a, hipStream_t s) {
+static void launch_mfma2(const GemvArgs& a, hipStream_t s, bool btile = false) {
   dim3 grid((a.N + 15) / 16), block((K / 192) * 64);
-  if (a.B <= 16) hipLaunchKernelGGL((ar_mfma2_kernel<K, 1, OUT, K, XM>), grid, block, 0, s, a);
+  if (btile && a.B > 16) {  // 16-row batch tiles in grid.z: half the operand bytes per block
+    grid.z = (a.B + 15) / 16;
+    hipLaunchKernelGGL((ar_mfma2_kernel<K, 1, OUT, K, XM>), grid, block, 0, s, a);
+  } else if (a.B <= 16) hipLaunchKernelGGL((ar_mfma2_kernel<K, 1, OUT, K, XM>), grid, block, 0, s, a);
   else if (a.B <= 32) hipLaunchKernelGGL((ar_mfma2_kernel<K, 2, OUT, K, XM>), grid, block, 0, s, a);
   else hipLaunchKernelGGL((ar_mfma2_kernel<K, 4, OUT, K, XM>), grid, block, 0, s, a);
 }
@@ -1758,6 +1765,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_bt_kernel(GemvArgs a) {
 // time of these short GEMMs: B = 8 / 16 / 32 v2 149 / 162 / 191 vs v3 172 / 181 / 203 (16-row
 // tiles, separate merge); a fused merge re-reads ns_max partials per row and block: 271 / 302 / 266.
 // v3 therefore runs only where v2 has no kernels (32 < B <= 64: 250 us, 16-row tiles).
+int g_opt_exp = 0;  // development A/B bits (lvx_set_option "exp"), 0 = production kernels
 int g_opt_bt = 1;  // 1: batched path v3 for 32 < B <= 64; 2: v3 for every batched B (cross-check of v2); 0: off
 
 template <int K, int IN, int OUT>
@@ -1896,7 +1904,9 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
         if (B > MFMA_LN_MAX) a.add_y = 0;  // ar_rows_kernel<4> of this layer's c_attn folded them
         if (nsm > 1) launch_merge_bf16(a.st, B, nsm, s);  // nsm == 1: the attention wrote xn itself
         a.ln_w = w.ln2[l];  // OUT 7: the bf16 copy is x * ln_2.weight (c_fc's operand)
-        if (B > MFMA_LN_MAX) launch_mfma2<768, 7>(a, s);  // + bf16 x and row statistics for c_fc
+        // + bf16 x and row statistics for c_fc; 16-row batch tiles (B = 32: 96 blocks of 49 KB operands
+        // instead of 48 of 74 KB: -3.4 us/step at t = 512-1,151)
+        if (B > MFMA_LN_MAX) launch_mfma2<768, 7>(a, s, true);
         else launch_mfma2<768, 1>(a, s);
       } else {
         launch_gemv<TW, 768, 1, 1, 2, 1>(a, s);
