@@ -671,6 +671,187 @@ static void gemm2_launch(GemmArgs g, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------------
+// bf16 weight GEMM for the batched chunk decodes (M >= ~2,048 frames, bf16 operands and weights):
+// operands staged by LDS-DMA (global_load_lds_dwordx4: no register staging, no ds_write pass) into
+// two LDS stages (the DMA of k-tile kt+1 in flight while kt is multiplied; raw s_barrier, a
+// __syncthreads() would drain the DMAs), one barrier per k-tile, both k32 sub-steps' fragments
+// read before the first MFMA. Block tile 128 x 192, BK 64, 8 waves in 2 (M) x 4 (N), each 64 x 48 =
+// 4 x 3 v_mfma_f32_16x16x32_bf16 accumulators. With >= 2 tiles per CU: 2 stages = 80 KB of LDS,
+// two blocks per CU (the other block's
+// MFMAs cover a block's barrier / fragment-read / epilogue phases: tools/gemm_ubench.hip measured the
+// fragment reads and barriers of one lock-stepped block, not the MFMAs or the DMA, as its time);
+// with fewer tiles, 3 stages (120 KB, the DMA of k-tile kt+2 in flight) and one block per CU.
+// 128 x 192 divides the codec's shapes at 8,192 frames evenly over the 256 CUs: N = 768 -> 256
+// tiles, N = 2,304 -> 768. LDS image: [row][64 k] bf16 (128-B rows, one DMA instruction = 8 rows),
+// 16-B segment s of row r stored in slot s ^ (r & 7) (swizzled through the per-lane SOURCE address;
+// each ds_read_b128 lane group then hits 16 distinct 4-bank groups: conflict-free). Conv padding
+// rows are DMA'd from a zero granule. Rows past M / N are clamped (never stored).
+// ---------------------------------------------------------------------------------
+constexpr int G3_BM = 128, G3_BN = 192, G3_BK = 64;
+constexpr int G3_ABYTES = G3_BM * G3_BK * 2, G3_BBYTES = G3_BN * G3_BK * 2, G3_STAGE = G3_ABYTES + G3_BBYTES;
+constexpr int G3_AP = G3_BM / 8 / 8, G3_BP = G3_BN / 8 / 8;  // 1-KB DMA pieces per wave per k-tile (A, B)
+static_assert(2 * 2 * G3_STAGE <= 160 * 1024 && 3 * G3_STAGE <= 160 * 1024, "LDS stages");
+__device__ __attribute__((aligned(16))) uint32_t g3_zero[4];
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void glds16(const void* src, unsigned char* lds) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+template <int AMODE, int EPI, typename TC, int NS>
+__global__ __launch_bounds__(512, NS == 2 ? 2 : 1) void gemm_glds_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[NS * G3_STAGE];  // the only LDS object
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 2, wn = wave & 3;
+  // XCD-aware tile order (as gemm_bf16_kernel): an XCD's blocks walk 8 M-tiles down an N column
+  const int ntn = gridDim.x, ntm = gridDim.y, T = ntn * ntm;
+  const int pid = blockIdx.x + ntn * blockIdx.y;
+  const int q = (T & 7) == 0 ? (pid & 7) * (T >> 3) + (pid >> 3) : pid;
+  const int gsz = 8 * ntn, grp = q / gsz, within = q - grp * gsz;
+  const int gm = min(8, ntm - grp * 8);
+  const int m0 = (grp * 8 + within % gm) * G3_BM, n0 = (within / gm) * G3_BN;
+  const bf16_t* __restrict__ A = reinterpret_cast<const bf16_t*>(g.A);
+  const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(g.W);
+  const int nkt = g.K / G3_BK;  // K % 64 == 0 (checked by the launcher)
+  // DMA geometry: lane -> row lane / 8 of a 1-KB piece, LDS slot lane % 8 <- global segment gseg
+  const int lrow = lane >> 3, gseg = (lane & 7) ^ lrow;
+  const bf16_t* bsrc[G3_BP];
+#pragma unroll
+  for (int i = 0; i < G3_BP; ++i) {
+    const int n = min(n0 + (wave * G3_BP + i) * 8 + lrow, g.N - 1);  // rows past N: never stored
+    bsrc[i] = W + (size_t)n * g.ldw + gseg * 8;
+  }
+  const bf16_t* asrc[G3_AP];
+  int cb[G3_AP], ct[G3_AP];
+#pragma unroll
+  for (int i = 0; i < G3_AP; ++i) {
+    const int m = min(m0 + (wave * G3_AP + i) * 8 + lrow, g.M - 1);  // rows past M: never stored
+    asrc[i] = A + (size_t)m * g.lda + gseg * 8;
+    cb[i] = AMODE == A_CONV ? m / g.L : 0;
+    ct[i] = m - cb[i] * g.L;
+  }
+  auto issue = [&](int kt, int st) {
+    unsigned char* sa = smem + st * G3_STAGE;
+    unsigned char* sb = sa + G3_ABYTES;
+    const int kb = kt * G3_BK;
+#pragma unroll
+    for (int i = 0; i < G3_AP; ++i) {
+      const void* src;
+      if (AMODE == A_PLAIN) {
+        src = asrc[i] + kb;
+      } else {  // implicit conv: a 64-wide k-tile lies in one tap; padding rows from the zero granule
+        const int tap = kb / g.cin, c = kb - tap * g.cin + gseg * 8;
+        const int tt = ct[i] + tap - (g.taps - 1) / 2;
+        src = (tt >= 0 && tt < g.L) ? (const void*)(A + ((size_t)cb[i] * g.L + tt) * g.cin + c) : (const void*)g3_zero;
+      }
+      glds16(src, sa + (wave * G3_AP + i) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < G3_BP; ++i) glds16(bsrc[i] + kb, sb + (wave * G3_BP + i) * 1024);
+  };
+
+  f32x4v acc[4][3];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  // fragment addresses: lane l reads row (l & 15) of a 16-row sub-tile, segment kk / 8 + (l >> 4)
+  const int frow = lane & 15, fseg = lane >> 4, fsw = lane & 7;
+  const int kl = nkt - 1;
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p) issue(min(p, kl), p);
+  for (int kt = 0; kt < nkt; ++kt) {
+    // this wave's DMAs of tile kt have landed (the NS - 2 later tiles' stay in flight); after the
+    // barrier every wave's have, and every wave is done reading the stage (tile kt - 1) that tile
+    // kt + NS - 1 now goes to (clamped: the tail re-loads the last tile, never read)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * (G3_AP + G3_BP)) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(min(kt + NS - 1, kl), (kt + NS - 1) % NS);
+    const unsigned char* sa = smem + (kt % NS) * G3_STAGE;
+    const unsigned char* sb = sa + G3_ABYTES;
+    // both k32 sub-steps' fragments issued before the first MFMA
+    bf16x8 fa[2][4], fb[2][3];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int slot = ((kk * 4 + fseg) ^ fsw) * 16;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        fa[kk][i] = *reinterpret_cast<const bf16x8*>(sa + (wm * 64 + i * 16 + frow) * 128 + slot);
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        fb[kk][j] = *reinterpret_cast<const bf16x8*>(sb + (wn * 48 + j * 16 + frow) * 128 + slot);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[kk][j], acc[i][j], 0, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail DMAs
+  // epilogue: acc[i][j][e] = C[m0 + wm*64 + i*16 + 4*(lane >> 4) + e][n0 + wn*48 + j*16 + (lane & 15)];
+  // every operand in flight at once (one round trip; rows / columns clamped, no branch)
+  TC* C = reinterpret_cast<TC*>(g.C);
+  float bias[3], gam[3], rv[3][4][4];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int colc = min(n0 + wn * 48 + j * 16 + (lane & 15), g.N - 1);
+    bias[j] = g.bias ? g.bias[colc] : 0.f;
+    gam[j] = (EPI == E_BIAS_GAMMA_RES) ? g.gamma[colc] : 0.f;
+    if constexpr (EPI == E_BIAS_GAMMA_RES || EPI == E_BIAS_RES) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          rv[j][i][e] = g.res[(size_t)min(m0 + wm * 64 + i * 16 + 4 * (lane >> 4) + e, g.M - 1) * g.ldr + colc];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int col = n0 + wn * 48 + j * 16 + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row0 = m0 + wm * 64 + i * 16 + 4 * (lane >> 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v = acc[i][j][e] + bias[j];
+        float o;
+        if constexpr (EPI == E_BIAS) o = v;
+        else if constexpr (EPI == E_BIAS_GELU) o = gelu_erf(v);
+        else if constexpr (EPI == E_BIAS_GAMMA_RES) o = rv[j][i][e] + gam[j] * v;
+        else o = rv[j][i][e] + v;
+        acc[i][j][e] = o;
+        asm volatile("" : "+v"(acc[i][j][e]));
+      }
+      if (col < g.N) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (row0 + e < g.M) store_out<TC>(C + (size_t)(row0 + e) * g.ldc + col, acc[i][j][e]);
+      }
+    }
+  }
+}
+
+int g_opt_codec_g3 = 1;  // 1: large-M bf16 GEMMs on gemm_glds_kernel; 0: off (cross-check)
+// the LDS-DMA kernel needs enough 128 x 192 tiles to fill the chip
+static bool g3_ok(const GemmArgs& g) {
+  return g_opt_codec_g3 && g.K % G3_BK == 0 && ((g.M + G3_BM - 1) / G3_BM) * ((g.N + G3_BN - 1) / G3_BN) >= 192;
+}
+template <int AMODE, int EPI, typename TC>
+static void g3_launch(GemmArgs g, hipStream_t s) {
+  static_assert(EPI != E_SCALE, "weight GEMMs only");
+  dim3 grid((g.N + G3_BN - 1) / G3_BN, (g.M + G3_BM - 1) / G3_BM);
+  // more tiles than CUs: two blocks per CU (2 stages, 80 KB each), else one (3 stages, 120 KB).
+  // Kernel traces of the 32 x 256-frame decode: N = 2,304 (768 tiles) 52.5 vs 61 us, N = 768 (256
+  // tiles) 40.4 vs 47 us; 16 x 256 frames (N = 2,304: 384 tiles) 1.57 vs 1.70 ms per decode
+  if (grid.x * grid.y > 256) hipLaunchKernelGGL((gemm_glds_kernel<AMODE, EPI, TC, 2>), grid, dim3(512), 0, s, g);
+  else hipLaunchKernelGGL((gemm_glds_kernel<AMODE, EPI, TC, 3>), grid, dim3(512), 0, s, g);
+}
+
+// ---------------------------------------------------------------------------------
 // Skinny weight GEMM for the small decodes (bf16 mode, M <= SKINNY_MAX_M frames: the first dumps
 // and short single-stream chunks). C[M][N] = epi(A[M][K] . W[N][K]^T). One block owns 16 x NJ
 // weight rows and 16 x MI frames; its NWV waves take K in NWV slices, so a block's whole operand
@@ -815,6 +996,7 @@ static void gemm_w(const GemmArgs& g, hipStream_t s) {
     if (g.wscale) gemm2_launch<TA, fp8_t, AMODE, EPI, TC>(g, s);  // fp8 codec weights: any M
     else if (sizeof(TA) == 2 && g_opt_codec_skinny && g.M <= SKINNY_MAX_M && skinny_launch<AMODE, EPI, TC>(g, s))
       return;
+    else if (sizeof(TA) == 2 && EPI != E_SCALE && g3_ok(g)) g3_launch<AMODE, (EPI == E_SCALE ? E_BIAS : EPI), TC>(g, s);
     else if (g_opt_codec_g2 && g.M >= CODEC_G2_MIN_M) gemm2_launch<TA, bf16_t, AMODE, EPI, TC>(g, s);
     else gemm_launch<true, TA, bf16_t, AMODE, EPI, TC>(g, 1, s);
   } else {

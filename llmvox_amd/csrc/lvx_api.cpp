@@ -557,6 +557,7 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   else if (n == "bt") g_opt_bt = std::min(std::max(value, 0), 2);
   else if (n == "codec_g2") g_opt_codec_g2 = value != 0;
   else if (n == "codec_skinny") g_opt_codec_skinny = value != 0;
+  else if (n == "codec_g3") g_opt_codec_g3 = value != 0;
   else if (n == "exp") g_opt_exp = value;
   else return fail(LVX_E_NAME, "unknown option " + n);
   g_opt_epoch.fetch_add(1);  // every context's captured kernels change (checked in cached_graph)

@@ -17,7 +17,7 @@ constexpr int NSPLIT = 16;  // max KV splits per (stream, head) in decode attent
 #endif
 constexpr int YCOPIES = LVX_YCOPIES;  // accumulator copies of the fused MLP (spreads atomic contention)
 constexpr int LM_MAX_BLOCKS = 1024;  // lm_head blocks of the fused argmax tail (4096 rows / 8 per block = 512)
-extern int g_opt_defer_select, g_opt_fuse_mlp, g_opt_bt, g_opt_codec_g2, g_opt_codec_skinny, g_opt_exp;  // cross-check switches (lvx_set_option)
+extern int g_opt_defer_select, g_opt_fuse_mlp, g_opt_bt, g_opt_codec_g2, g_opt_codec_skinny, g_opt_codec_g3, g_opt_exp;  // cross-check switches (lvx_set_option)
 
 // Device-resident AR weights. Matrices are [out][in] row-major (torch Linear layout),
 // in the context's weight dtype; vectors and gathered tables are fp32.

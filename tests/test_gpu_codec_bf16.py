@@ -66,6 +66,27 @@ def test_large_m_gemm_agrees_with_small_m_gemm(engs):
     assert _rel_rms(big, small) < 5e-3
 
 
+@pytest.mark.parametrize("S,L", [(16, 256), (5, 700)])
+def test_lds_dma_gemm_agrees_with_register_staged_gemm(engs, S, L):
+    """gemm_glds_kernel (LDS-DMA staging, 128 x 192 tiles, 16x16x32 MFMA; M >= ~4,096 frames, and
+    the N = 2,304 GEMMs from ~2,048) against gemm_bf16_kernel (register staging, 32x32x16 MFMA):
+    the same bf16 products, summed in another order. (5, 700): M = 3,500, a partial last M tile
+    and A_CONV windows crossing stream boundaries inside a tile."""
+    e16, e32 = engs
+    g = torch.Generator().manual_seed(S + L)
+    codes = torch.randint(0, 4096, (S, L), generator=g).to(e16.device)
+    dma = e16.decode_codes(codes).cpu().numpy()
+    e16.set_option("codec_g3", 0)
+    try:
+        reg = e16.decode_codes(codes).cpu().numpy()
+    finally:
+        e16.set_option("codec_g3", 1)
+    assert _rel_rms(dma, reg) < 5e-3
+    p32 = e32.decode_codes(codes[:2]).cpu().numpy()
+    for b in range(2):
+        assert _rel_rms(dma[b], p32[b]) < 0.02, b
+
+
 @pytest.mark.parametrize("S,L", [(1, 10), (1, 30), (1, 90), (1, 256), (2, 160), (3, 100)])
 def test_skinny_gemm_close_to_fp32(engs, S, L):
     """M = S x L <= 384: the codec's weight GEMMs run on gemm_skinny_kernel (K split over the

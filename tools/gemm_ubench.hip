@@ -1,0 +1,157 @@
+// Development micro-benchmark of the codec's large-M GEMM structure (gemm_glds_kernel in
+// codec_kernels.hip): LDS-DMA staged bf16 GEMM C[M][N] = A[M][K] . W[N][K]^T, fp32 out, 8 waves
+// (2 x 4), 16x16x32 MFMA, NS-deep LDS ring. Switches isolate the memory pipeline (no MFMA) and the
+// compute pipeline (no DMA after the prologue) so their rates can be compared with the full loop.
+// hipcc -O3 --offload-arch=gfx950 tools/gemm_ubench.hip -o tools/gemm_ubench && tools/gemm_ubench
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void glds16(const void* src, unsigned char* lds) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+// MODE bit 0: no MFMA, bit 1: no DMA in the loop, bit 2: s_setprio(1) around the MFMAs, bit 3: no
+// output stores (kept live by an impossible condition), bit 4: no fragment reads, bit 5: fragment
+// reads of the next k32 sub-step issued before the MFMAs of this one (software pipeline)
+template <int BM, int BN, int NS, int MODE, int WV = 8, int OCC = 1>
+__global__ __launch_bounds__(WV * 64, OCC) void k_gemm(const unsigned short* __restrict__ A, const unsigned short* __restrict__ W,
+                                                 float* __restrict__ C, int M, int N, int K) {
+  constexpr int WNN = WV / 2, STAGE = (BM + BN) * 128, AP = BM / 8 / WV, BP = BN / 8 / WV, MI = BM / 32, NJ = BN / WNN / 16;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[NS * STAGE];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, wm = wave / WNN, wn = wave % WNN;
+  const int ntn = gridDim.x, ntm = gridDim.y, T = ntn * ntm, pid = blockIdx.x + ntn * blockIdx.y;
+  const int q = (T & 7) == 0 ? (pid & 7) * (T >> 3) + (pid >> 3) : pid;
+  const int gsz = 8 * ntn, grp = q / gsz, within = q - grp * gsz, gm = min(8, ntm - grp * 8);
+  const int m0 = (grp * 8 + within % gm) * BM, n0 = (within / gm) * BN;
+  const int lrow = lane >> 3, gseg = (lane & 7) ^ lrow, nkt = K / 64;
+  const unsigned short* as[AP];
+  const unsigned short* bs[BP];
+  for (int i = 0; i < AP; ++i) as[i] = A + (size_t)min(m0 + (wave * AP + i) * 8 + lrow, M - 1) * K + gseg * 8;
+  for (int i = 0; i < BP; ++i) bs[i] = W + (size_t)min(n0 + (wave * BP + i) * 8 + lrow, N - 1) * K + gseg * 8;
+  auto issue = [&](int kt, int st) {
+    unsigned char* sa = smem + st * STAGE;
+    unsigned char* sb = sa + BM * 128;
+#pragma unroll
+    for (int i = 0; i < AP; ++i) glds16(as[i] + kt * 64, sa + (wave * AP + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < BP; ++i) glds16(bs[i] + kt * 64, sb + (wave * BP + i) * 1024);
+  };
+  f32x4 acc[MI][NJ];
+  for (int i = 0; i < MI; ++i)
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
+  const int frow = lane & 15, fseg = lane >> 4, fsw = lane & 7, kl = nkt - 1;
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p) issue(min(p, kl), p);
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (MODE & 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * (AP + BP)) : "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (!(MODE & 2)) issue(min(kt + NS - 1, kl), (kt + NS - 1) % NS);
+    const unsigned char* sa = smem + (kt % NS) * STAGE;
+    const unsigned char* sb = sa + BM * 128;
+    auto rd = [&](int kk, bf16x8* fa, bf16x8* fb) {
+      const int slot = ((kk * 4 + fseg) ^ fsw) * 16;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+        fa[i] = (MODE & 16) ? bf16x8{} + (__bf16)(float)(kt + i) : *reinterpret_cast<const bf16x8*>(sa + (wm * (BM / 2) + i * 16 + frow) * 128 + slot);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        fb[j] = (MODE & 16) ? bf16x8{} + (__bf16)(float)(kt - j) : *reinterpret_cast<const bf16x8*>(sb + (wn * (BN / WNN) + j * 16 + frow) * 128 + slot);
+    };
+    auto mm = [&](const bf16x8* fa, const bf16x8* fb) {
+      if (MODE & 4) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          if (MODE & 1) {
+            acc[i][j][0] += (float)fa[i][0] * (float)fb[j][0];
+          } else {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+          }
+        }
+      if (MODE & 4) __builtin_amdgcn_s_setprio(0);
+    };
+    if (MODE & 32) {
+      bf16x8 fa0[MI], fb0[NJ], fa1[MI], fb1[NJ];
+      rd(0, fa0, fb0);
+      rd(1, fa1, fb1);
+      mm(fa0, fb0);
+      mm(fa1, fb1);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 fa[MI], fb[NJ];
+        rd(kk, fa, fb);
+        mm(fa, fb);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int i = 0; i < MI; ++i)
+    for (int j = 0; j < NJ; ++j) {
+      const int col = n0 + wn * (BN / WNN) + j * 16 + (lane & 15);
+      for (int e = 0; e < 4; ++e) {
+        const int row = m0 + wm * (BM / 2) + i * 16 + 4 * (lane >> 4) + e;
+        if ((MODE & 8) && acc[i][j][e] != -1.2345f) continue;
+        if (row < M && col < N) C[(size_t)row * N + col] = acc[i][j][e];
+      }
+    }
+}
+
+template <int BM, int BN, int NS, int MODE, int WV = 8, int OCC = 1>
+void run(const char* name, const unsigned short* A, const unsigned short* W, float* C, int M, int N, int K) {
+  dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM);
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((k_gemm<BM, BN, NS, MODE, WV, OCC>), grid, dim3(WV * 64), 0, 0, A, W, C, M, N, K);
+  CK(hipEventRecord(a, 0));
+  const int reps = 20;
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((k_gemm<BM, BN, NS, MODE, WV, OCC>), grid, dim3(WV * 64), 0, 0, A, W, C, M, N, K);
+  CK(hipEventRecord(b, 0));
+  CK(hipEventSynchronize(b));
+  float ms;
+  CK(hipEventElapsedTime(&ms, a, b));
+  const double us = ms * 1e3 / reps;
+  printf("M %d N %4d K %4d %-22s occ %d waves %d tile %dx%d NS %d mode %2d: %7.1f us %7.1f TFLOP/s\n", M, N, K, name, OCC, WV, BM, BN, NS, MODE, us,
+         2.0 * M * N * K / us / 1e6);
+}
+
+int main() {
+  const int M = 8192;
+  unsigned short *A, *W;
+  float* C;
+  CK(hipMalloc(&A, (size_t)M * 3584 * 2));
+  CK(hipMalloc(&W, (size_t)2304 * 3584 * 2));
+  CK(hipMalloc(&C, (size_t)M * 2304 * 4));
+  std::vector<unsigned short> h((size_t)M * 3584);
+  for (size_t i = 0; i < h.size(); ++i) h[i] = 0x3c00 + (unsigned short)((i * 2654435761u >> 7) & 0xff);  // ~[0.0078, 0.016)
+  CK(hipMemcpy(A, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+  CK(hipMemcpy(W, h.data(), (size_t)2304 * 3584 * 2, hipMemcpyHostToDevice));
+  const int shapes[2][2] = {{768, 2304}, {2304, 768}};
+  for (auto& s : shapes) {
+    const int N = s[0], K = s[1];
+    run<128, 192, 3, 0>("full", A, W, C, M, N, K);
+    run<128, 192, 3, 32>("pipelined reads", A, W, C, M, N, K);
+    run<128, 192, 3, 36>("pipelined + setprio", A, W, C, M, N, K);
+    run<128, 192, 3, 43>("pipelined reads only", A, W, C, M, N, K);
+    run<128, 192, 2, 0, 8, 2>("full", A, W, C, M, N, K);
+    run<128, 192, 2, 32, 8, 2>("pipelined reads", A, W, C, M, N, K);
+    run<128, 128, 2, 32, 8, 2>("pipelined reads", A, W, C, M, N, K);
+    run<128, 128, 3, 32, 8, 2>("pipelined reads", A, W, C, M, N, K);
+    run<128, 256, 2, 32, 8, 2>("pipelined reads", A, W, C, M, N, K);
+    run<128, 192, 2, 32, 4, 2>("pipelined reads", A, W, C, M, N, K);
+  }
+  return 0;
+}
