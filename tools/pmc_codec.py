@@ -1,11 +1,11 @@
-"""MFMA utilisation of the codec's large GEMM (gemm_bf16_kernel) from a rocprofv3 --pmc pass.
+"""MFMA utilisation of the codec's large-M GEMMs (gemm_glds_kernel, gemm_bf16_kernel) from a
+rocprofv3 --pmc pass.
 
 usage: python tools/pmc_codec.py COUNTER_CSV KEY [OUT_JSON]
 
 The pass collects SQ_VALU_MFMA_BUSY_CYCLES and GRBM_GUI_ACTIVE (one SQ and one GRBM slot) over
-bench.py, whose codec calls all decode the same S x chunk frames. Over every gemm_bf16_kernel
-dispatch: busy = sum of SQ_VALU_MFMA_BUSY_CYCLES (MFMA-busy cycles summed over the SIMDs: 32 per
-v_mfma_f32_32x32x16_bf16, MI355X_MICROARCH.md), active = sum of GRBM_GUI_ACTIVE / 8 (GRBM sums the
+bench.py, whose codec calls all decode the same S x chunk frames. Over every large-M GEMM dispatch:
+busy = sum of SQ_VALU_MFMA_BUSY_CYCLES (MFMA-busy cycles summed over the SIMDs, MI355X_MICROARCH.md), active = sum of GRBM_GUI_ACTIVE / 8 (GRBM sums the
 8 XCDs), util = busy / (active x 1024 SIMDs). KEY = bench.py's codec key
 "<dtype>/F<frames>/L<frames per stream>".
 """
@@ -21,7 +21,7 @@ def main():
                                                              "pmc_codec.json")
     per = {}
     for r in csv.DictReader(open(path)):
-        if "gemm_bf16_kernel" not in r["Kernel_Name"]:
+        if "gemm_bf16_kernel" not in r["Kernel_Name"] and "gemm_glds_kernel" not in r["Kernel_Name"]:
             continue
         d = per.setdefault(r["Dispatch_Id"], {})
         d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
