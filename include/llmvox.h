@@ -177,6 +177,28 @@ int lvx_codec_decode_features(lvx_ctx* ctx, const float* feats_dev, int B, int L
 int lvx_codec_decode_codes(lvx_ctx* ctx, const int32_t* codes_dev, int B, int L, int bandwidth_id,
                            float* pcm_dev, void* stream);
 
+/* ---- WavTokenizer encoder, a context of its own (its weights are not needed for TTS).
+ * Replaces WavTokenizer.encode_infer (WavTokenizer/decoder/pretrained.py:185-190 ->
+ * decoder/feature_extractors.py:122-133): SEANet encoder (encoder/modules/seanet.py:94-143) + the
+ * 1-codebook quantiser (encoder/quantization/vq.py:115-140, core_vq.py:175-183), fp32.
+ * Weights by reference state_dict name: "feature_extractor.encodec.encoder.model.<i>.conv.conv.weight"
+ * with weight_norm already resolved (w = g v / |v|, torch._weight_norm(v, g, 0)) [cout][cin][k], ".bias",
+ * the LSTM's "<...>.13.lstm.{weight,bias}_{ih,hh}_l{0,1}", and the codebook
+ * "feature_extractor.encodec.quantizer.vq.layers.0._codebook.embed" [4096][512]. */
+typedef struct lvx_enc lvx_enc;
+int lvx_enc_create(int device, long long max_samples, lvx_enc** out);  /* max_samples >= B * N of any call */
+int lvx_enc_set_weight(lvx_enc* enc, const char* name, const float* data, int64_t numel);
+int lvx_enc_finalize(lvx_enc* enc);
+void lvx_enc_destroy(lvx_enc* enc);
+/* frames T of an N-sample input (ceil(N / 320): the SConv1d padding chain) */
+int lvx_enc_frames(int n_samples);
+/* audio_dev [B][N] f32 -> features_dev [B][512][T] (codebook rows of the codes, the reference's
+ * features layout), codes_dev [B][T] int32 (the reference returns them as [1][B][T]). Async on stream. */
+int lvx_encode(lvx_enc* enc, const float* audio_dev, int B, int N, float* features_dev, int32_t* codes_dev,
+               void* stream);
+/* test hook: the pre-quantisation embedding [B][T][512] of the last lvx_encode */
+int lvx_enc_embedding(lvx_enc* enc, float* dst_dev, int B, int T, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

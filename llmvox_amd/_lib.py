@@ -82,6 +82,13 @@ _SIGS = {
     "lvx_device_cus": (_I, [_P, ctypes.POINTER(_I)]),
     "lvx_codec_decode_features": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "lvx_codec_decode_codes": (_I, [_P, _P, _I, _I, _I, _P, _P]),
+    "lvx_enc_create": (_I, [_I, ctypes.c_longlong, ctypes.POINTER(_P)]),
+    "lvx_enc_set_weight": (_I, [_P, ctypes.c_char_p, _P, ctypes.c_int64]),
+    "lvx_enc_finalize": (_I, [_P]),
+    "lvx_enc_destroy": (None, [_P]),
+    "lvx_enc_frames": (_I, [_I]),
+    "lvx_encode": (_I, [_P, _P, _I, _I, _P, _P, _P]),
+    "lvx_enc_embedding": (_I, [_P, _P, _I, _I, _P]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)

@@ -817,3 +817,239 @@ int lvx_codec_decode_codes(lvx_ctx* c, const int32_t* codes, int B, int L, int b
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// WavTokenizer encoder (encode_infer): its own context, since its weights are not needed for TTS.
+// ---------------------------------------------------------------------------
+namespace {
+constexpr const char* kEncPrefix = "feature_extractor.encodec.encoder.model.";
+constexpr const char* kCodebookKey = "feature_extractor.encodec.quantizer.vq.layers.0._codebook.embed";
+struct EncConv {
+  std::string name;
+  int cin, cout, k, stride, dil;
+  bool elu;
+};
+// seanet.py:94-140 with n_filters 32, ratios [8, 5, 4, 2] reversed, compress 2 (llmvox_amd.weights.encoder_convs)
+std::vector<EncConv> enc_convs() {
+  std::vector<EncConv> v{{"0", 1, 32, 7, 1, 1, false}};
+  int dim = 32, idx = 1;
+  for (int ratio : {2, 4, 5, 8}) {
+    v.push_back({std::to_string(idx) + ".block.1", dim, dim / 2, 3, 1, 1, true});
+    v.push_back({std::to_string(idx) + ".block.3", dim / 2, dim, 1, 1, 1, true});
+    v.push_back({std::to_string(idx) + ".shortcut", dim, dim, 1, 1, 1, false});
+    v.push_back({std::to_string(idx + 2), dim, 2 * dim, 2 * ratio, ratio, 1, true});
+    dim *= 2;
+    idx += 3;
+  }
+  v.push_back({"15", 512, 512, 7, 1, 1, true});
+  return v;
+}
+// SConv1d geometry (conv.py:54-61,79-96,195-211): left pad, reflect domain, output length
+struct ConvGeo {
+  int pl, lext, T;
+};
+ConvGeo conv_geo(int L, int k, int stride, int dil) {
+  const int keff = (k - 1) * dil + 1, pt = keff - stride;
+  const int nf = (L + stride - 1) / stride;  // ceil(n_frames) of get_extra_padding_for_conv1d (L >= 1)
+  const int extra = nf * stride - L;
+  const int pr = pt / 2, pl = pt - pr, right = pr + extra;
+  const int max_pad = std::max(pl, right);
+  const int ex0 = L <= max_pad ? max_pad - L + 1 : 0;
+  return {pl, L + ex0, (pl + L + right - keff) / stride + 1};
+}
+int enc_frames_of(int n) {
+  int L = n;
+  for (const EncConv& cv : enc_convs()) L = conv_geo(L, cv.k, cv.stride, cv.dil).T;
+  return L;
+}
+}  // namespace
+
+struct lvx_enc {
+  int device = 0;
+  long long max_samples = 0;
+  bool finalized = false;
+  std::map<std::string, std::vector<float>> host;
+  std::vector<void*> allocs;
+  std::vector<EncConv> convs = enc_convs();
+  std::vector<const float*> cw, cb;  // per conv: [cout][k][cin] weights, bias
+  const float *wih[2] = {}, *bih[2] = {}, *whh[2] = {}, *bhh[2] = {};
+  const float* codebook = nullptr;  // [4096][512]
+  const float* esq = nullptr;       // [4096] |e|^2
+  float* buf[4] = {};
+  size_t buf_floats = 0;
+  float *h = nullptr, *c = nullptr;  // [2][Bmax][512], [Bmax][512]
+  int bmax = 0;
+  int alloc(float** p, size_t n) {
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, n * 4 + 256);
+    if (e != hipSuccess) return fail(LVX_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+    allocs.push_back(q);
+    *p = reinterpret_cast<float*>(q);
+    return 0;
+  }
+  int upload(const std::vector<float>& v, const float** out) {
+    float* d;
+    if (int r = alloc(&d, v.size())) return r;
+    HIP_TRY(hipMemcpy(d, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+    *out = d;
+    return 0;
+  }
+  std::map<std::string, size_t> expected() const {
+    std::map<std::string, size_t> m;
+    for (const EncConv& cv : convs) {
+      m[std::string(kEncPrefix) + cv.name + ".conv.conv.weight"] = (size_t)cv.cout * cv.cin * cv.k;
+      m[std::string(kEncPrefix) + cv.name + ".conv.conv.bias"] = cv.cout;
+    }
+    for (int l = 0; l < 2; ++l) {
+      const std::string p = std::string(kEncPrefix) + "13.lstm.", sfx = "_l" + std::to_string(l);
+      m[p + "weight_ih" + sfx] = m[p + "weight_hh" + sfx] = (size_t)2048 * 512;
+      m[p + "bias_ih" + sfx] = m[p + "bias_hh" + sfx] = 2048;
+    }
+    m[kCodebookKey] = (size_t)4096 * 512;
+    return m;
+  }
+};
+
+extern "C" {
+
+int lvx_enc_frames(int n_samples) { return n_samples >= 1 ? enc_frames_of(n_samples) : 0; }
+
+int lvx_enc_create(int device, long long max_samples, lvx_enc** out) {
+  if (!out) return fail(LVX_E_ARG, "null argument");
+  if (max_samples < 1) return fail(LVX_E_ARG, "max_samples must be >= 1");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(LVX_E_HIP, "no HIP device available");
+  if (device < 0 || device >= ndev) return fail(LVX_E_ARG, "device ordinal out of range");
+  auto* e = new lvx_enc();
+  e->device = device;
+  e->max_samples = max_samples;
+  *out = e;
+  return LVX_OK;
+}
+
+void lvx_enc_destroy(lvx_enc* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  for (void* p : e->allocs) (void)hipFree(p);
+  delete e;
+}
+
+int lvx_enc_set_weight(lvx_enc* e, const char* name, const float* data, int64_t numel) {
+  if (!e || !name || !data) return fail(LVX_E_ARG, "null argument");
+  if (e->finalized) return fail(LVX_E_STATE, "weights are frozen after lvx_enc_finalize");
+  const auto exp = e->expected();
+  auto it = exp.find(name);
+  if (it == exp.end()) return fail(LVX_E_NAME, std::string("unknown encoder weight name: ") + name);
+  if ((size_t)numel != it->second)
+    return fail(LVX_E_ARG, std::string("weight ") + name + ": expected " + std::to_string(it->second) + " elements");
+  e->host[name] = std::vector<float>(data, data + numel);
+  return LVX_OK;
+}
+
+int lvx_enc_finalize(lvx_enc* e) {
+  if (!e) return fail(LVX_E_ARG, "null argument");
+  if (e->finalized) return LVX_OK;
+  for (auto& kv : e->expected())
+    if (!e->host.count(kv.first)) return fail(LVX_E_STATE, "missing encoder weight: " + kv.first);
+  HIP_TRY(hipSetDevice(e->device));
+  int r;
+  for (const EncConv& cv : e->convs) {
+    const std::string p = std::string(kEncPrefix) + cv.name + ".conv.conv.";
+    const float *w, *b;
+    if ((r = e->upload(repack_conv(e->host[p + "weight"], cv.cout, cv.cin, cv.k), &w)) || (r = e->upload(e->host[p + "bias"], &b)))
+      return r;
+    e->cw.push_back(w);
+    e->cb.push_back(b);
+  }
+  for (int l = 0; l < 2; ++l) {
+    const std::string p = std::string(kEncPrefix) + "13.lstm.", sfx = "_l" + std::to_string(l);
+    if ((r = e->upload(e->host[p + "weight_ih" + sfx], &e->wih[l])) || (r = e->upload(e->host[p + "bias_ih" + sfx], &e->bih[l])) ||
+        (r = e->upload(e->host[p + "weight_hh" + sfx], &e->whh[l])) || (r = e->upload(e->host[p + "bias_hh" + sfx], &e->bhh[l])))
+      return r;
+  }
+  const std::vector<float>& cbk = e->host[kCodebookKey];
+  if ((r = e->upload(cbk, &e->codebook))) return r;
+  std::vector<float> esq(4096);
+  for (int n = 0; n < 4096; ++n) {  // |e|^2 (core_vq.py:180: embed.pow(2).sum(0)), double accumulation
+    double a = 0.0;
+    for (int k = 0; k < 512; ++k) a += (double)cbk[(size_t)n * 512 + k] * cbk[(size_t)n * 512 + k];
+    esq[n] = (float)a;
+  }
+  if ((r = e->upload(esq, &e->esq))) return r;
+  // activations: at most 32 channels per input sample through the SEANet stack; the LSTM gates
+  // (2,048 per frame) and the quantiser scores (4,096 per frame) of up to 64 one-frame streams
+  e->buf_floats = (size_t)e->max_samples * 32 + (size_t)64 * 4096;
+  for (auto& b : e->buf)
+    if ((r = e->alloc(&b, e->buf_floats))) return r;
+  e->bmax = 1024;
+  if ((r = e->alloc(&e->h, (size_t)2 * e->bmax * 512)) || (r = e->alloc(&e->c, (size_t)e->bmax * 512))) return r;
+  HIP_TRY(hipDeviceSynchronize());
+  e->host.clear();
+  e->finalized = true;
+  return LVX_OK;
+}
+
+// audio [B][N] -> features [B][512][T], codes [B][T] (device pointers; T = lvx_enc_frames(N))
+int lvx_encode(lvx_enc* e, const float* audio, int B, int N, float* features, int32_t* codes, void* stream) {
+  if (!e) return fail(LVX_E_ARG, "null argument");
+  if (!e->finalized) return fail(LVX_E_STATE, "call lvx_enc_finalize first");
+  if (B < 1 || N < 1 || !audio || !features || !codes) return fail(LVX_E_ARG, "bad audio / outputs");
+  if ((long long)B * N > e->max_samples || B > e->bmax)
+    return fail(LVX_E_CAPACITY, "B*N = " + std::to_string((long long)B * N) + " exceeds max_samples " + std::to_string(e->max_samples));
+  HIP_TRY(hipSetDevice(e->device));
+  hipStream_t s = (hipStream_t)stream;
+  float** buf = e->buf;
+  // the whole chain's sizes first (every intermediate within a buffer)
+  {
+    int L = N;
+    for (const EncConv& cv : e->convs) {
+      const ConvGeo g = conv_geo(L, cv.k, cv.stride, cv.dil);
+      if ((size_t)B * g.T * cv.cout > e->buf_floats || (size_t)B * L * cv.cin > e->buf_floats)
+        return fail(LVX_E_CAPACITY, "encoder activations exceed the scratch sized by max_samples");
+      L = g.T;
+    }
+    if ((size_t)B * L * 4096 > e->buf_floats) return fail(LVX_E_CAPACITY, "quantiser scores exceed the scratch");
+  }
+  auto conv = [&](int i, const float* x, int L, float* y, const float* res) {
+    const EncConv& cv = e->convs[i];
+    const ConvGeo g = conv_geo(L, cv.k, cv.stride, cv.dil);
+    enc_launch_conv(x, e->cw[i], e->cb[i], res, y, B, L, g.T, cv.cin, cv.cout, cv.k, cv.stride, cv.dil, g.pl, g.lext, cv.elu, s);
+    return g.T;
+  };
+  // conv 0, then per ratio: t1 = block.1(ELU x), sc = shortcut(x), x' = block.3(ELU t1) + sc, down(ELU x')
+  int L = conv(0, audio, N, buf[0], nullptr);
+  for (int blk = 0; blk < 4; ++blk) {
+    const int i = 1 + 4 * blk;
+    conv(i, buf[0], L, buf[1], nullptr);
+    conv(i + 2, buf[0], L, buf[2], nullptr);
+    conv(i + 1, buf[1], L, buf[3], buf[2]);
+    L = conv(i + 3, buf[3], L, buf[0], nullptr);
+  }
+  const int T = L;  // x = buf[0] [B][T][512]
+  // SLSTM: layer 0 -> buf[2], layer 1 (+ skip from the LSTM input) -> buf[3]
+  for (int l = 0; l < 2; ++l) {
+    const float* xin = l == 0 ? buf[0] : buf[2];
+    float* yout = l == 0 ? buf[2] : buf[3];
+    enc_launch_conv(xin, e->wih[l], e->bih[l], nullptr, buf[1], B, T, T, 512, 2048, 1, 1, 1, 0, T, false, s);
+    HIP_TRY(hipMemsetAsync(e->h, 0, (size_t)B * 512 * 4, s));
+    HIP_TRY(hipMemsetAsync(e->c, 0, (size_t)B * 512 * 4, s));
+    for (int t = 0; t < T; ++t)
+      enc_launch_lstm_step(buf[1], e->whh[l], e->bhh[l], e->h + (size_t)(t & 1) * e->bmax * 512,
+                           e->h + (size_t)((t + 1) & 1) * e->bmax * 512, e->c, yout, l == 1 ? buf[0] : nullptr, B, T, t, s);
+  }
+  conv(17, buf[3], T, buf[0], nullptr);  // ELU -> final conv: embedding [B][T][512]
+  // quantiser: scores x . e (a 1-tap conv with the codebook as weights), then argmax + gather
+  enc_launch_conv(buf[0], e->codebook, nullptr, nullptr, buf[1], B, T, T, 512, 4096, 1, 1, 1, 0, T, false, s);
+  enc_launch_vq(buf[0], buf[1], e->esq, e->codebook, codes, features, B, T, s);
+  HIP_TRY(hipGetLastError());
+  return LVX_OK;
+}
+
+// test hook: the encoder's output before quantisation ([B][T][512], time-major) of the last lvx_encode
+int lvx_enc_embedding(lvx_enc* e, float* dst, int B, int T, void* stream) {
+  if (!e || !e->finalized || !dst) return fail(LVX_E_ARG, "bad arguments");
+  HIP_TRY(hipMemcpyAsync(dst, e->buf[0], (size_t)B * T * 512 * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return LVX_OK;
+}
+
+}  // extern "C"

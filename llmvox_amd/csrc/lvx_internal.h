@@ -147,4 +147,12 @@ struct CodecScratch {
 void codec_launch_decode(const CodecWeights& w, const CodecScratch& sc, int wdtype, const float* feats_in,
                          const int32_t* codes, int B, int L, int bw, float* pcm, hipStream_t s);
 
+// ---------------- encoder (encode_infer) ----------------
+void enc_launch_conv(const float* x, const float* w, const float* bias, const float* res, float* y, int B, int L, int T,
+                     int cin, int cout, int k, int stride, int dil, int pl, int lext, bool elu, hipStream_t s);
+void enc_launch_lstm_step(const float* gin, const float* whh, const float* bhh, const float* hprev, float* hnext,
+                          float* c, float* y, const float* skip, int B, int T, int t, hipStream_t s);
+void enc_launch_vq(const float* emb, const float* scores, const float* esq, const float* cb, int32_t* codes,
+                   float* feats, int B, int T, hipStream_t s);
+
 }  // namespace lvx

@@ -140,10 +140,23 @@ class TextEmbedding:
 
 class WavTokenizerDecoder:
     """``.wavtokenizer``: codes_to_features + decode of WavTokenizer
-    (decoder/pretrained.py:192-239) for the yaml the reference ships (n_q = 1)."""
+    (decoder/pretrained.py:192-239) for the yaml the reference ships (n_q = 1), and encode_infer
+    (pretrained.py:185-190) on its own encoder context, built on first use."""
 
-    def __init__(self, engine: Engine):
+    def __init__(self, engine: Engine, encoder_weights=None, codebook=None, max_encode_samples: int = 24000 * 30):
         self.engine = engine
+        self._enc_src = (encoder_weights, codebook, int(max_encode_samples))
+        self._enc = None
+
+    def encode_infer(self, audio_input: torch.Tensor, bandwidth_id=None, **kw):
+        """audio [B, N] at 24 kHz -> (features [B, 512, T], codes [1, B, T]) as the reference returns them"""
+        if self._enc is None:
+            from .encoder import WavEncoder
+            ew, cb, ms = self._enc_src
+            if ew is None or not any(k.startswith(LW.ENC_PREFIX) for k in ew):
+                raise KeyError("no WavTokenizer encoder weights (the checkpoint holds only the decode path)")
+            self._enc = WavEncoder(self.engine.device_index, ew, cb, ms)
+        return self._enc.encode(audio_input)
 
     def codes_to_features(self, codes: torch.Tensor) -> torch.Tensor:
         # pretrained.py:226-239: a 2-D input is (K, L), a 3-D input (K, B, L); K = n_q = 1.
@@ -194,7 +207,9 @@ class ModelHandler:
                              int(get("max_codec_frames", C.MAX_DUMP_SIZE)), get("codec_dtype", None))
         self.device = self.engine.device
         self.engine.load_weights(gw, cw, tt)
-        self.wavtokenizer = WavTokenizerDecoder(self.engine)
+        ew = LW.synthetic_encoder(int(get("seed", 1234))) if src == "synthetic" else cw
+        self.wavtokenizer = WavTokenizerDecoder(self.engine, ew, cw[LW.CODEBOOK_KEY],
+                                                int(get("max_encode_samples", 24000 * 30)))
         self.tokenizer = ByteTokenizer()
         self.llm_model = TextEmbedding(self.engine)
         self.model = SpeechGPT(self.engine, _SlotPool(self.engine.max_streams), block)

@@ -165,6 +165,92 @@ def synthetic_all(seed: int = 1234):
 
 
 # ---------------------------------------------------------------------------
+# WavTokenizer encoder (SURVEY 8f.4: encode_infer, decoder/pretrained.py:185-190): the SEANet encoder
+# EncodecFeatures builds (decoder/feature_extractors.py:66-69: n_filters 32, ratios [8, 5, 4, 2]
+# reversed, one residual block per ratio, compress 2, ELU, weight_norm, reflect padding, 2-layer LSTM
+# with skip, dimension 512; encoder/modules/seanet.py:94-140) and the 1-codebook quantizer.
+# ---------------------------------------------------------------------------
+
+ENC_PREFIX = "feature_extractor.encodec.encoder.model."
+ENC_RATIOS = (2, 4, 5, 8)
+ENC_LSTM = 13  # model index of the SLSTM
+
+
+def encoder_convs():
+    """[(name, cin, cout, kernel, stride, dilation, elu_before)] in execution order: name is the
+    state_dict prefix of the SConv1d ('<prefix>.conv.conv.{weight_g,weight_v,bias}'). Residual blocks
+    are the triples (block.1, block.3, shortcut) at model indices 1, 4, 7, 10
+    (seanet.py:117-135, residual block seanet.py:36-64)."""
+    out = [("0", 1, 32, 7, 1, 1, False)]
+    mult, idx = 1, 1
+    for ratio in ENC_RATIOS:
+        dim = 32 * mult
+        out += [(f"{idx}.block.1", dim, dim // 2, 3, 1, 1, True),
+                (f"{idx}.block.3", dim // 2, dim, 1, 1, 1, True),
+                (f"{idx}.shortcut", dim, dim, 1, 1, 1, False)]
+        out.append((f"{idx + 2}", dim, 2 * dim, 2 * ratio, ratio, 1, True))
+        mult *= 2
+        idx += 3
+    out.append(("15", 512, 512, 7, 1, 1, True))
+    return out
+
+
+def encoder_param_shapes():
+    s = {}
+    for name, cin, cout, k, _, _, _ in encoder_convs():
+        p = ENC_PREFIX + name + ".conv.conv."
+        s[p + "weight_v"] = (cout, cin, k)
+        s[p + "weight_g"] = (cout, 1, 1)
+        s[p + "bias"] = (cout,)
+    p = ENC_PREFIX + f"{ENC_LSTM}.lstm."
+    for layer in range(2):
+        s[p + f"weight_ih_l{layer}"] = (4 * 512, 512)
+        s[p + f"weight_hh_l{layer}"] = (4 * 512, 512)
+        s[p + f"bias_ih_l{layer}"] = (4 * 512,)
+        s[p + f"bias_hh_l{layer}"] = (4 * 512,)
+    return s
+
+
+def synthetic_encoder(seed: int = 1234) -> Weights:
+    """weight_v ~ N(0, 1 / (cin k)) (unit gain), weight_g = |v| (1 + 0.1 N) per output channel (x 3
+    for the last conv, so the embedding lives on the codebook's N(0, 1) scale and the quantiser's
+    choice depends on x . e, not only on |e|), bias 0.01 N; LSTM weights and biases
+    ~ N(0, 1/sqrt(3 x 512)) (the spread of PyTorch's U(-1/sqrt(512), 1/sqrt(512)) init). The codebook
+    is the decoder's (CODEBOOK_KEY)."""
+    w = {}
+    for k, shp in encoder_param_shapes().items():
+        if k.endswith("weight_v"):
+            w[k] = _normal(k, shp, 1.0 / np.sqrt(shp[1] * shp[2]), seed)
+        elif k.endswith("weight_g"):
+            v = w[k[:-1] + "v"]
+            nrm = np.sqrt((v.astype(np.float64) ** 2).sum(axis=(1, 2))).astype(np.float32).reshape(shp)
+            gain = 3.0 if k.startswith(ENC_PREFIX + "15.") else 1.0
+            w[k] = (gain * nrm * _normal(k, shp, 0.1, seed, mean=1.0)).astype(np.float32)
+        elif ".lstm." in k:
+            w[k] = _normal(k, shp, 1.0 / np.sqrt(3 * 512), seed)
+        else:
+            w[k] = _normal(k, shp, 0.01, seed)
+    return w
+
+
+def encoder_effective(we: Weights) -> Weights:
+    """weight_norm resolved as the reference's forward pre-hook does (torch.nn.utils.weight_norm:
+    w = torch._weight_norm(v, g, 0), on the CPU in fp32: the same bits as the reference), keyed
+    '<prefix>.conv.conv.weight'; LSTM and bias entries unchanged."""
+    import torch
+    out = {}
+    for k, v in we.items():
+        if k.endswith("weight_g"):
+            continue
+        if k.endswith("weight_v"):
+            g = torch.from_numpy(np.ascontiguousarray(we[k[:-1] + "g"]))
+            out[k[:-2]] = torch._weight_norm(torch.from_numpy(np.ascontiguousarray(v)), g, 0).numpy()
+        else:
+            out[k] = v
+    return out
+
+
+# ---------------------------------------------------------------------------
 # Checkpoint loaders (SURVEY §8f.2).  Only loaders that execute nothing from the
 # file: torch.load(weights_only=True).
 # ---------------------------------------------------------------------------
@@ -218,7 +304,8 @@ def load_llmvox_checkpoint(path: str) -> GPTWeights:
 
 def load_wavtokenizer_checkpoint(path: str) -> Weights:
     """Lightning ckpt: ckpt['state_dict'] filtered to backbone./head./feature_extractor.
-    (WavTokenizer/decoder/pretrained.py:101-105)."""
+    (WavTokenizer/decoder/pretrained.py:101-105). The encoder's entries (ENC_PREFIX, used by
+    encode_infer) come along when the checkpoint holds them."""
     import torch
     ck = torch.load(path, map_location="cpu", weights_only=True)
     sd = ck["state_dict"]

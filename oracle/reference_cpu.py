@@ -239,3 +239,83 @@ def decode_codes(Wc, codes: torch.Tensor, bw=0):
     reference does per dump."""
     feats = F.embedding(codes, Wc[CODEBOOK_KEY]).transpose(1, 2)
     return decode(Wc, feats, bw)
+
+
+# ---------------------------------------------------------------------------
+# 8f.4: WavTokenizer.encode_infer (decoder/pretrained.py:185-190 -> feature_extractors.py:122-133):
+# SEANet encoder (encoder/modules/seanet.py:94-143) + the 1-codebook quantizer's inference path
+# (encoder/quantization/vq.py:115-140, core_vq.py:171-231, 245-276, 296-310). Weights: the effective
+# dict of llmvox_amd.weights.encoder_effective (weight_norm resolved) + the codebook.
+# ---------------------------------------------------------------------------
+
+ENC_PREFIX = "feature_extractor.encodec.encoder.model."
+
+
+def _enc_pad(x, k_eff, stride):
+    """SConv1d's non-causal padding (encoder/modules/conv.py:54-61, 79-96, 195-211): reflect with
+    padding_total = k_eff - stride split right-heavy-last, plus the extra right padding that makes the
+    last window full; inputs no longer than the pad are zero-extended before reflecting."""
+    L = x.shape[-1]
+    pt = k_eff - stride
+    n_frames = (L - k_eff + pt) / stride + 1
+    extra = (math.ceil(n_frames) - 1) * stride + (k_eff - pt) - L
+    pr = pt // 2
+    pl = pt - pr
+    right = pr + extra
+    max_pad = max(pl, right)
+    ex0 = max_pad - L + 1 if L <= max_pad else 0
+    if ex0:
+        x = F.pad(x, (0, ex0))
+    y = F.pad(x, (pl, right), "reflect")
+    return y[..., :y.shape[-1] - ex0]
+
+
+def enc_conv(We, name, x, stride=1, dilation=1, elu=False):
+    """[ELU ->] SConv1d (conv.py:195-211) on x [B, C, T]."""
+    if elu:
+        x = F.elu(x)  # nn.ELU(alpha=1.0)
+    w = We[ENC_PREFIX + name + ".conv.conv.weight"]
+    b = We[ENC_PREFIX + name + ".conv.conv.bias"]
+    k_eff = (w.shape[-1] - 1) * dilation + 1
+    return F.conv1d(_enc_pad(x, k_eff, stride), w, b, stride, 0, dilation)
+
+
+def enc_lstm(We, x):
+    """SLSTM (encoder/modules/lstm.py:31-39): 2-layer nn.LSTM over time, + the input (skip)."""
+    lstm = torch.nn.LSTM(512, 512, 2)
+    p = ENC_PREFIX + "13.lstm."
+    with torch.no_grad():
+        for n, t in lstm.named_parameters():
+            t.copy_(We[p + n])
+        y, _ = lstm(x.permute(2, 0, 1))
+    return y.permute(1, 2, 0) + x
+
+
+def seanet_encode(We, audio):
+    """audio [B, N] -> embedding [B, 512, T] (seanet.py:94-143; ratios [2, 4, 5, 8])."""
+    x = enc_conv(We, "0", audio.unsqueeze(1))
+    idx = 1
+    for ratio in (2, 4, 5, 8):
+        h = enc_conv(We, f"{idx}.block.1", x, elu=True)      # ELU -> conv k3 (dim -> dim / 2)
+        h = enc_conv(We, f"{idx}.block.3", h, elu=True)      # ELU -> conv k1 (dim / 2 -> dim)
+        x = enc_conv(We, f"{idx}.shortcut", x) + h           # seanet.py:63-64
+        x = enc_conv(We, f"{idx + 2}", x, stride=ratio, elu=True)
+        idx += 3
+    x = enc_lstm(We, x)
+    return enc_conv(We, "15", x, elu=True)
+
+
+def vq_encode(codebook, emb):
+    """emb [B, 512, T] -> codes [B, T] (core_vq.py:175-183: argmax of -(|x|^2 - 2 x.e + |e|^2))."""
+    x = emb.permute(0, 2, 1).reshape(-1, emb.shape[1])
+    embed = codebook.t()
+    dist = -(x.pow(2).sum(1, keepdim=True) - 2 * x @ embed + embed.pow(2).sum(0, keepdim=True))
+    return dist.max(dim=-1).indices.view(emb.shape[0], emb.shape[2]), dist
+
+
+def encode_infer(We, codebook, audio):
+    """pretrained.py:185-190: (features [B, 512, T] = codebook rows of the codes, codes [1, B, T])."""
+    emb = seanet_encode(We, audio)
+    codes, _ = vq_encode(codebook, emb)
+    feats = F.embedding(codes, codebook).transpose(1, 2)
+    return feats, codes.unsqueeze(0)

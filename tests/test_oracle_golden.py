@@ -93,3 +93,36 @@ def test_long_stream_ids_through_smallest_margin(W):
     ids, margins, _ = R.ar_decode(Wg, tt, Wc[R.CODEBOOK_KEY], g["text_ids"].tolist(), n)
     assert ids == g["ids"][:n].tolist()
     np.testing.assert_array_equal(np.float32(margins), g["margins"][:n])
+
+
+def test_encoder_oracle_matches_reference_encode_infer():
+    """8f.4: the oracle's SEANet encoder + quantiser against the reference's own encode_infer
+    (tests/golden/make_golden_encoder.py): codes and the pre-quantisation embedding bit for bit."""
+    g = np.load(os.path.join(GOLDEN, "encoder_golden.npz"))
+    We = R.to_torch(LW.encoder_effective(LW.synthetic_encoder(1234)))
+    cb = torch.from_numpy(LW.synthetic_codec(1234)[LW.CODEBOOK_KEY])
+    tags = sorted(k[len("codes_"):] for k in g.files if k.startswith("codes_"))
+    assert len(tags) == 5
+    for tag in tags:
+        audio = torch.from_numpy(g[f"audio_{tag}"])
+        feats, codes = R.encode_infer(We, cb, audio)
+        np.testing.assert_array_equal(codes.numpy(), g[f"codes_{tag}"])
+        assert feats.shape == (audio.shape[0], 512, g[f"codes_{tag}"].shape[-1])
+        emb = R.seanet_encode(We, audio).numpy()
+        if f"emb_{tag}" in g.files:
+            np.testing.assert_array_equal(emb, g[f"emb_{tag}"])
+        else:
+            np.testing.assert_array_equal(emb.reshape(-1)[::7], g[f"emb_{tag}_every7"])
+
+
+def test_encoder_frame_count_matches_reference():
+    """lvx_enc_frames (host-side SConv1d length chain, no GPU) = the reference's T = ceil(N / 320)"""
+    from llmvox_amd import _lib
+    lib = _lib.load()
+    g = np.load(os.path.join(GOLDEN, "encoder_golden.npz"))
+    for k in g.files:
+        if k.startswith("codes_"):
+            N = g["audio_" + k[len("codes_"):]].shape[1]
+            assert lib.lvx_enc_frames(N) == g[k].shape[-1] == -(-N // 320)
+    for N in (1, 2, 319, 320, 321, 641, 24000, 24001):
+        assert lib.lvx_enc_frames(N) == -(-N // 320)
