@@ -56,6 +56,9 @@ INITIAL_DUMP_SIZE_2 = 160
 MAX_DUMP_SIZE = 1280
 MAX_AUDIO_LENGTH = 8000
 EOS_TOKEN = "<|eot_id|>"
+# configs/inference_config.py:29 (the LLM text streamer's system prompt, llm_streaming.py)
+SYSTEM_PROMPT = ("You are a friendly voicebot that answers questions in a concise way and do not use "
+                 "abbreviation.Give short responses")
 
 
 @dataclass

@@ -214,12 +214,17 @@ class ModelHandler:
         self.llm_model = TextEmbedding(self.engine)
         self.model = SpeechGPT(self.engine, _SlotPool(self.engine.max_streams), block)
 
-    # upstream LLM producers are outside the hot path
     def initialize_stream_model(self):
-        raise NotImplementedError("the LLM text streamer is outside the TTS hot path")
+        """the LLM text streamer (model_handler.py:108-118; llm_streaming.StreamModel on PyTorch-ROCm,
+        config["llm_checkpoint"] a local path)"""
+        from .llm_streaming import StreamModel
+        return StreamModel(self.config).load()
 
-    initialize_vlm_model = initialize_stream_model
-    initialize_stream_multimodal = initialize_stream_model
+    # the VLM / multimodal producers are out of scope (SURVEY §2)
+    def initialize_vlm_model(self):
+        raise NotImplementedError("VLM producers are outside the TTS path (SURVEY §2)")
+
+    initialize_stream_multimodal = initialize_vlm_model
 
 
 def _load_t5_state(path):

@@ -13,12 +13,13 @@ step, codec per dump). The response body is the same byte stream the reference p
 f32le mono 24 kHz chunks, in order, no framing.
 
 Differences, on purpose:
-  * the text is spoken as given. The reference hands it to an LLM first and, through
-    ``"text" in request`` being False for a pydantic model (:209), actually routes /tts requests
-    to its ASR branch; the intended text path is what is built here, the LLM (an upstream text
-    source) is out of scope. The request text is followed by the EOS token,
-    as an LLM stream would end, so the replica that receives it ends the response at its
-    end-of-audio token.
+  * the reference hands the request text to an LLM and speaks its streamed reply; through
+    ``"text" in request`` being False for a pydantic model (:209) it actually routes /tts requests
+    to its ASR branch. The intended text path is what is built here: with a ``stream_model``
+    (llm_streaming.StreamModel; ``--llm-checkpoint``) the request text is the prompt
+    and the reply is routed to the replicas as it streams (text_streamer_producer); without one
+    the request text itself is spoken, followed by the EOS token, as an LLM stream would end, so
+    the replica that receives it ends the response at its end-of-audio token.
   * ``max_tokens`` bounds a request (the reference relies on the model emitting end-of-audio;
     synthetic weights never do): a stream that was fed text stops once it has generated
     ``max_tokens`` tokens, or when its segment would outgrow the KV capacity (``max_positions``);
@@ -51,8 +52,14 @@ class TTSService:
     in speaking order (audio_generator_async semantics) and closes the session at the end."""
 
     def __init__(self, engine, max_chunk: int = 64, max_tokens: Optional[int] = None, eos: str = C.EOS_TOKEN,
-                 eoa_id: int = C.EOA_TOKEN_ID, dumps=(C.INITIAL_DUMP_SIZE_1, C.INITIAL_DUMP_SIZE_2)):
+                 eoa_id: int = C.EOA_TOKEN_ID, dumps=(C.INITIAL_DUMP_SIZE_1, C.INITIAL_DUMP_SIZE_2),
+                 stream_model=None, system_prompt: str = C.SYSTEM_PROMPT):
+        """stream_model: an llm_streaming.StreamModel (or anything with its predict()): the request
+        text is then the LLM prompt and its streamed reply is spoken, as the reference's /tts does
+        (streaming_server.py:184-248, 494-540); None speaks the request text itself."""
         self.engine = engine
+        self.stream_model = stream_model
+        self.system_prompt = system_prompt
         self.sched = FusedScheduler(engine, max_chunk=max_chunk, to_bytes=True)
         self.max_tokens = max_tokens or max(1, engine.max_positions - max_chunk - 1)
         self.eos = eos
@@ -83,11 +90,34 @@ class TTSService:
                 def put(self, w):
                     self.st.feed(w)
 
-            route_text(text.split() + [self.eos], [_Feed(streams[0]), _Feed(streams[1])], eos=self.eos)
+            if self.stream_model is None:
+                route_text(text.split() + [self.eos], [_Feed(streams[0]), _Feed(streams[1])], eos=self.eos)
+            else:  # the LLM's reply, routed as it streams (text_streamer_producer on its own thread)
+                threading.Thread(target=self._produce, args=(text, streams), name="lvx-llm-producer",
+                                 daemon=True).start()
             s = _Session(streams, queues)
             self.sessions.append(s)
             self.lock.notify_all()
         return s
+
+    def _produce(self, prompt: str, streams):
+        from .llm_streaming import text_streamer_producer
+        svc = self
+
+        class _LockedFeed:
+            def __init__(self, st):
+                self.st = st
+
+            def put(self, w):
+                with svc.lock:
+                    self.st.feed(w)
+                    svc.lock.notify_all()
+
+        try:
+            text_streamer_producer(prompt, self.stream_model, _LockedFeed(streams[0]), _LockedFeed(streams[1]),
+                                   {"system_prompt": self.system_prompt, "eos_token": self.eos})
+        except BaseException as e:  # an LLM failure ends the service's requests like a scheduler failure
+            self.error = e
 
     def chunks(self, session: _Session, timeout: float = 0.05):
         try:
@@ -220,6 +250,9 @@ def main(argv=None):
     ap.add_argument("--text-embed", default=None,
                     help="ByT5 encoder state dict (torch, weights_only) for the 386-row text table")
     ap.add_argument("--seed", type=int, default=1234, help="synthetic weights for whatever is not given")
+    ap.add_argument("--llm-checkpoint", default=None,
+                    help="local HF causal-LM directory: /tts speaks its reply to the request text")
+    ap.add_argument("--llm-max-tokens", type=int, default=1000)
     a = ap.parse_args(argv)
     from .engine import build_engine
     from . import weights as W
@@ -235,7 +268,12 @@ def main(argv=None):
     weights = (gw, cw, tt)
     eng = build_engine(a.device, a.dtype, a.kv_dtype or a.dtype, seed=a.seed, max_streams=a.max_streams,
                        max_positions=a.max_positions, max_codec_frames=C.MAX_DUMP_SIZE * 2, weights=weights)
-    svc = TTSService(eng)
+    sm = None
+    if a.llm_checkpoint:
+        from .llm_streaming import StreamModel
+        sm = StreamModel({"llm_checkpoint": a.llm_checkpoint, "llm_device": f"cuda:{a.device}",
+                          "llm_max_tokens": a.llm_max_tokens}).load()
+    svc = TTSService(eng, stream_model=sm)
     import uvicorn
     uvicorn.run(create_app(svc), host=a.host, port=a.port)
 

@@ -120,8 +120,29 @@ def _segment_tokens(eng, words, n):
     return st.tokens[:n]
 
 
+class _ScriptedLLM:
+    """llm_streaming.StreamModel stand-in: predict() streams fixed pieces (leading spaces, as a
+    tokenizer's streamer yields them) with small delays, so words reach the replicas while they
+    decode; the prompt must be the request text."""
+
+    def __init__(self, pieces):
+        self.pieces = pieces
+        self.requests = []
+
+    def predict(self, request):
+        import time
+        self.requests.append(dict(request))
+
+        def gen():
+            for p in self.pieces:
+                time.sleep(0.003)
+                yield p
+        return gen()
+
+
 @pytest.mark.gpu
-def test_tts_two_replica_order_matches_reference_consumers(handler):
+@pytest.mark.parametrize("mode", ["text", "llm"])
+def test_tts_two_replica_order_matches_reference_consumers(handler, mode):
     """POST /tts with an end-of-audio id that every segment emits (chosen from the synthetic model's
     own tokens): replica 0's chunks -> its switch signal -> replica 1's chunks -> its switch back ->
     replica 0's EOS segment -> 'end' (streaming_server.py:397-404,428-469). The response body must
@@ -157,11 +178,17 @@ def test_tts_two_replica_order_matches_reference_consumers(handler):
     assert trace[0].count(1) == 1 and trace[0].count("end") == 1 and trace[1].count(0) == 1
     want = b"".join(S.audio_chunks(qs_audio[0], qs_audio[1], timeout=0.01,
                                    stop=lambda: all(q.empty() for q in qs_audio)))
-    svc = TTSService(eng, max_chunk=32, max_tokens=4000, eoa_id=eoa)
+    # mode "llm": the request text is the LLM prompt and the (scripted) reply is spoken, as the
+    # reference's /tts does through text_streamer_producer (streaming_server.py:184-248): same
+    # routed words, so the same byte stream, although they arrive while the replicas decode
+    llm = _ScriptedLLM([" " + w if i else w for i, w in enumerate(text.split())] + ["<|eot_id|>"])
+    svc = TTSService(eng, max_chunk=32, max_tokens=4000, eoa_id=eoa, stream_model=llm if mode == "llm" else None)
     try:
-        body = TestClient(create_app(svc)).post("/tts", json={"text": text}).content
+        body = TestClient(create_app(svc)).post("/tts", json={"text": "tell me about the fox" if mode == "llm" else text}).content
     finally:
         svc.shutdown()
+    if mode == "llm":
+        assert llm.requests == [{"system": svc.system_prompt, "prompt": "tell me about the fox"}]
     got, ref = np.frombuffer(body, dtype=np.float32), np.frombuffer(want, dtype=np.float32)
     assert got.shape == ref.shape and got.size > 0
     assert np.abs(got - ref).max() < 1e-5
