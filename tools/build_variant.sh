@@ -8,7 +8,8 @@ O=build/var_$NAME; mkdir -p $O
 CXX="/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../../include -Wall -Wno-unused-function $FLAGS"
 $CXX -c ar_kernels.hip -o $O/ar.o &
 $CXX -c codec_kernels.hip -o $O/codec.o &
+$CXX -c encoder_kernels.hip -o $O/enc.o &
 $CXX -x hip -c lvx_api.cpp -o $O/api.o &
 wait
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ../libllmvox_hip_$NAME.so $O/ar.o $O/codec.o $O/api.o
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ../libllmvox_hip_$NAME.so $O/ar.o $O/codec.o $O/enc.o $O/api.o
 echo built ../libllmvox_hip_$NAME.so

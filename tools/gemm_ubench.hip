@@ -18,7 +18,9 @@ __device__ __forceinline__ void glds16(const void* src, unsigned char* lds) {
 
 // MODE bit 0: no MFMA, bit 1: no DMA in the loop, bit 2: s_setprio(1) around the MFMAs, bit 3: no
 // output stores (kept live by an impossible condition), bit 4: no fragment reads, bit 5: fragment
-// reads of the next k32 sub-step issued before the MFMAs of this one (software pipeline)
+// reads of the next k32 sub-step issued before the MFMAs of this one (software pipeline), bit 6:
+// bf16 output (2-byte stores), bit 7: GELU (erf) before the store, bit 8: bf16 output staged
+// through LDS and written with 16-byte stores, bit 9: a cheap GELU stand-in (x sigmoid(1.702 x))
 template <int BM, int BN, int NS, int MODE, int WV = 8, int OCC = 1>
 __global__ __launch_bounds__(WV * 64, OCC) void k_gemm(const unsigned short* __restrict__ A, const unsigned short* __restrict__ W,
                                                  float* __restrict__ C, int M, int N, int K) {
@@ -98,13 +100,43 @@ __global__ __launch_bounds__(WV * 64, OCC) void k_gemm(const unsigned short* __r
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  auto act = [](float v) {
+    if (MODE & 128) return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+    if (MODE & 512) return v / (1.0f + __expf(-1.702f * v));
+    return v;
+  };
+  auto bf = [](float v) {
+    const unsigned u = __float_as_uint(v);
+    return (unsigned short)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+  };
+  if (MODE & 256) {
+    constexpr int WR = BM / 2, WC = BN / WNN, LD = WC + 8;
+    __syncthreads();
+    unsigned short* ws = reinterpret_cast<unsigned short*>(smem) + wave * WR * LD;
+    for (int i = 0; i < MI; ++i)
+      for (int j = 0; j < NJ; ++j)
+        for (int e = 0; e < 4; ++e)
+          ws[(i * 16 + 4 * (lane >> 4) + e) * LD + j * 16 + (lane & 15)] = bf(act(acc[i][j][e]));
+    __syncthreads();
+    unsigned short* Cb = reinterpret_cast<unsigned short*>(C);
+    for (int c = lane; c < WR * WC / 8; c += 64) {
+      const int r = c / (WC / 8), q = c - r * (WC / 8);
+      const int row = m0 + wm * WR + r, col = n0 + wn * WC + q * 8;
+      if (row < M && col < N)
+        *reinterpret_cast<uint4*>(Cb + (size_t)row * N + col) = *reinterpret_cast<const uint4*>(ws + r * LD + q * 8);
+    }
+    return;
+  }
   for (int i = 0; i < MI; ++i)
     for (int j = 0; j < NJ; ++j) {
       const int col = n0 + wn * (BN / WNN) + j * 16 + (lane & 15);
       for (int e = 0; e < 4; ++e) {
         const int row = m0 + wm * (BM / 2) + i * 16 + 4 * (lane >> 4) + e;
         if ((MODE & 8) && acc[i][j][e] != -1.2345f) continue;
-        if (row < M && col < N) C[(size_t)row * N + col] = acc[i][j][e];
+        if (row < M && col < N) {
+          if (MODE & (64 | 128 | 512)) reinterpret_cast<unsigned short*>(C)[(size_t)row * N + col] = bf(act(acc[i][j][e]));
+          else C[(size_t)row * N + col] = acc[i][j][e];
+        }
       }
     }
 }
@@ -139,19 +171,15 @@ int main() {
   for (size_t i = 0; i < h.size(); ++i) h[i] = 0x3c00 + (unsigned short)((i * 2654435761u >> 7) & 0xff);  // ~[0.0078, 0.016)
   CK(hipMemcpy(A, h.data(), h.size() * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(W, h.data(), (size_t)2304 * 3584 * 2, hipMemcpyHostToDevice));
-  const int shapes[2][2] = {{768, 2304}, {2304, 768}};
-  for (auto& s : shapes) {
-    const int N = s[0], K = s[1];
-    run<128, 192, 3, 0>("full", A, W, C, M, N, K);
-    run<128, 192, 3, 32>("pipelined reads", A, W, C, M, N, K);
-    run<128, 192, 3, 36>("pipelined + setprio", A, W, C, M, N, K);
-    run<128, 192, 3, 43>("pipelined reads only", A, W, C, M, N, K);
-    run<128, 192, 2, 0, 8, 2>("full", A, W, C, M, N, K);
-    run<128, 192, 2, 32, 8, 2>("pipelined reads", A, W, C, M, N, K);
-    run<128, 128, 2, 32, 8, 2>("pipelined reads", A, W, C, M, N, K);
-    run<128, 128, 3, 32, 8, 2>("pipelined reads", A, W, C, M, N, K);
-    run<128, 256, 2, 32, 8, 2>("pipelined reads", A, W, C, M, N, K);
-    run<128, 192, 2, 32, 4, 2>("pipelined reads", A, W, C, M, N, K);
+  {
+    const int N = 2304, K = 768;  // pwconv1: bias + GELU (erf), bf16 output
+    run<128, 192, 2, 32, 8, 2>("fp32 out", A, W, C, M, N, K);
+    run<128, 192, 2, 32 | 64, 8, 2>("bf16 2-B stores", A, W, C, M, N, K);
+    run<128, 192, 2, 32 | 64 | 128, 8, 2>("GELU + bf16 2-B", A, W, C, M, N, K);
+    run<128, 192, 2, 32 | 64 | 512, 8, 2>("fast act + bf16 2-B", A, W, C, M, N, K);
+    run<128, 192, 2, 32 | 256, 8, 2>("bf16 via LDS 16-B", A, W, C, M, N, K);
+    run<128, 192, 2, 32 | 256 | 128, 8, 2>("GELU + bf16 LDS 16-B", A, W, C, M, N, K);
+    run<128, 192, 2, 32 | 256 | 512, 8, 2>("fast act + LDS 16-B", A, W, C, M, N, K);
   }
   return 0;
 }
