@@ -1,7 +1,9 @@
 """us per AR step (HIP graph replay, all kernels) at positions [P0, P0+256) for B streams under
 option sets; each config measured 3 times (median).
-usage: python tools/step_sweep.py B P0 'opt=v,...' ['opt=v' ...]"""
-import statistics, sys, time
+usage: python tools/step_sweep.py B P0 'opt=v,...' ['opt=v' ...]
+LVX_SWEEP_STREAM=1: run on a torch side stream (the library then replays 16-step HIP graphs; on the
+default (null) stream it launches every kernel)."""
+import os, statistics, sys, time
 import torch
 from llmvox_amd.engine import build_engine
 
@@ -11,6 +13,9 @@ dev = e.device
 plan = torch.full((B, P0 + 256), 100, dtype=torch.int32, device=dev)
 slots = torch.arange(B, dtype=torch.int32, device=dev)
 tok = torch.zeros(B, P0 + 256, dtype=torch.int32, device=dev)
+side = torch.cuda.Stream(device=dev) if os.environ.get("LVX_SWEEP_STREAM") == "1" else None
+if side is not None:
+    torch.cuda.set_stream(side)
 for spec in sys.argv[3:] or [""]:
     opts = [kv.split("=") for kv in spec.split(",") if kv]
     for k, v in opts:
