@@ -121,7 +121,7 @@ def pmc_traffic(key, kernel):
 
 
 def pmc_codec(key):
-    """MFMA busy cycles / GRBM active cycles of the codec's large GEMM (gemm_bf16_kernel) from a
+    """MFMA busy cycles / GRBM active cycles of the codec's large GEMM (gemm_glds_kernel, gemm_bf16_kernel) from a
     committed rocprofv3 pass over the same codec call (profiles/pmc_codec.json, tools/pmc_codec.py)."""
     pmc = os.path.join(ROOT, "profiles", "pmc_codec.json")
     try:
