@@ -931,14 +931,21 @@ template <> struct KvPiece<fp8_t> {
 // direct = 1 (batched path with one split per (row, head)): the normalised head output goes
 // straight to the bf16 operand row xn, as the merge kernel would write it (o * (1 / l)), and the
 // merge kernel is skipped.
-template <typename TKV, int DEPTH, int NW>
+// QKV (bf16 KV, direct: 17 <= B <= 32): c_attn left its output as four K-slice partials
+// (ar_qkv_ksplit_kernel, st.qkvp); threads 0-287 sum them in the K-slice order the one-launch GEMM
+// summed its waves (bit-identical), q goes through LDS, the new key's K / V are appended to the cache
+// here, and the tile holding key t - 1 takes them from LDS (this block's own store is not read back).
+template <typename TKV, int DEPTH, int NW, bool QKV = false>
 __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int layer, int ns_max, int direct,
                                                          int selcopy) {
   // NW waves: a tile is NW x 16 keys (4 lanes per key); NW = 8 doubles the bytes in flight per
   // block for long splits (batched steps)
   constexpr int TK = NW * 16;
+  static_assert(!QKV || (sizeof(TKV) == 2 && NW == 4 && 3 * HD <= 2 * NW * 64), "the K-split c_attn path: bf16 keys, 256 threads");
   __shared__ float wm_s[NW], wl_s[NW];
   __shared__ float wo_s[NW][4][HD];  // [wave][16-lane row][part * 24 + i]
+  __shared__ float qs_s[QKV ? HD : 1];
+  __shared__ __attribute__((aligned(16))) bf16_t kvh_s[QKV ? 2 : 1][HD];  // QKV: the new key's K, V
   const int sp = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   TS_DECL;
@@ -948,6 +955,19 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
   // (the next text id, a dependent plan load, is looked up at the end of the block, when every
   // other load has landed)
   const int4 ri = selcopy ? st.rowinfo_n[b] : st.rowinfo[b];
+  // QKV: thread tid owns elements e = tid and tid + 256 (tid < 32) of this head's (q, k, v) (element
+  // e % 96 of q / k / v for e / 96 = 0 / 1 / 2); their four K-slice partials are issued with the
+  // control record (clamped element: no load under a branch)
+  float pq[QKV ? 2 : 1][QKV ? 4 : 1];
+  if constexpr (QKV) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = min(tid + 256 * h, 3 * HD - 1);
+      const float* pp = st.qkvp + (size_t)b * (3 * D) + (e / HD) * D + head * HD + e % HD;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pq[h][k] = pp[(size_t)k * st.max_streams * (3 * D)];
+    }
+  }
   const bool cp = selcopy && sp == 0 && head == 0 && tid == 0;
   int jn = 0;
   if (cp) {
@@ -973,7 +993,7 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
   const TKV* __restrict__ Vg = reinterpret_cast<const TKV*>(st.vc) + base * HD;
   const int part = tid & 3, kq = tid >> 2;  // key slot within the TK-key tile
   float q[24];
-  {
+  if constexpr (!QKV) {
     const float* qg = st.q + (size_t)b * D + head * HD + part * 24;
 #pragma unroll
     for (int i = 0; i < 24; i += 4) {
@@ -1003,8 +1023,23 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
   auto tile = [&](int kb, const KvPiece<TKV>(&kp)[3], const KvPiece<TKV>(&vp)[3]) {
     const bool valid = kb + kq < k1;
     float kf[24], vf[24];
+    if constexpr (QKV) {  // the tile holding key t - 1 (wave-uniform): that lane takes it from LDS
+      KvPiece<TKV> kx[3], vx[3];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) { kp[i].get(kf + 8 * i); vp[i].get(vf + 8 * i); }
+      for (int i = 0; i < 3; ++i) { kx[i] = kp[i]; vx[i] = vp[i]; }
+      if (kb + TK >= k1 && min(kb + kq, k1 - 1) == t - 1) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          kx[i].u = reinterpret_cast<const uint4*>(kvh_s[0])[part * 3 + i];
+          vx[i].u = reinterpret_cast<const uint4*>(kvh_s[1])[part * 3 + i];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) { kx[i].get(kf + 8 * i); vx[i].get(vf + 8 * i); }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) { kp[i].get(kf + 8 * i); vp[i].get(vf + 8 * i); }
+    }
     float sc = 0.f;
 #pragma unroll
     for (int i = 0; i < 24; ++i) sc = fmaf(q[i], kf[i], sc);
@@ -1021,6 +1056,30 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
   };
 #pragma unroll
   for (int d = 0; d < DEPTH; ++d) issue(k0 + d * TK, kpr[d], vpr[d]);
+  if constexpr (QKV) {
+    // the partials were issued before the tiles (vmcnt retires in issue order: this waits for them
+    // alone); raw barrier after the LDS writes, the tiles stay in flight
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = tid + 256 * h;
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v += pq[h][k];
+      if (e < HD) {
+        qs_s[e] = v;
+      } else if (e < 3 * HD) {  // K / V of the new key: appended to the cache, kept in LDS
+        const int which = e / HD - 1, d = e % HD;
+        const bf16_t hv = f32_to_bf16(v);
+        kvh_s[which][d] = hv;
+        reinterpret_cast<bf16_t*>(which ? st.vc : st.kc)[(base + ri.y) * HD + d] = hv;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 24; ++i) q[i] = qs_s[part * 24 + i] * 0.10206207261596575f;
+  }
   // DEPTH 2 (few tiles per block, the B <= 2 step): leave after the last valid tile. DEPTH >= 4
   // (long splits, batched steps): whole groups of DEPTH tiles with no exit inside a group (a tile
   // past k1 is all-invalid: alpha = 1, p = 0), which keeps the compiler from draining every
@@ -1517,6 +1576,78 @@ static void launch_mfma2(const GemvArgs& a, hipStream_t s, bool btile = false) {
   else hipLaunchKernelGGL((ar_mfma2_kernel<K, 4, OUT, K, XM>), grid, block, 0, s, a);
 }
 
+// c_attn of the batched steps with one attention block per (row, head) (17 <= B <= 32, bf16 KV):
+// the K = 768 reduction split over the grid instead of over a block's waves. A block is 4 waves x 16
+// output rows (64 rows) of one 192-wide K slice: 24.6 KB of weights + 12.3 KB of operand rows per
+// block instead of 24.6 + 49 KB. Each wave stores its 16 x 32 partial (one 16-B store per
+// lane and batch tile) to st.qkvp[slice]; the attention sums the four slices in the order the
+// one-launch kernel summed its waves and appends the new key (bit-identical to ar_mfma2_kernel OUT 0).
+template <int NT>
+__global__ __launch_bounds__(256) void ar_qkv_ksplit_kernel(GemvArgs a) {
+  // The batched GEMM launches are bound by the bytes each CU loads (~30 GB/s per CU from entry to
+  // operands landed, tools/step_timeline.py: 72 KB per CU 2.8 us, 36 KB 1.5 us, nothing 0.5 us), so
+  // the block's operand slice (NT * 16 rows x 192 columns), which all four waves multiply, is loaded
+  // once and shared through LDS: four waves each loading it measured as slow as the one-launch layout.
+  // B = 32, t = 512: c_attn 3.9 -> 2.0 us per launch, 154.3 -> 149.6 us per step.
+  constexpr int XR = NT * 16, XS = 200;  // rows, bf16 row stride (400 B: 16 rows hit distinct bank groups)
+  __shared__ __attribute__((aligned(16))) bf16_t xs[XR * XS];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int n0 = (blockIdx.x * 4 + wave) * 16, ks = blockIdx.y;
+  const int B = a.B;
+  TS_DECL;
+  TS_MARK(0);
+  const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(a.W);
+  const bf16_t* __restrict__ X = a.st.xn;
+  // operand slice first (vmcnt retires in issue order: the LDS fill then waits for it alone): the
+  // XR x 24 16-B chunks spread over the block, chunk c = tid + 256 j -> row c / 24, chunk c % 24
+  constexpr int XC = XR * 24 / 256;
+  static_assert(XR * 24 % 256 == 0, "operand chunks per thread");
+  uint4 xv[XC];
+#pragma unroll
+  for (int j = 0; j < XC; ++j) {
+    const int c = tid + 256 * j, r = c / 24, q = c - r * 24;
+    xv[j] = *reinterpret_cast<const uint4*>(X + (size_t)min(r, B - 1) * D + ks * 192 + q * 8);  // rows past B: row B-1, never stored
+  }
+  const int k0 = ks * 192 + 8 * (lane >> 4);
+  uint4 wf[6], xf[NT][6];
+#pragma unroll
+  for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(W + (size_t)(n0 + (lane & 15)) * D + k0 + kk * 32);
+#pragma unroll
+  for (int j = 0; j < XC; ++j) {
+    const int c = tid + 256 * j, r = c / 24, q = c - r * 24;
+    *reinterpret_cast<uint4*>(xs + r * XS + q * 8) = xv[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int kk = 0; kk < 6; ++kk)
+      xf[t][kk] = *reinterpret_cast<const uint4*>(xs + (t * 16 + (lane & 15)) * XS + 8 * (lane >> 4) + kk * 32);
+  __builtin_amdgcn_sched_barrier(0);
+  f32x4_t acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < 6; ++kk)
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[kk]),
+                                                       __builtin_bit_cast(bf16x8_t, xf[t][kk]), acc[t], 0, 0, 0);
+  TS_MARK(1);
+  // lane: C[n0 + 4 (lane >> 4) + i][t * 16 + (lane & 15)], i = 0..3
+  float* dst = a.st.qkvp + (size_t)ks * a.st.max_streams * (3 * D) + n0 + 4 * (lane >> 4);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int b = t * 16 + (lane & 15);
+    if (b < B) *reinterpret_cast<float4*>(dst + (size_t)b * (3 * D)) = make_float4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
+  }
+  TS_SAVE(1, a.layer, blockIdx.x + gridDim.x * blockIdx.y);
+}
+static_assert(3 * D == 4 * 16 * 36, "qkv_ksplit: 36 blocks of 64 rows");
+
+template <typename TW>
+static bool qkv_ksplit(int B, int kvdtype);  // defined with the B-dependent kernel choice below
+
 // mlp c_proj (K = 3072) split into YCOPIES K slices of 768: 4x the blocks of the unsplit GEMM;
 // each slice's partial goes to its pending copy (plain stores, deterministic), folded into x by
 // the next c_proj and read as x + sum of copies by the next c_attn / lm_head prologue
@@ -1783,9 +1914,11 @@ static int attn_ns_max(int B) {  // enough splits to fill the chip, no more (ear
 }
 
 static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_t s, int ns_max = NSPLIT,
-                        int direct = 0, int selcopy = 0) {
+                        int direct = 0, int selcopy = 0, bool qkv = false) {
   dim3 grid(ns_max, N_HEAD, B);
-  if (kvdtype == LVX_DTYPE_BF16)
+  if (qkv)  // c_attn left K-slice partials (qkv_ksplit): bf16 KV, direct, one split
+    hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2, 4, true>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
+  else if (kvdtype == LVX_DTYPE_BF16)
     hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2, 4>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
   else if (kvdtype == LVX_DTYPE_FP8)
     hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t, 2, 4>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
@@ -1856,6 +1989,14 @@ static bool fused_mlp(int B) {
   return sizeof(TW) == 2 && g_opt_fuse_mlp && B <= 2 && !use_mfma<TW>(B);
 }
 
+// c_attn as K-slice partials summed by the attention: batched bf16 steps with one attention block
+// per (row, head) (attn_ns_max(B) == 1 and the v2 kernels: 17 <= B <= 32), bf16 KV
+template <typename TW>
+static bool qkv_ksplit(int B, int kvdtype) {
+  return use_mfma<TW>(B) && !use_bt<TW>(B) && B > MFMA_LN_MAX && B <= 32 && attn_ns_max(B) == 1 &&
+         kvdtype == LVX_DTYPE_BF16 && !(g_opt_exp & 1);
+}
+
 // returns false when the op has no kernel of its own at this B (mlp c_proj inside the fused MLP)
 template <typename TW>
 static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtype, int B, hipStream_t s) {
@@ -1874,14 +2015,16 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       a.W = w.w_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
       if (mf && l == 0 && a.defer_sel == 2) {  // embedding + the previous step's select, then c_attn
         hipLaunchKernelGGL(ar_embed_select_kernel, dim3(B), dim3(256), 0, s, a);
-        launch_mfma2<768, 0>(a, s);
+        if (qkv_ksplit<TW>(B, kvdtype)) hipLaunchKernelGGL(ar_qkv_ksplit_kernel<2>, dim3(36, 4), dim3(256), 0, s, a);
+        else launch_mfma2<768, 0>(a, s);
       } else if (mf && B <= MFMA_LN_MAX) {
         if (l == 0) launch_mfma_ln<0, 3>(a, s);
         else launch_mfma_ln<0, 4>(a, s);
       } else if (mf) {  // rows kernel: LayerNorm (layer 0: of the embedding; else of x + the MLP copies)
         if (l == 0) hipLaunchKernelGGL((ar_rows_kernel<3>), dim3(B), dim3(64), 0, s, a);
         else hipLaunchKernelGGL((ar_rows_kernel<4>), dim3(B), dim3(64), 0, s, a);
-        launch_mfma2<768, 0>(a, s);
+        if (qkv_ksplit<TW>(B, kvdtype)) hipLaunchKernelGGL(ar_qkv_ksplit_kernel<2>, dim3(36, 4), dim3(256), 0, s, a);
+        else launch_mfma2<768, 0>(a, s);
       } else if (l == 0 && a.defer_sel) {
         launch_gemv<TW, 768, 1, 2, 5, 0>(a, s);  // + the previous step's select
       } else if (l == 0) {
@@ -1892,7 +2035,9 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
         launch_gemv<TW, 768, 1, 2, 0, 0>(a, s);
       }
       break;
-    case 1: launch_attn(a.st, kvdtype, B, l, s, nsm, mf && nsm == 1, a.defer_sel == 1 && l == 0); break;
+    case 1:
+      launch_attn(a.st, kvdtype, B, l, s, nsm, mf && nsm == 1, a.defer_sel == 1 && l == 0, qkv_ksplit<TW>(B, kvdtype));
+      break;
     case 2:
       a.W = w.w_aproj[l]; a.N = D;
       if (mf) {

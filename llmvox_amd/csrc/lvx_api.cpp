@@ -450,7 +450,7 @@ int lvx_finalize(lvx_ctx* c) {
       (r = c->dalloc(&st.xn, (size_t)S * D)) || (r = c->dalloc(&st.hb, (size_t)S * DFF)) ||
       (r = c->dalloc(&st.xb, (size_t)S * D)) || (r = c->dalloc(&st.xstat, (size_t)(D / 16) * S * 2)) ||
       (r = c->dalloc(&st.lmbest, (size_t)LM_MAX_BLOCKS * 4 * 2)) ||
-      (r = c->dalloc(&st.yacc, (size_t)YCOPIES * S * D)))
+      (r = c->dalloc(&st.yacc, (size_t)YCOPIES * S * D)) || (r = c->dalloc(&st.qkvp, (size_t)4 * S * 3 * D)))
     return r;
   HIP_TRY(hipMemset(st.yacc, 0, (size_t)YCOPIES * S * D * 4));
   HIP_TRY(hipMemset(st.selp, 0, 16));

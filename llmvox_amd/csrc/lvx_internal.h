@@ -65,6 +65,7 @@ struct ArState {
   bf16_t* xb = nullptr;         // [B][768] bf16 copy of x after c_proj (batched path: c_fc's operand, normalised from xstat)
   float* xstat = nullptr;       // [max_streams][48 column blocks][2] (mean, M2) of x over 16 columns
   float* logits = nullptr;      // [B][4096]
+  float* qkvp = nullptr;        // [4][max_streams][2304] c_attn K-slice partials (batched B > 16: summed by the attention)
   uint64_t* lmbest = nullptr;   // [LM_MAX_BLOCKS][4][2] per-block top1/top2 granules of lm_head (deferred select, B <= 2)
   float* yacc = nullptr;        // [max_streams][YCOPIES][768] fused-MLP output accumulators (fp32 atomics);
                                 // a row's copies adjacent: spaced by max_streams rows they shared

@@ -4,14 +4,14 @@
 in step order: blocks, CUs, first/last entry and last exit relative to the step's first entry, the
 median entry->operands and operands->exit spans, and the gap from the previous kernel's last exit
 to this kernel's first entry (the boundary as the CUs see it).
-usage: python tools/step_timeline.py [B] [P0] [graphs 0/1]"""
+usage: python tools/step_timeline.py [B] [P0] [graphs 0/1] [opt=value,...]"""
 import ctypes
 import os
 import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["LVX_LIB_PATH"] = os.path.join(ROOT, "llmvox_amd", "libllmvox_hip_timing.so")
+os.environ.setdefault("LVX_LIB_PATH", os.path.join(ROOT, "llmvox_amd", "libllmvox_hip_timing.so"))
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -30,6 +30,9 @@ lib.lvx_debug_timeline.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_in
 
 e = build_engine(0, "bf16", "bf16", max_streams=B, max_positions=P0 + 512, max_codec_frames=256)
 dev = e.device
+for kv in (sys.argv[4].split(",") if len(sys.argv) > 4 else []):
+    k, v = kv.split("=")
+    e.set_option(k, int(v))
 stream = torch.cuda.Stream(device=dev) if graphs else torch.cuda.current_stream(dev)
 plan = torch.full((B, 64), 100, dtype=torch.int32, device=dev)
 slots = torch.arange(B, dtype=torch.int32, device=dev)
