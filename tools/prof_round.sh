@@ -27,6 +27,8 @@ python3 tools/pmc_codec.py $(csv m) $CKEY $O/pmc_codec.json || exit 1
 rm -rf $O/m
 run kt 300 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 bench.py $ARGS
 find $O/kt -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
+python3 tools/probe_trace.py $(find $O/kt -name "*kernel_trace.csv" | head -1) > $O/probe_trace.txt || exit 1
+cat $O/probe_trace.txt
 rm -rf $O/kt
 timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.jsonl 2> $O/bench.err || { echo BENCH_FAIL; tail -20 $O/bench.err; exit 1; }
 tail -c 600 $O/bench.jsonl
