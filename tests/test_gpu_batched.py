@@ -130,3 +130,26 @@ def test_v3_path_agrees_with_v2(eng, B):
     finally:
         eng.set_option("bt", eng.bt_mode)
     assert np.abs(got - ref).max() < 0.02 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("B", [17, 32])
+def test_qkv_ksplit_matches_one_launch_cattn(B):
+    """17 <= B <= 32 (bf16): c_attn runs as K-slice partials summed by the attention, which also
+    appends the new key (ar_qkv_ksplit_kernel); option exp bit 1 restores the one-launch c_attn with
+    the KV append in its epilogue. Same K-slice order: tokens, margins and logits bit for bit, with
+    permuted slots and ragged positions."""
+    from llmvox_amd.engine import build_engine
+    e = build_engine(0, "bf16", "bf16", max_streams=64, max_positions=512, max_codec_frames=256)
+    try:
+        texts = _texts(B, 96, seed=11)
+        order = list(np.random.default_rng(B).permutation(B))
+        prefix = set(range(0, B, 3))
+        res = []
+        for exp in (0, 1):
+            e.set_option("exp", exp)
+            res.append(_run(e, order, texts, prefix, 40, 56))
+        e.set_option("exp", 0)
+        np.testing.assert_array_equal(res[0][0], res[1][0])
+        np.testing.assert_array_equal(res[0][1], res[1][1])
+    finally:
+        e.close()
