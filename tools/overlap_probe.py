@@ -3,7 +3,7 @@ small GEMMs (latency-bound). Do two half-batches on two HIP streams (two engines
 scratch) overlap one's attention with the other's GEMMs? Prints us per step of 32 rows for
 1 chain x B = 32 vs 2 chains x B = 16 (and 4 x 8), starting at KV position P, N steps,
 graph replays (side streams) and eager launches.
-usage: python tools/overlap_probe.py [P] [N]"""
+usage: python tools/overlap_probe.py [P] [N] [CHAINSxB ...] (default 1x32 2x16 4x8 1x16 1x8)"""
 import sys
 import time
 
@@ -53,6 +53,7 @@ def run(n_chains, B, graphs):
           f"({us * 32 / (n_chains * B):7.1f} us per 32 rows)  {n_chains * B * N / best:9.0f} tok/s", flush=True)
 
 
+cfgs = [tuple(int(v) for v in c.split("x")) for c in sys.argv[3:]] or [(1, 32), (2, 16), (4, 8), (1, 16), (1, 8)]
 for graphs in (True, False):
-    for n, B in [(1, 32), (2, 16), (4, 8), (1, 16), (1, 8)]:
+    for n, B in cfgs:
         run(n, B, graphs)
