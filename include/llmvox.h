@@ -152,7 +152,10 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
  *   "bt"           1: batched path v3 for 32 < B <= 64; 2: v3 for every batched B; 0: never;
  *   "codec_g2"     1: large-M bf16 codec GEMMs on the 128 x 128 MFMA tile kernel; 0: the general one;
  *   "codec_skinny" 1: bf16 codec weight GEMMs with M <= 384 frames on the K-split-over-waves kernel
- *                     (no split-K combine); 0: the tile kernels. */
+ *                     (no split-K combine); 0: the tile kernels;
+ *   "exp"          development bits, 0 = production kernels; bit 1: at 17 <= B <= 32 (bf16) c_attn
+ *                     as one launch with the KV append in its epilogue instead of K-slice partials
+ *                     summed by the attention (bit-identical: tests/test_gpu_batched.py). */
 int lvx_set_option(lvx_ctx* ctx, const char* name, int value);
 /* Enable/disable HIP-graph replay of lvx_ar_step for a given B (default on). */
 int lvx_set_graphs(lvx_ctx* ctx, int enable);
