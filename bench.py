@@ -400,7 +400,7 @@ def run_config3(args, eng, world, rank, local, dist):
         rl["pmc_key"] = pmc_key(args.dtype, args.kv_dtype or args.dtype, S, N)
         rl["traffic"] = pmc_traffic(rl["pmc_key"], dom["name"])
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the CPU baseline: N = 1 runs only
         cpu = cpu_baseline(0, 0, schedule=dump_schedule(N, 10))
     if rank == 0:
         out = {
@@ -779,11 +779,11 @@ def main():
              "gemm_mfma_busy": pmc_codec(ckey), "pmc_key": ckey}
 
     parity = None
-    if rank == 0 and not args.no_parity_line and args.dtype == "bf16" and args.config in (1, 2):
+    if rank == 0 and world == 1 and not args.no_parity_line and args.dtype == "bf16" and args.config in (1, 2):
         parity = parity_mode_line(S, chunk)
 
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the CPU baseline: N = 1 runs only
         # the same utterance length as the timed run (one stream: the oracle is B = 1)
         cpu = cpu_baseline(min(K, reset_every) if reset_every else K, chunk)
 
