@@ -81,12 +81,12 @@ def plan_for(ids, start, n, pad=384):
 # ---------------------------------------------------------------------------------------
 def kernel_bytes(which, B, t, wbytes, kvbytes):
     """Algorithmic HBM bytes of one launch (weights streamed once + KV + activations). At
-    17 <= B <= 32 with bf16 weights and KV, c_attn hands its output to the attention as four K-slice
+    9 <= B <= 32 with bf16 weights and KV, c_attn hands its output to the attention as four K-slice
     partials (ar_qkv_ksplit_kernel: 4 x 2,304 fp32 per row written, read back by the attention, which
     also appends the new key)."""
     D, F, V = 768, 3072, 4096
     act = 4 * B
-    ksplit = wbytes == 2 and kvbytes == 2 and 17 <= B <= 32
+    ksplit = wbytes == 2 and kvbytes == 2 and 9 <= B <= 32
     if which == 0:
         if ksplit:
             return 3 * D * D * wbytes + 2 * D * B + act * 4 * 3 * D

@@ -153,7 +153,7 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
  *   "codec_g2"     1: large-M bf16 codec GEMMs on the 128 x 128 MFMA tile kernel; 0: the general one;
  *   "codec_skinny" 1: bf16 codec weight GEMMs with M <= 384 frames on the K-split-over-waves kernel
  *                     (no split-K combine); 0: the tile kernels;
- *   "exp"          development bits, 0 = production kernels; bit 1: at 17 <= B <= 32 (bf16) c_attn
+ *   "exp"          development bits, 0 = production kernels; bit 1: at 9 <= B <= 32 (bf16) c_attn
  *                     as one launch with the KV append in its epilogue instead of K-slice partials
  *                     summed by the attention (bit-identical: tests/test_gpu_batched.py). */
 int lvx_set_option(lvx_ctx* ctx, const char* name, int value);

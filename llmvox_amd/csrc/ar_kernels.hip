@@ -931,10 +931,11 @@ template <> struct KvPiece<fp8_t> {
 // direct = 1 (batched path with one split per (row, head)): the normalised head output goes
 // straight to the bf16 operand row xn, as the merge kernel would write it (o * (1 / l)), and the
 // merge kernel is skipped.
-// QKV (bf16 KV, direct: 17 <= B <= 32): c_attn left its output as four K-slice partials
+// QKV (bf16 KV, 9 <= B <= 32): c_attn left its output as four K-slice partials
 // (ar_qkv_ksplit_kernel, st.qkvp); threads 0-287 sum them in the K-slice order the one-launch GEMM
-// summed its waves (bit-identical), q goes through LDS, the new key's K / V are appended to the cache
-// here, and the tile holding key t - 1 takes them from LDS (this block's own store is not read back).
+// summed its waves (bit-identical), q goes through LDS, and the split holding key t - 1 appends the
+// new key's K / V to the cache and takes them from LDS in its last tile (its own store is not read
+// back).
 template <typename TKV, int DEPTH, int NW, bool QKV = false>
 __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int layer, int ns_max, int direct,
                                                          int selcopy) {
@@ -1067,7 +1068,7 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
       for (int k = 0; k < 4; ++k) v += pq[h][k];
       if (e < HD) {
         qs_s[e] = v;
-      } else if (e < 3 * HD) {  // K / V of the new key: appended to the cache, kept in LDS
+      } else if (e < 3 * HD && k1 == t) {  // K / V of the new key (the last split): appended, kept in LDS
         const int which = e / HD - 1, d = e % HD;
         const bf16_t hv = f32_to_bf16(v);
         kvh_s[which][d] = hv;
@@ -1600,12 +1601,11 @@ __global__ __launch_bounds__(256) void ar_qkv_ksplit_kernel(GemvArgs a) {
   const bf16_t* __restrict__ X = a.st.xn;
   // operand slice first (vmcnt retires in issue order: the LDS fill then waits for it alone): the
   // XR x 24 16-B chunks spread over the block, chunk c = tid + 256 j -> row c / 24, chunk c % 24
-  constexpr int XC = XR * 24 / 256;
-  static_assert(XR * 24 % 256 == 0, "operand chunks per thread");
+  constexpr int XC = (XR * 24 + 255) / 256;
   uint4 xv[XC];
 #pragma unroll
   for (int j = 0; j < XC; ++j) {
-    const int c = tid + 256 * j, r = c / 24, q = c - r * 24;
+    const int c = min(tid + 256 * j, XR * 24 - 1), r = c / 24, q = c - r * 24;
     xv[j] = *reinterpret_cast<const uint4*>(X + (size_t)min(r, B - 1) * D + ks * 192 + q * 8);  // rows past B: row B-1, never stored
   }
   const int k0 = ks * 192 + 8 * (lane >> 4);
@@ -1615,7 +1615,7 @@ __global__ __launch_bounds__(256) void ar_qkv_ksplit_kernel(GemvArgs a) {
 #pragma unroll
   for (int j = 0; j < XC; ++j) {
     const int c = tid + 256 * j, r = c / 24, q = c - r * 24;
-    *reinterpret_cast<uint4*>(xs + r * XS + q * 8) = xv[j];
+    if (c < XR * 24) *reinterpret_cast<uint4*>(xs + r * XS + q * 8) = xv[j];
   }
   __syncthreads();
 #pragma unroll
@@ -1916,7 +1916,7 @@ static int attn_ns_max(int B) {  // enough splits to fill the chip, no more (ear
 static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_t s, int ns_max = NSPLIT,
                         int direct = 0, int selcopy = 0, bool qkv = false) {
   dim3 grid(ns_max, N_HEAD, B);
-  if (qkv)  // c_attn left K-slice partials (qkv_ksplit): bf16 KV, direct, one split
+  if (qkv)  // c_attn left K-slice partials (qkv_ksplit): bf16 KV
     hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2, 4, true>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
   else if (kvdtype == LVX_DTYPE_BF16)
     hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2, 4>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
@@ -1989,12 +1989,16 @@ static bool fused_mlp(int B) {
   return sizeof(TW) == 2 && g_opt_fuse_mlp && B <= 2 && !use_mfma<TW>(B);
 }
 
-// c_attn as K-slice partials summed by the attention: batched bf16 steps with one attention block
-// per (row, head) (attn_ns_max(B) == 1 and the v2 kernels: 17 <= B <= 32), bf16 KV
+// c_attn as K-slice partials summed by the attention: batched bf16 steps on the v2 kernels with the
+// rows kernel before c_attn (9 <= B <= 32), bf16 KV
 template <typename TW>
 static bool qkv_ksplit(int B, int kvdtype) {
-  return use_mfma<TW>(B) && !use_bt<TW>(B) && B > MFMA_LN_MAX && B <= 32 && attn_ns_max(B) == 1 &&
-         kvdtype == LVX_DTYPE_BF16 && !(g_opt_exp & 1);
+  return use_mfma<TW>(B) && !use_bt<TW>(B) && B > MFMA_LN_MAX && B <= 32 && kvdtype == LVX_DTYPE_BF16 &&
+         !(g_opt_exp & 1);
+}
+static void launch_qkv_ksplit(const GemvArgs& a, hipStream_t s) {
+  if (a.B <= 16) hipLaunchKernelGGL(ar_qkv_ksplit_kernel<1>, dim3(36, 4), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(ar_qkv_ksplit_kernel<2>, dim3(36, 4), dim3(256), 0, s, a);
 }
 
 // returns false when the op has no kernel of its own at this B (mlp c_proj inside the fused MLP)
@@ -2015,7 +2019,7 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       a.W = w.w_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
       if (mf && l == 0 && a.defer_sel == 2) {  // embedding + the previous step's select, then c_attn
         hipLaunchKernelGGL(ar_embed_select_kernel, dim3(B), dim3(256), 0, s, a);
-        if (qkv_ksplit<TW>(B, kvdtype)) hipLaunchKernelGGL(ar_qkv_ksplit_kernel<2>, dim3(36, 4), dim3(256), 0, s, a);
+        if (qkv_ksplit<TW>(B, kvdtype)) launch_qkv_ksplit(a, s);
         else launch_mfma2<768, 0>(a, s);
       } else if (mf && B <= MFMA_LN_MAX) {
         if (l == 0) launch_mfma_ln<0, 3>(a, s);
@@ -2023,7 +2027,7 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       } else if (mf) {  // rows kernel: LayerNorm (layer 0: of the embedding; else of x + the MLP copies)
         if (l == 0) hipLaunchKernelGGL((ar_rows_kernel<3>), dim3(B), dim3(64), 0, s, a);
         else hipLaunchKernelGGL((ar_rows_kernel<4>), dim3(B), dim3(64), 0, s, a);
-        if (qkv_ksplit<TW>(B, kvdtype)) hipLaunchKernelGGL(ar_qkv_ksplit_kernel<2>, dim3(36, 4), dim3(256), 0, s, a);
+        if (qkv_ksplit<TW>(B, kvdtype)) launch_qkv_ksplit(a, s);
         else launch_mfma2<768, 0>(a, s);
       } else if (l == 0 && a.defer_sel) {
         launch_gemv<TW, 768, 1, 2, 5, 0>(a, s);  // + the previous step's select
