@@ -1602,10 +1602,11 @@ __global__ __launch_bounds__(256) void ar_qkv_ksplit_kernel(GemvArgs a) {
   // operand slice first (vmcnt retires in issue order: the LDS fill then waits for it alone): the
   // XR x 24 16-B chunks spread over the block, chunk c = tid + 256 j -> row c / 24, chunk c % 24
   constexpr int XC = (XR * 24 + 255) / 256;
+  constexpr bool EXACT = XR * 24 % 256 == 0;  // NT = 2: three chunks per thread; NT = 1: 1.5 (clamped)
   uint4 xv[XC];
 #pragma unroll
   for (int j = 0; j < XC; ++j) {
-    const int c = min(tid + 256 * j, XR * 24 - 1), r = c / 24, q = c - r * 24;
+    const int c = EXACT ? tid + 256 * j : min(tid + 256 * j, XR * 24 - 1), r = c / 24, q = c - r * 24;
     xv[j] = *reinterpret_cast<const uint4*>(X + (size_t)min(r, B - 1) * D + ks * 192 + q * 8);  // rows past B: row B-1, never stored
   }
   const int k0 = ks * 192 + 8 * (lane >> 4);
@@ -1615,7 +1616,7 @@ __global__ __launch_bounds__(256) void ar_qkv_ksplit_kernel(GemvArgs a) {
 #pragma unroll
   for (int j = 0; j < XC; ++j) {
     const int c = tid + 256 * j, r = c / 24, q = c - r * 24;
-    if (c < XR * 24) *reinterpret_cast<uint4*>(xs + r * XS + q * 8) = xv[j];
+    if (EXACT || c < XR * 24) *reinterpret_cast<uint4*>(xs + r * XS + q * 8) = xv[j];
   }
   __syncthreads();
 #pragma unroll
