@@ -576,7 +576,7 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
             const int s = ri.x, p = ri.y;
             if (s < 0) continue;
             const size_t idx =
-                ((((size_t)a.layer * a.st.max_streams + s) * N_HEAD + head) * a.st.max_pos + p) * HD + d;
+                kv_at(a.layer, a.st.kv_chunks, a.st.max_streams, s, head, p) + d;
             store_kv(a, which, idx, v);
           }
         } else if (OUT == 1) {
@@ -633,7 +633,7 @@ __device__ __forceinline__ void gemv_store(const GemvArgs& a, int n, int b, floa
       const int head = c / HD, d = c - head * HD;
       const int4 ri = a.st.rowinfo[b];
       if (ri.x < 0) return;
-      const size_t idx = ((((size_t)a.layer * a.st.max_streams + ri.x) * N_HEAD + head) * a.st.max_pos + ri.y) * HD + d;
+      const size_t idx = kv_at(a.layer, a.st.kv_chunks, a.st.max_streams, ri.x, head, ri.y) + d;
       store_kv(a, which, idx, v);
     }
   } else if (OUT == 1) {
@@ -989,9 +989,12 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
   if (sp >= ns) return;
   const int chunk = (t + ns - 1) / ns;
   const int k0 = sp * chunk, k1 = min(t, k0 + chunk);
-  const size_t base = (((size_t)layer * st.max_streams + s) * N_HEAD + head) * st.max_pos;
-  const TKV* __restrict__ Kg = reinterpret_cast<const TKV*>(st.kc) + base * HD;
-  const TKV* __restrict__ Vg = reinterpret_cast<const TKV*>(st.vc) + base * HD;
+  // key k of this (slot, head): chunk k / KV_CHUNK (cstride elements apart), row k % KV_CHUNK
+  const size_t base = kv_at(layer, st.kv_chunks, st.max_streams, s, head, 0);
+  const size_t cstride = (size_t)st.max_streams * N_HEAD * KV_CHUNK * HD;
+  const TKV* __restrict__ Kg = reinterpret_cast<const TKV*>(st.kc) + base;
+  const TKV* __restrict__ Vg = reinterpret_cast<const TKV*>(st.vc) + base;
+  auto krow = [&](int k) { return (size_t)(k / KV_CHUNK) * cstride + (size_t)(k % KV_CHUNK) * HD; };
   const int part = tid & 3, kq = tid >> 2;  // key slot within the TK-key tile
   float q[24];
   if constexpr (!QKV) {
@@ -1017,8 +1020,8 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
     const int key = min(kb + kq, k1 - 1);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      kp[i].load(Kg + (size_t)key * HD + part * 24 + i * 8);
-      vp[i].load(Vg + (size_t)key * HD + part * 24 + i * 8);
+      kp[i].load(Kg + krow(key) + part * 24 + i * 8);
+      vp[i].load(Vg + krow(key) + part * 24 + i * 8);
     }
   };
   auto tile = [&](int kb, const KvPiece<TKV>(&kp)[3], const KvPiece<TKV>(&vp)[3]) {
@@ -1072,7 +1075,7 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
         const int which = e / HD - 1, d = e % HD;
         const bf16_t hv = f32_to_bf16(v);
         kvh_s[which][d] = hv;
-        reinterpret_cast<bf16_t*>(which ? st.vc : st.kc)[(base + ri.y) * HD + d] = hv;
+        reinterpret_cast<bf16_t*>(which ? st.vc : st.kc)[base + krow(ri.y) + d] = hv;
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1525,7 +1528,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
       const int c = (n - D) % D, which = (n - D) / D;
       const int head = c / HD, d = c - head * HD;
       if (ripre.x < 0) continue;
-      const size_t idx = ((((size_t)a.layer * a.st.max_streams + ripre.x) * N_HEAD + head) * a.st.max_pos + ripre.y) * HD + d;
+      const size_t idx = kv_at(a.layer, a.st.kv_chunks, a.st.max_streams, ripre.x, head, ripre.y) + d;
       store_kv(a, which, idx, v);
     } else if (OUT == 5) {
       if constexpr (XM == 1) {  // LayerNorm after the GEMM: rstd * (v - mean * G[n])

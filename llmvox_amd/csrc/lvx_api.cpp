@@ -440,6 +440,7 @@ int lvx_finalize(lvx_ctx* c) {
   const int S = c->cfg.max_streams, P = c->cfg.max_positions;
   st.max_pos = P;
   st.max_streams = S;
+  st.kv_chunks = (P + KV_CHUNK - 1) / KV_CHUNK;
   if ((r = c->dalloc(&st.slots, S)) || (r = c->dalloc(&st.pos, S)) || (r = c->dalloc(&st.prev, S)) ||
       (r = c->dalloc(&st.err, 4)) || (r = c->dalloc(&st.x, (size_t)S * D)) || (r = c->dalloc(&st.q, (size_t)S * D)) ||
       (r = c->dalloc(&st.part_o, (size_t)S * N_HEAD * NSPLIT * HD)) ||
@@ -459,7 +460,7 @@ int lvx_finalize(lvx_ctx* c) {
   HIP_TRY(hipMemset(st.pos, 0, S * 4));
   HIP_TRY(hipMemset(st.prev, 0, S * 4));
   HIP_TRY(hipMemset(st.err, 0, 16));
-  const size_t kvn = (size_t)N_LAYER * S * N_HEAD * P * HD;
+  const size_t kvn = (size_t)N_LAYER * st.kv_chunks * S * N_HEAD * KV_CHUNK * HD;
   const size_t kvb = c->cfg.kv_dtype == LVX_DTYPE_BF16 ? 2 : c->cfg.kv_dtype == LVX_DTYPE_FP8 ? 1 : 4;
   {
     char* k;

@@ -12,6 +12,13 @@ namespace lvx {
 constexpr int N_LAYER = 4, N_HEAD = 8, D = 768, HD = 96, DFF = 3072, VOCAB = 4096;
 constexpr int TEXT_DIM = 256, SPEECH_DIM = 512, TEXT_VOCAB = 386, BLOCK_SIZE = 8192;
 constexpr int NSPLIT = 16;  // max KV splits per (stream, head) in decode attention
+// KV cache in chunks of KV_CHUNK positions, chunk-major over (slot, head): the positions a step reads
+// (0..t-1 of every stream) lie in the first ceil(t / KV_CHUNK) chunks of a layer, whatever the
+// capacity (max_positions) is
+constexpr int KV_CHUNK = 64;
+__host__ __device__ inline size_t kv_at(size_t layer, size_t chunks, size_t streams, int s, int head, int pos) {
+  return (((((layer * chunks + (size_t)(pos / KV_CHUNK)) * streams + s) * 8 + head) * KV_CHUNK) + (size_t)(pos % KV_CHUNK)) * 96;
+}
 #ifndef LVX_YCOPIES
 #define LVX_YCOPIES 4
 #endif
@@ -70,9 +77,9 @@ struct ArState {
   float* yacc = nullptr;        // [max_streams][YCOPIES][768] fused-MLP output accumulators (fp32 atomics);
                                 // a row's copies adjacent: spaced by max_streams rows they shared
                                 // L2 channels (B = 1: 82.6 vs 69.6 us/step at max_streams 32)
-  void* kc = nullptr;           // [4][max_streams][8][max_pos][96]
+  void* kc = nullptr;           // [4][kv_chunks][max_streams][8][KV_CHUNK][96] (kv_at)
   void* vc = nullptr;
-  int max_pos = 0, max_streams = 0;
+  int max_pos = 0, max_streams = 0, kv_chunks = 0;
 };
 
 // Launches the whole decode step (embed -> 4 blocks -> lm_head [-> argmax]).
