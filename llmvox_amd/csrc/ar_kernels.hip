@@ -70,6 +70,7 @@ __device__ uint64_t g_lvx_ts[16 * 4 * TS_BLOCKS * 4];
 struct GemvArgs {
   ArState st;
   const void* W;
+  const void* Wf;        // batched MFMA GEMMs: the fragment-packed copy of W (ArWeights f_*), or null
   int N;
   int B;
   int layer;
@@ -1464,8 +1465,13 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
     __builtin_amdgcn_sched_barrier(0);  // keep them ahead of the weight / operand loads
   }
   uint4 wf[6], xf[NT][6];
+  // fragment-packed weights (a.Wf): the wave's 6 loads are 6 contiguous KB
+  const bf16_t* wsrc = a.Wf ? reinterpret_cast<const bf16_t*>(a.Wf) +
+                                  (((size_t)(n0 >> 4) * (KTOT / 32) + (blockIdx.y * K + wave * 192) / 32) * 64 + lane) * 8
+                            : W + (size_t)wrow * KTOT + k0;
+  const int wstep = a.Wf ? 512 : 32;
 #pragma unroll
-  for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(W + (size_t)wrow * KTOT + k0 + kk * 32);
+  for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(wsrc + kk * wstep);
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int b = min(r0 + t * 16 + (lane & 15), B - 1);  // padded columns recompute row B-1, never stored
@@ -1614,8 +1620,11 @@ __global__ __launch_bounds__(256) void ar_qkv_ksplit_kernel(GemvArgs a) {
   }
   const int k0 = ks * 192 + 8 * (lane >> 4);
   uint4 wf[6], xf[NT][6];
+  const bf16_t* wsrc = a.Wf ? reinterpret_cast<const bf16_t*>(a.Wf) + (((size_t)(n0 >> 4) * (D / 32) + ks * 6) * 64 + lane) * 8
+                            : W + (size_t)(n0 + (lane & 15)) * D + k0;
+  const int wstep = a.Wf ? 512 : 32;
 #pragma unroll
-  for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(W + (size_t)(n0 + (lane & 15)) * D + k0 + kk * 32);
+  for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(wsrc + kk * wstep);
 #pragma unroll
   for (int j = 0; j < XC; ++j) {
     const int c = tid + 256 * j, r = c / 24, q = c - r * 24;
@@ -2015,12 +2024,13 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
   const bool mf = use_mfma<TW>(B);
   const bool fm = fused_mlp<TW>(B);
   const int nsm = mf ? attn_ns_max(B) : NSPLIT;
+  const bool pk = mf && !(g_opt_exp & 2);  // fragment-packed weights for the MFMA GEMMs (exp bit 2: row-major)
   a.layer = l;
   a.yacc = (fm || mf) ? a.st.yacc : nullptr;
   a.add_y = l > 0;
   switch (op) {
     case 0:
-      a.W = w.w_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
+      a.W = w.w_attn[l]; a.Wf = pk ? w.f_attn[l] : nullptr; a.N = 3 * D; a.ln_w = w.ln1[l];
       if (mf && l == 0 && a.defer_sel == 2) {  // embedding + the previous step's select, then c_attn
         hipLaunchKernelGGL(ar_embed_select_kernel, dim3(B), dim3(256), 0, s, a);
         if (qkv_ksplit<TW>(B, kvdtype)) launch_qkv_ksplit(a, s);
@@ -2047,7 +2057,7 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       launch_attn(a.st, kvdtype, B, l, s, nsm, mf && nsm == 1, a.defer_sel == 1 && l == 0, qkv_ksplit<TW>(B, kvdtype));
       break;
     case 2:
-      a.W = w.w_aproj[l]; a.N = D;
+      a.W = w.w_aproj[l]; a.Wf = pk ? w.f_aproj[l] : nullptr; a.N = D;
       if (mf) {
         if (B > MFMA_LN_MAX) a.add_y = 0;  // ar_rows_kernel<4> of this layer's c_attn folded them
         if (nsm > 1) launch_merge_bf16(a.st, B, nsm, s);  // nsm == 1: the attention wrote xn itself
@@ -2061,7 +2071,7 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       }
       break;
     case 3:
-      a.W = w.w_fc[l]; a.N = DFF; a.ln_w = w.ln2[l];
+      a.W = w.w_fc[l]; a.Wf = pk ? w.f_fc[l] : nullptr; a.N = DFF; a.ln_w = w.ln2[l];
       if (fm) {  // 16 h rows per block (192 blocks)
         const bf16_t* wfc = reinterpret_cast<const bf16_t*>(w.w_fc[l]);
         const bf16_t* wpk = reinterpret_cast<const bf16_t*>(w.w_mproj_pk[l]);
@@ -2077,13 +2087,13 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       }
       break;
     case 4:
-      a.W = w.w_mproj[l]; a.N = D;
+      a.W = w.w_mproj[l]; a.Wf = pk ? w.f_mproj[l] : nullptr; a.N = D;
       if (fm) return false;
       if (mf) launch_mproj_split<6>(a, s);
       else launch_gemv<TW, 3072, 4, 2, 1, 1>(a, s);
       break;
     case 5:
-      a.W = w.w_lm; a.N = VOCAB; a.ln_w = w.lnf;
+      a.W = w.w_lm; a.Wf = pk ? w.f_lm : nullptr; a.N = VOCAB; a.ln_w = w.lnf;
       if (mf && B <= MFMA_LN_MAX) {
         launch_mfma_ln<3, 4>(a, s);
       } else if (mf) {

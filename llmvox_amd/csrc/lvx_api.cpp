@@ -240,6 +240,18 @@ static std::vector<float> pack_mproj(const std::vector<float>& w) {
   return o;
 }
 
+// [N][K] -> [N / 16][K / 32][64 lanes][8]: lane l of fragment (T, j) holds W[16 T + l % 16][32 j + 8 (l / 16) ..+8],
+// the A operand of v_mfma_f32_16x16x32_bf16 as the batched GEMMs load it (one contiguous KB per wave load)
+static std::vector<float> pack_frag(const std::vector<float>& w, int N, int K) {
+  std::vector<float> o((size_t)N * K);
+  size_t q = 0;
+  for (int t = 0; t < N / 16; ++t)
+    for (int j = 0; j < K / 32; ++j)
+      for (int l = 0; l < 64; ++l)
+        for (int e = 0; e < 8; ++e) o[q++] = w[(size_t)(16 * t + l % 16) * K + 32 * j + 8 * (l / 16) + e];
+  return o;
+}
+
 extern "C" {
 
 int lvx_version(void) { return 1; }
@@ -336,6 +348,10 @@ int lvx_finalize(lvx_ctx* c) {
     UP_W(c->H(p + "mlp.c_proj.weight"), w.w_mproj[i]);
     if (c->cfg.weight_dtype == LVX_DTYPE_BF16) {  // thread-packed copy for the fused MLP (ar_mlp_fused_kernel)
       UP_W(pack_mproj(c->H(p + "mlp.c_proj.weight")), w.w_mproj_pk[i]);
+      UP_W(pack_frag(c->H(p + "attn.c_attn.weight"), 3 * D, D), w.f_attn[i]);
+      UP_W(pack_frag(c->H(p + "attn.c_proj.weight"), D, D), w.f_aproj[i]);
+      UP_W(pack_frag(c->H(p + "mlp.c_fc.weight"), DFF, D), w.f_fc[i]);
+      UP_W(pack_frag(c->H(p + "mlp.c_proj.weight"), D, DFF), w.f_mproj[i]);
       // batched c_fc: LN2(x) . W^T = rstd * ((x * g) . W^T - mean * G), G[n] = sum_k g[k] W[n][k]
       // over the bf16 weights the GEMM multiplies (double accumulation, rounded once)
       const std::vector<float>& wf = c->H(p + "mlp.c_fc.weight");
@@ -356,6 +372,7 @@ int lvx_finalize(lvx_ctx* c) {
   }
   UP_F("transformer.ln_f.weight", w.lnf);
   UP_W(c->H("lm_head.weight"), w.w_lm);
+  if (c->cfg.weight_dtype == LVX_DTYPE_BF16) UP_W(pack_frag(c->H("lm_head.weight"), VOCAB, D), w.f_lm);
   // ---- codec ----
   CodecWeights& cw = c->cw;
   cw.codebook = w.codebook;

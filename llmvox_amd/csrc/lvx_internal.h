@@ -43,6 +43,13 @@ struct ArWeights {
   const float* fc_gsum[N_LAYER] = {};    // bf16 only: G[n] = sum_k ln_2.weight[k] * bf16(c_fc W[n][k]) (batched
                                          // c_fc: LayerNorm applied after the GEMM, ar_mfma2_kernel XM 1)
   const void* w_lm = nullptr;         // [4096][768]
+  // bf16 only: MFMA-fragment-packed copies for the batched GEMMs (pack_frag): [N / 16][K / 32][64][8],
+  // fragment (tile, k-step) = the 1 KB one wave-wide 16-B load of v_mfma_f32_16x16x32_bf16's A operand
+  const void* f_attn[N_LAYER] = {};
+  const void* f_aproj[N_LAYER] = {};
+  const void* f_fc[N_LAYER] = {};
+  const void* f_mproj[N_LAYER] = {};
+  const void* f_lm = nullptr;
 };
 
 // Device-resident decode state + scratch.

@@ -153,3 +153,23 @@ def test_qkv_ksplit_matches_one_launch_cattn(B):
         np.testing.assert_array_equal(res[0][1], res[1][1])
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("B", [8, 32])
+def test_fragment_packed_weights_match_row_major(B):
+    """The batched MFMA GEMMs read an MFMA-fragment-packed copy of the bf16 weights; option exp bit 2
+    reads the row-major matrices: the same products in the same order, bit for bit."""
+    from llmvox_amd.engine import build_engine
+    e = build_engine(0, "bf16", "bf16", max_streams=64, max_positions=512, max_codec_frames=256)
+    try:
+        texts = _texts(B, 64, seed=5)
+        order = list(np.random.default_rng(B + 1).permutation(B))
+        res = []
+        for exp in (0, 2):
+            e.set_option("exp", exp)
+            res.append(_run(e, order, texts, set(range(0, B, 4)), 24, 40))
+        e.set_option("exp", 0)
+        np.testing.assert_array_equal(res[0][0], res[1][0])
+        np.testing.assert_array_equal(res[0][1], res[1][1])
+    finally:
+        e.close()
