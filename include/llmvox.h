@@ -157,7 +157,8 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
  *                     as one launch with the KV append in its epilogue instead of K-slice partials
  *                     summed by the attention (bit-identical: tests/test_gpu_batched.py); bit 2: the
  *                     batched MFMA GEMMs read the row-major weights instead of the fragment-packed
- *                     copy (bit-identical). */
+ *                     copy (bit-identical); bit 4: at 9 <= B <= 32 the bf16 operand rows (xn, xb,
+ *                     hb) row-major instead of fragment-packed (bit-identical). */
 int lvx_set_option(lvx_ctx* ctx, const char* name, int value);
 /* Enable/disable HIP-graph replay of lvx_ar_step for a given B (default on). */
 int lvx_set_graphs(lvx_ctx* ctx, int enable);

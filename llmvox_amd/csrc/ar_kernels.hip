@@ -67,10 +67,19 @@ __device__ uint64_t g_lvx_ts[16 * 4 * TS_BLOCKS * 4];
 // prologue (they do not depend on it), so the HBM/MALL latency overlaps the LN / merge /
 // embed work, and the weights stay in registers across batch groups of BG rows.
 // ---------------------------------------------------------------------------------
+// Operand rows (bf16 [B][K]) in MFMA-fragment order, the B operand of v_mfma_f32_16x16x32_bf16 as
+// the batched GEMMs load it: element (b, k) of tile b / 16, k-step k / 32, lane 16 ((k / 8) % 4) + b % 16,
+// slot k % 8 — one wave-wide 16-B load reads one contiguous KB (row-major: 16 rows x 64 B)
+__device__ __forceinline__ size_t xfrag(int b, int k, int K) {
+  return ((((size_t)(b >> 4) * (K >> 5) + (k >> 5)) * 64 + ((k >> 3) & 3) * 16 + (b & 15)) << 3) + (k & 7);
+}
+
 struct GemvArgs {
   ArState st;
   const void* W;
   const void* Wf;        // batched MFMA GEMMs: the fragment-packed copy of W (ArWeights f_*), or null
+  int xpk;               // batched v2 steps at 9 <= B <= 32: the bf16 operand rows xn / xb / hb are kept
+                         // fragment-packed (xfrag), as the GEMMs load them
   int N;
   int B;
   int layer;
@@ -1128,7 +1137,7 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
       lv += f * wl_s[w];
     }
     if (direct) {
-      st.xn[(size_t)b * D + head * HD + tid] = f32_to_bf16(ov * (1.0f / lv));
+      st.xn[direct == 2 ? xfrag(b, head * HD + tid, D) : (size_t)b * D + head * HD + tid] = f32_to_bf16(ov * (1.0f / lv));
       return;
     }
     st.part_o[((size_t)(b * N_HEAD + head) * NSPLIT + sp) * HD + tid] = ov;
@@ -1290,7 +1299,10 @@ __global__ __launch_bounds__(256) void ar_rows_kernel(GemvArgs a) {
   wave_ln_regs(v, g);
   uint2* dst = reinterpret_cast<uint2*>(a.st.xn + (size_t)b * D);
 #pragma unroll
-  for (int j = 0; j < 3; ++j) dst[j * 64 + lane] = pack4_bf16(v[j]);
+  for (int j = 0; j < 3; ++j) {
+    if (a.xpk) *reinterpret_cast<uint2*>(a.st.xn + xfrag(b, j * 256 + lane * 4, D)) = pack4_bf16(v[j]);
+    else dst[j * 64 + lane] = pack4_bf16(v[j]);
+  }
   TS_SAVE(a.N == VOCAB ? 8 : 0, a.layer, blockIdx.x);
 }
 
@@ -1357,7 +1369,10 @@ __global__ __launch_bounds__(256) void ar_embed_select_kernel(GemvArgs a) {
   wave_ln_regs(v, g);
   uint2* dst = reinterpret_cast<uint2*>(a.st.xn + (size_t)b * D);
 #pragma unroll
-  for (int j = 0; j < 3; ++j) dst[j * 64 + lane] = pack4_bf16(v[j]);
+  for (int j = 0; j < 3; ++j) {
+    if (a.xpk) *reinterpret_cast<uint2*>(a.st.xn + xfrag(b, j * 256 + lane * 4, D)) = pack4_bf16(v[j]);
+    else dst[j * 64 + lane] = pack4_bf16(v[j]);
+  }
   // the plan load for the next text id last: waiting for it earlier held the embedding loads
   if (take && lane == 0) a.st.rowx[b] = make_int2(rx.x + 1, plan_tok(a.st, b, rx.x + 2));
   TS_SAVE(7, 0, b);
@@ -1366,7 +1381,7 @@ __global__ __launch_bounds__(256) void ar_embed_select_kernel(GemvArgs a) {
 // split-KV merge for the batched path: y[b] (bf16) into st.xn. NS = ns_max (the attention's split
 // count at this B): only the splits that can exist are loaded
 template <int NS>
-__global__ __launch_bounds__(256) void ar_merge_bf16_kernel(ArState st, int ns_max) {
+__global__ __launch_bounds__(256) void ar_merge_bf16_kernel(ArState st, int ns_max, int xpk) {
   __shared__ float cf[N_HEAD * NSPLIT];
   const int b = blockIdx.x, tid = threadIdx.x;
   const int4 ri = st.rowinfo[b];
@@ -1398,15 +1413,15 @@ __global__ __launch_bounds__(256) void ar_merge_bf16_kernel(ArState st, int ns_m
     float y = 0.f;
 #pragma unroll
     for (int i = 0; i < NS; ++i) y += cf[head * NSPLIT + i] * pv[j][i];
-    st.xn[(size_t)b * D + e] = f32_to_bf16(y);
+    st.xn[xpk ? xfrag(b, e, D) : (size_t)b * D + e] = f32_to_bf16(y);
   }
 }
 
-static void launch_merge_bf16(const ArState& st, int B, int nsm, hipStream_t s) {
-  if (nsm <= 2) hipLaunchKernelGGL(ar_merge_bf16_kernel<2>, dim3(B), dim3(256), 0, s, st, nsm);
-  else if (nsm <= 4) hipLaunchKernelGGL(ar_merge_bf16_kernel<4>, dim3(B), dim3(256), 0, s, st, nsm);
-  else if (nsm <= 8) hipLaunchKernelGGL(ar_merge_bf16_kernel<8>, dim3(B), dim3(256), 0, s, st, nsm);
-  else hipLaunchKernelGGL(ar_merge_bf16_kernel<NSPLIT>, dim3(B), dim3(256), 0, s, st, nsm);
+static void launch_merge_bf16(const ArState& st, int B, int nsm, hipStream_t s, int xpk = 0) {
+  if (nsm <= 2) hipLaunchKernelGGL(ar_merge_bf16_kernel<2>, dim3(B), dim3(256), 0, s, st, nsm, xpk);
+  else if (nsm <= 4) hipLaunchKernelGGL(ar_merge_bf16_kernel<4>, dim3(B), dim3(256), 0, s, st, nsm, xpk);
+  else if (nsm <= 8) hipLaunchKernelGGL(ar_merge_bf16_kernel<8>, dim3(B), dim3(256), 0, s, st, nsm, xpk);
+  else hipLaunchKernelGGL(ar_merge_bf16_kernel<NSPLIT>, dim3(B), dim3(256), 0, s, st, nsm, xpk);
 }
 
 // OUT as gemv_store, plus OUT 5: h (bf16) = gelu_tanh(v) for the batched mlp c_proj. A block
@@ -1475,8 +1490,13 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int b = min(r0 + t * 16 + (lane & 15), B - 1);  // padded columns recompute row B-1, never stored
+    // fragment-packed rows (a.xpk): the tile's 6 fragments are 6 contiguous KB (padded rows: whatever
+    // the tile holds there, never stored)
+    const bf16_t* xsrc = a.xpk ? X + ((((size_t)(r0 >> 4) + t) * (KTOT / 32) + (blockIdx.y * K + wave * 192) / 32) * 64 + lane) * 8
+                               : X + (size_t)b * KTOT + k0;
+    const int xstep = a.xpk ? 512 : 32;
 #pragma unroll
-    for (int kk = 0; kk < 6; ++kk) xf[t][kk] = *reinterpret_cast<const uint4*>(X + (size_t)b * KTOT + k0 + kk * 32);
+    for (int kk = 0; kk < 6; ++kk) xf[t][kk] = *reinterpret_cast<const uint4*>(xsrc + kk * xstep);
   }
   // every operand load in flight before the first MFMA (left to itself the scheduler interleaves
   // them with the MFMAs: ~7 KB in flight per wave instead of (6 + 6 NT) KB)
@@ -1541,11 +1561,11 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
         const float2 st = rs[b - r0];
         v = (v - st.x * gpre[k]) * st.y;
       }
-      a.st.hb[(size_t)b * DFF + n] = f32_to_bf16(gelu_tanh(v));
+      a.st.hb[a.xpk ? xfrag(b, n, DFF) : (size_t)b * DFF + n] = f32_to_bf16(gelu_tanh(v));
     } else if (OUT == 7) {
       const float xn = xpre[k] + v;
       a.st.x[(size_t)b * D + n] = xn;
-      a.st.xb[(size_t)b * D + n] = f32_to_bf16(xn * gpre[k]);
+      a.st.xb[a.xpk ? xfrag(b, n, D) : (size_t)b * D + n] = f32_to_bf16(xn * gpre[k]);
       xo[e] = xn;
     } else {
       gemv_store<OUT>(a, n, b, v);
@@ -1616,7 +1636,11 @@ __global__ __launch_bounds__(256) void ar_qkv_ksplit_kernel(GemvArgs a) {
 #pragma unroll
   for (int j = 0; j < XC; ++j) {
     const int c = EXACT ? tid + 256 * j : min(tid + 256 * j, XR * 24 - 1), r = c / 24, q = c - r * 24;
-    xv[j] = *reinterpret_cast<const uint4*>(X + (size_t)min(r, B - 1) * D + ks * 192 + q * 8);  // rows past B: row B-1, never stored
+    // a.xpk: the slice is NT x 6 fragments (chunk c = fragment c / 64, lane c % 64), else rows of 384 B
+    // (rows past B: row B-1 / whatever the tile holds, never stored)
+    const bf16_t* src = a.xpk ? X + ((((size_t)(c / 384) * (D / 32) + ks * 6 + (c % 384) / 64) * 64 + (c & 63)) << 3)
+                              : X + (size_t)min(r, B - 1) * D + ks * 192 + q * 8;
+    xv[j] = *reinterpret_cast<const uint4*>(src);
   }
   const int k0 = ks * 192 + 8 * (lane >> 4);
   uint4 wf[6], xf[NT][6];
@@ -1628,14 +1652,15 @@ __global__ __launch_bounds__(256) void ar_qkv_ksplit_kernel(GemvArgs a) {
 #pragma unroll
   for (int j = 0; j < XC; ++j) {
     const int c = tid + 256 * j, r = c / 24, q = c - r * 24;
-    if (EXACT || c < XR * 24) *reinterpret_cast<uint4*>(xs + r * XS + q * 8) = xv[j];
+    if (EXACT || c < XR * 24) *reinterpret_cast<uint4*>(xs + (a.xpk ? c * 8 : r * XS + q * 8)) = xv[j];
   }
   __syncthreads();
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int kk = 0; kk < 6; ++kk)
-      xf[t][kk] = *reinterpret_cast<const uint4*>(xs + (t * 16 + (lane & 15)) * XS + 8 * (lane >> 4) + kk * 32);
+      xf[t][kk] = *reinterpret_cast<const uint4*>(
+          xs + (a.xpk ? ((t * 6 + kk) * 64 + lane) * 8 : (t * 16 + (lane & 15)) * XS + 8 * (lane >> 4) + kk * 32));
   __builtin_amdgcn_sched_barrier(0);
   f32x4_t acc[NT];
 #pragma unroll
@@ -2025,6 +2050,8 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
   const bool fm = fused_mlp<TW>(B);
   const int nsm = mf ? attn_ns_max(B) : NSPLIT;
   const bool pk = mf && !(g_opt_exp & 2);  // fragment-packed weights for the MFMA GEMMs (exp bit 2: row-major)
+  // fragment-packed operand rows on the v2 steps with the rows kernel (9 <= B <= 32; exp bit 4: row-major)
+  a.xpk = (mf && B > MFMA_LN_MAX && B <= 32 && !(g_opt_exp & 4)) ? 1 : 0;
   a.layer = l;
   a.yacc = (fm || mf) ? a.st.yacc : nullptr;
   a.add_y = l > 0;
@@ -2054,13 +2081,14 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       }
       break;
     case 1:
-      launch_attn(a.st, kvdtype, B, l, s, nsm, mf && nsm == 1, a.defer_sel == 1 && l == 0, qkv_ksplit<TW>(B, kvdtype));
+      launch_attn(a.st, kvdtype, B, l, s, nsm, (mf && nsm == 1) ? 1 + a.xpk : 0, a.defer_sel == 1 && l == 0,
+                  qkv_ksplit<TW>(B, kvdtype));
       break;
     case 2:
       a.W = w.w_aproj[l]; a.Wf = pk ? w.f_aproj[l] : nullptr; a.N = D;
       if (mf) {
         if (B > MFMA_LN_MAX) a.add_y = 0;  // ar_rows_kernel<4> of this layer's c_attn folded them
-        if (nsm > 1) launch_merge_bf16(a.st, B, nsm, s);  // nsm == 1: the attention wrote xn itself
+        if (nsm > 1) launch_merge_bf16(a.st, B, nsm, s, a.xpk);  // nsm == 1: the attention wrote xn itself
         a.ln_w = w.ln2[l];  // OUT 7: the bf16 copy is x * ln_2.weight (c_fc's operand)
         // + bf16 x and row statistics for c_fc; 16-row batch tiles (B = 32: 96 blocks of 49 KB operands
         // instead of 48 of 74 KB: -3.4 us/step at t = 512-1,151)

@@ -155,17 +155,18 @@ def test_qkv_ksplit_matches_one_launch_cattn(B):
         e.close()
 
 
-@pytest.mark.parametrize("B", [8, 32])
-def test_fragment_packed_weights_match_row_major(B):
-    """The batched MFMA GEMMs read an MFMA-fragment-packed copy of the bf16 weights; option exp bit 2
-    reads the row-major matrices: the same products in the same order, bit for bit."""
+@pytest.mark.parametrize("B,bit", [(8, 2), (32, 2), (12, 4), (32, 4)])
+def test_fragment_packed_weights_match_row_major(B, bit):
+    """The batched MFMA GEMMs read an MFMA-fragment-packed copy of the bf16 weights (option exp bit 2
+    reads the row-major matrices) and, at 9 <= B <= 32, operand rows their producers store
+    fragment-packed (exp bit 4: row-major rows): the same products in the same order, bit for bit."""
     from llmvox_amd.engine import build_engine
     e = build_engine(0, "bf16", "bf16", max_streams=64, max_positions=512, max_codec_frames=256)
     try:
         texts = _texts(B, 64, seed=5)
         order = list(np.random.default_rng(B + 1).permutation(B))
         res = []
-        for exp in (0, 2):
+        for exp in (0, bit):
             e.set_option("exp", exp)
             res.append(_run(e, order, texts, set(range(0, B, 4)), 24, 40))
         e.set_option("exp", 0)
