@@ -163,6 +163,7 @@ def test_fragment_packed_weights_match_row_major(B, bit):
     from llmvox_amd.engine import build_engine
     e = build_engine(0, "bf16", "bf16", max_streams=64, max_positions=512, max_codec_frames=256)
     try:
+        e.set_option("fuse_mlp", 0)  # the ragged prefix may run B <= 2 rows: no fp32 atomics there
         texts = _texts(B, 64, seed=5)
         order = list(np.random.default_rng(B + 1).permutation(B))
         res = []
@@ -170,6 +171,7 @@ def test_fragment_packed_weights_match_row_major(B, bit):
             e.set_option("exp", exp)
             res.append(_run(e, order, texts, set(range(0, B, 4)), 24, 40))
         e.set_option("exp", 0)
+        e.set_option("fuse_mlp", 1)
         np.testing.assert_array_equal(res[0][0], res[1][0])
         np.testing.assert_array_equal(res[0][1], res[1][1])
     finally:
