@@ -1606,7 +1606,7 @@ static void launch_mfma2(const GemvArgs& a, hipStream_t s, bool btile = false) {
   else hipLaunchKernelGGL((ar_mfma2_kernel<K, 4, OUT, K, XM>), grid, block, 0, s, a);
 }
 
-// c_attn of the batched steps with one attention block per (row, head) (17 <= B <= 32, bf16 KV):
+// c_attn of the batched v2 steps with the rows kernel before it (9 <= B <= 32, bf16 KV):
 // the K = 768 reduction split over the grid instead of over a block's waves. A block is 4 waves x 16
 // output rows (64 rows) of one 192-wide K slice: 24.6 KB of weights + 12.3 KB of operand rows per
 // block instead of 24.6 + 49 KB. Each wave stores its 16 x 32 partial (one 16-B store per
