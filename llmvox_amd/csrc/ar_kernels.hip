@@ -1744,7 +1744,10 @@ __global__ __launch_bounds__(256) void ar_mfma_ln_kernel(GemvArgs a) {
   __builtin_amdgcn_sched_barrier(0);  // (the scheduler otherwise moves them behind the weights)
   uint4 wf[6];
 #pragma unroll
-  for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(W + (size_t)wrow * K + k0 + kk * 32);
+  for (int kk = 0; kk < 6; ++kk)  // fragment-packed weights (a.Wf): 6 contiguous KB per wave
+    wf[kk] = *reinterpret_cast<const uint4*>(
+        a.Wf ? reinterpret_cast<const bf16_t*>(a.Wf) + (((size_t)(n0 >> 4) * (K / 32) + wave * 6 + kk) * 64 + lane) * 8
+             : W + (size_t)wrow * K + k0 + kk * 32);
   // 2. rows -> LayerNorm -> bf16 tile (rows >= B are zero: padded columns, never stored)
 #pragma unroll
   for (int i = 0; i < RW; ++i) {
