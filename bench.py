@@ -79,31 +79,62 @@ def plan_for(ids, start, n, pad=384):
 
 
 # ---------------------------------------------------------------------------------------
+def attn_splits(B, wbytes):
+    """KV splits per (row, head) of the decode attention at this B (ar_kernels.hip attn_ns_max):
+    16 on the B <= 2 GEMV path (and fp32 weights), else halved until splits x 8 heads x B <= 256
+    blocks. One split (B >= 32): the attention writes the normalised bf16 operand rows itself and
+    no split partials exist."""
+    if wbytes != 2 or B < 3:
+        return 16
+    ns = 16
+    while ns > 1 and ns * 8 * B > 256:
+        ns //= 2
+    return ns
+
+
 def kernel_bytes(which, B, t, wbytes, kvbytes):
-    """Algorithmic HBM bytes of one launch (weights streamed once + KV + activations). At
+    """Algorithmic HBM bytes of one launch of op `which` (weights streamed once + KV + the
+    activations it must read and write), as the batched path at this B moves them. At
     9 <= B <= 32 with bf16 weights and KV, c_attn hands its output to the attention as four K-slice
-    partials (ar_qkv_ksplit_kernel: 4 x 2,304 fp32 per row written, read back by the attention, which
-    also appends the new key)."""
+    partials (ar_qkv_ksplit_kernel: 4 x 2,304 fp32 per row written, read back by the attention,
+    which also appends the new key). Split-KV partials (8 heads x ns x (96 + 2) fp32 per row) are
+    charged only when the attention runs more than one split (attn_splits)."""
     D, F, V = 768, 3072, 4096
     act = 4 * B
-    ksplit = wbytes == 2 and kvbytes == 2 and 9 <= B <= 32
+    mfma = wbytes == 2 and 3 <= B <= 64
+    ksplit = mfma and kvbytes == 2 and 9 <= B <= 32
+    ns = attn_splits(B, wbytes)
+    parts = act * 8 * ns * 98 if ns > 1 else 0           # split-KV partials written / read once
+    rows_bf16 = 2 * D * B                                  # one bf16 operand row set
     if which == 0:
-        if ksplit:
-            return 3 * D * D * wbytes + 2 * D * B + act * 4 * 3 * D
-        return 3 * D * D * wbytes + act * (D + D) + 2 * D * kvbytes * B
+        if ksplit:  # operand rows in, 4 K-slice partials out (the KV append happens in the attention)
+            return 3 * D * D * wbytes + rows_bf16 + act * 4 * 3 * D
+        return 3 * D * D * wbytes + (rows_bf16 if mfma else act * D) + act * D + 2 * D * kvbytes * B
     if which == 1:
-        if ksplit:
-            return 2 * t * D * kvbytes * B + act * 4 * 3 * D + 2 * D * kvbytes * B + 2 * D * B
-        return 2 * t * D * kvbytes * B + act * (D + 8 * 16 * 98)
-    if which == 2:
-        return D * D * wbytes + act * (8 * 16 * 98 + 2 * D)
+        kv = 2 * t * D * kvbytes * B
+        if ksplit:  # partials in, new key appended, head outputs (bf16 rows or split partials) out
+            return kv + act * 4 * 3 * D + 2 * D * kvbytes * B + (rows_bf16 if ns == 1 else parts)
+        return kv + act * D + (rows_bf16 if (mfma and ns == 1) else parts)
+    if which == 2:  # (+ the merge kernel when ns > 1) x read + written, bf16 copy for c_fc
+        merge = (parts + 2 * rows_bf16) if (mfma and ns > 1) else parts
+        return D * D * wbytes + (rows_bf16 if (mfma and ns == 1) else merge) + 2 * act * D + \
+            (rows_bf16 if mfma else 0)
     if which == 3:
-        return F * D * wbytes + act * (D + F)
-    if which == 4:
-        return D * F * wbytes + act * (F + 2 * D)
+        return F * D * wbytes + ((rows_bf16 + 2 * F * B) if mfma else act * (D + F))
+    if which == 4:  # mfma: four K-slice partials (fp32) out
+        return D * F * wbytes + ((2 * F * B + 4 * act * D) if mfma else act * (F + 2 * D))
     if which == 5:
-        return V * D * wbytes + act * (D + V)
+        return V * D * wbytes + ((rows_bf16 if mfma else act * D) + act * V)
     raise ValueError(which)
+
+
+def step_bytes(B, t, wbytes, kvbytes):
+    """Algorithmic HBM bytes of one whole decode step of B rows at KV position t:
+    every GEMM weight once (62.9 MB bf16) + the K/V history of 4 layers read + the new key / value
+    written, per row."""
+    D, F, V, L = 768, 3072, 4096, 4
+    weights = (L * (3 * D * D + D * D + 2 * F * D) + V * D) * wbytes
+    return weights + L * B * (2 * t * D * kvbytes + 2 * D * kvbytes)
 
 
 KNAMES = {0: "ar_gemv c_attn", 1: "ar_attn (split-KV decode)", 2: "ar_gemv c_proj(+merge)",
@@ -542,6 +573,11 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
     pcm_bufs = [pcm, torch.empty_like(pcm)]
     ev_ar = [torch.cuda.Event(), torch.cuda.Event()]
     ev_codec = [torch.cuda.Event(), torch.cuda.Event()]
+    # per-chunk AR time (the decode steps alone), timing events on the decode stream around
+    # ar_steps: read after the timed region for the whole-step roofline (no host sync inside it)
+    ar_t = []
+
+    timing = None
 
     def run_chunk(c):
         i = c & 1
@@ -553,8 +589,15 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
                 eng.reset_slot(s_)
         text_plan.copy_(mine[:, col:col + chunk])
         rowstep.zero_()
+        if timing is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record(main)
         eng.ar_steps(chunk, slots, text_plan, rowstep, tok_bufs[i])
         ev_ar[i].record(main)
+        if timing is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record(main)
+            timing.append((e0, e1))
         with torch.cuda.stream(codec_stream):
             codec_stream.wait_event(ev_ar[i])
             eng.decode_codes(tok_bufs[i], 0, out=pcm_bufs[i])
@@ -587,6 +630,7 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
+    timing = ar_t
     t0 = time.perf_counter()
     for c in range(K):
         run_chunk(c)
@@ -595,6 +639,7 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
         dist.barrier()
     dt = time.perf_counter() - t0
     eng.check_errors()
+    run_chunks.ar_ms = [a.elapsed_time(b) for a, b in ar_t]
     return dt, tok_bufs[(K - 1) & 1], codec_stream, tok_bufs, pcm_bufs
 
 
@@ -757,6 +802,9 @@ def main():
               "unit": "GB/s", "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(key, dom["name"]),
               "bytes_per_launch": dom["bytes"], "avg_us": round(dom["avg_us"], 3), "kv_positions": ppos,
               "pmc_key": key}
+        # PMC traffic / algorithmic bytes per probed kernel (a ratio well above 1 = operand re-fetch)
+        rl["traffic_ratio"] = {v["name"]: (round(pmc_traffic(key, v["name"]) / v["bytes"], 3)
+                                           if pmc_traffic(key, v["name"]) else None) for v in kern.values()}
 
     # ---- codec: one batched decode of a chunk (S streams x chunk frames), HIP events on the
     # stream it runs on; algorithmic FLOPs per SURVEY 8(d): 125,566,976 + 3,072 L per frame
@@ -777,6 +825,25 @@ def main():
              "achieved": round(codec_flops / (codec_ms * 1e-3) / 1e12, 2), "peak": codec_peak, "unit": "TFLOP/s",
              "frac": round(codec_flops / (codec_ms * 1e-3) / 1e12 / codec_peak, 4),
              "gemm_mfma_busy": pmc_codec(ckey), "pmc_key": ckey}
+
+    # whole decode step against HBM: algorithmic bytes of every step of the timed chunks (their KV
+    # positions) over the measured AR time of those chunks (events around ar_steps in the timed loop)
+    wb = 2 if args.dtype == "bf16" else 4
+    kb = {"bf16": 2, "fp8": 1, "fp32": 4}[kvd]
+    ar_ms = getattr(run_chunks, "ar_ms", [])
+    step_rl = None
+    if ar_ms:
+        tot_b = 0
+        for c in range(K):
+            p0 = (c % reset_every) * chunk if reset_every else c * chunk
+            tot_b += sum(step_bytes(S, p + 1, wb, kb) for p in range(p0, p0 + chunk))
+        us = sum(ar_ms) * 1e3 / (K * chunk)
+        gbs = tot_b / (K * chunk) / (us * 1e-6) / 1e9
+        step_rl = {"bound": "hbm", "bytes_per_step": round(tot_b / (K * chunk)), "us_per_step": round(us, 2),
+                   "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                   "ar_ms_per_chunk": round(sum(ar_ms) / K, 3),
+                   "note": "all GEMM weights once + 4 layers of K/V history read and the new key/value written, "
+                           "per decode step at the timed chunks' positions, over the decode steps' own time"}
 
     parity = None
     if rank == 0 and world == 1 and not args.no_parity_line and args.dtype == "bf16" and args.config in (1, 2):
@@ -815,6 +882,7 @@ def main():
             "realtime_factor_per_stream": round(value / (world * S) / 75.0, 1),
             "p50_first_chunk_latency_ms": round(p50, 3),
             "roofline": rl,
+            "step_roofline": step_rl,
             "codec_roofline": codec,
             "kv_dtype": kvd,
             "codec_weights": args.codec_dtype or args.dtype,

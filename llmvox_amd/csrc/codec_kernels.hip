@@ -369,8 +369,12 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmArgs g, int batch)
   }
 }
 
-static size_t g_ws_floats = 0;  // capacity of the split-K workspace (set by the front end)
-static uint32_t* g_tick = nullptr;  // per-tile counters of the in-launch combine (set by the front end)
+// capacity of the split-K workspace and the per-tile counters of the in-launch combine, set from
+// the context's scratch at the start of each codec_launch_decode and read by the launch helpers it
+// calls on the same host thread: thread_local, so two contexts decoding from two threads (two
+// devices) never see each other's workspace or tickets
+static thread_local size_t g_ws_floats = 0;
+static thread_local uint32_t* g_tick = nullptr;
 
 template <bool BF, typename TA, typename TB, int AMODE, int EPI, typename TC>
 static void gemm_launch(GemmArgs g, int batch, hipStream_t s) {

@@ -455,6 +455,9 @@ int lvx_finalize(lvx_ctx* c) {
   // ---- AR state ----
   ArState& st = c->st;
   const int S = c->cfg.max_streams, P = c->cfg.max_positions;
+  // the bf16 operand rows (xn, xb, hb) are stored and read in whole 16-row MFMA tiles when they are
+  // fragment-packed (xfrag, 9 <= B <= 32): a partly filled tile spans 16 rows, so round up
+  const int S16 = (S + 15) / 16 * 16;
   st.max_pos = P;
   st.max_streams = S;
   st.kv_chunks = (P + KV_CHUNK - 1) / KV_CHUNK;
@@ -465,8 +468,8 @@ int lvx_finalize(lvx_ctx* c) {
       (r = c->dalloc(&st.logits, (size_t)S * VOCAB)) || (r = c->dalloc(&st.rowinfo, S)) ||
       (r = c->dalloc(&st.rowinfo_n, S)) || (r = c->dalloc(&st.rowx, S)) || (r = c->dalloc(&st.rowx_n, S)) ||
       (r = c->dalloc(&st.selp, 4)) || (r = c->dalloc(&st.selrow, S)) ||
-      (r = c->dalloc(&st.xn, (size_t)S * D)) || (r = c->dalloc(&st.hb, (size_t)S * DFF)) ||
-      (r = c->dalloc(&st.xb, (size_t)S * D)) || (r = c->dalloc(&st.xstat, (size_t)(D / 16) * S * 2)) ||
+      (r = c->dalloc(&st.xn, (size_t)S16 * D)) || (r = c->dalloc(&st.hb, (size_t)S16 * DFF)) ||
+      (r = c->dalloc(&st.xb, (size_t)S16 * D)) || (r = c->dalloc(&st.xstat, (size_t)(D / 16) * S * 2)) ||
       (r = c->dalloc(&st.lmbest, (size_t)LM_MAX_BLOCKS * 4 * 2)) ||
       (r = c->dalloc(&st.yacc, (size_t)YCOPIES * S * D)) || (r = c->dalloc(&st.qkvp, (size_t)4 * S * 3 * D)))
     return r;

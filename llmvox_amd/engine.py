@@ -174,8 +174,12 @@ def build_engine(device_index=0, weight_dtype="fp32", kv_dtype="fp32", seed=1234
     """Engine loaded with ``weights`` = (gpt, codec, text_table) or the seeded synthetic set.
     codec_dtype "fp8": codec GEMM weights stored as e4m3fn with per-row scales (configs[4])."""
     from .weights import synthetic_all
-    e = Engine(device_index, weight_dtype, kv_dtype, max_streams, max_positions, max_codec_frames, codec_dtype)
     gw, cw, tt = weights if weights is not None else synthetic_all(seed)
+    # a checkpoint trained with a smaller block_size has zero-padded wpe rows past it: positions
+    # there must raise (the reference asserts t <= block_size, src/model.py:205), so the KV
+    # capacity never exceeds it (ADVICE r02)
+    max_positions = min(int(max_positions), int(getattr(gw, "block_size", max_positions)))
+    e = Engine(device_index, weight_dtype, kv_dtype, max_streams, max_positions, max_codec_frames, codec_dtype)
     e.load_weights(gw, cw, tt)
     return e
 

@@ -12,6 +12,13 @@ open streams of all requests are decoded together (continuous batching, one HIP-
 step, codec per dump). The response body is the same byte stream the reference produces: raw
 f32le mono 24 kHz chunks, in order, no framing.
 
+Multi-device: the reference pins its two replicas to two GPUs
+(streaming_server.py:162-169, configs/inference_config.py:25-26). Here ``TTSService`` takes one
+engine per GPU and runs one scheduler thread per engine (``_Worker``); request k's two replica
+streams are placed on GPU k mod G (round robin over the healthy devices), so independent requests
+decode concurrently on every card. A request's streams share a device: the session logic (caps,
+tails, the end signal) then never spans two scheduler threads.
+
 Differences, on purpose:
   * the reference hands the request text to an LLM and speaks its streamed reply; through
     ``"text" in request`` being False for a pydantic model (:209) it actually routes /tts requests
@@ -26,8 +33,10 @@ Differences, on purpose:
     when every fed stream of a request has stopped or gone idle, their undumped tails are decoded
     and the response ends. A stream that never received text (a one-sentence request leaves
     replica 1 empty) does not hold a request open.
-  * a KV-capacity error of the decode step ends the request(s) whose streams are at the capacity
-    edge (all open requests if none is), not the service.
+  * a KV-capacity error of the decode step ends only the request(s) whose streams reached the
+    capacity edge (FusedScheduler.run_chunk still delivers the chunk to every other stream); an
+    LLM producer failure ends only its own request. A scheduler-thread failure takes its device
+    out of service (its requests end with the error; new requests go to the other devices).
 """
 
 import threading
@@ -39,113 +48,30 @@ from .streaming import FusedScheduler, audio_chunks, route_text
 
 
 class _Session:
-    def __init__(self, streams, queues):
+    def __init__(self, streams, queues, worker):
         self.streams = streams
         self.queues = queues
+        self.worker = worker
         self.done = False
         self.error: Optional[BaseException] = None
 
 
-class TTSService:
-    """Owns the scheduler thread. ``submit(text)`` returns a session whose two queues carry the
-    replica outputs (bytes and 0 / 1 / 'end' signals); ``chunks(session)`` yields the PCM bytes
-    in speaking order (audio_generator_async semantics) and closes the session at the end."""
+class _Worker:
+    """One device of the service: its engine, a FusedScheduler over it and the thread that runs it."""
 
-    def __init__(self, engine, max_chunk: int = 64, max_tokens: Optional[int] = None, eos: str = C.EOS_TOKEN,
-                 eoa_id: int = C.EOA_TOKEN_ID, dumps=(C.INITIAL_DUMP_SIZE_1, C.INITIAL_DUMP_SIZE_2),
-                 stream_model=None, system_prompt: str = C.SYSTEM_PROMPT):
-        """stream_model: an llm_streaming.StreamModel (or anything with its predict()): the request
-        text is then the LLM prompt and its streamed reply is spoken, as the reference's /tts does
-        (streaming_server.py:184-248, 494-540); None speaks the request text itself."""
+    def __init__(self, svc, engine, index: int, max_chunk: int, max_tokens: Optional[int]):
+        self.svc = svc
         self.engine = engine
-        self.stream_model = stream_model
-        self.system_prompt = system_prompt
+        self.index = index
         self.sched = FusedScheduler(engine, max_chunk=max_chunk, to_bytes=True)
         self.max_tokens = max_tokens or max(1, engine.max_positions - max_chunk - 1)
-        self.eos = eos
-        self.eoa_id = eoa_id
-        self.dumps = dumps
         self.sessions: List[_Session] = []
         self.lock = threading.Condition()
         self.running = True
         self.error: Optional[BaseException] = None
-        self.thread = threading.Thread(target=self._loop, name="lvx-tts-scheduler", daemon=True)
+        self.thread = threading.Thread(target=self._loop, name=f"lvx-tts-scheduler-{index}", daemon=True)
         self.thread.start()
 
-    # -- request side --
-    def submit(self, text: str) -> _Session:
-        if self.error is not None:
-            raise RuntimeError("TTS scheduler thread failed") from self.error
-        queues = [Queue(), Queue()]
-        with self.lock:
-            if len(self.sched.free_slots) < 2:
-                raise RuntimeError("no free KV slots: too many concurrent requests")
-            streams = [self.sched.open_stream(index=i, dump_size=self.dumps[i], sink=queues[i], eoa_id=self.eoa_id)
-                       for i in range(2)]
-
-            class _Feed:  # route_text puts words on "queues"; here they go straight to the streams
-                def __init__(self, st):
-                    self.st = st
-
-                def put(self, w):
-                    self.st.feed(w)
-
-            if self.stream_model is None:
-                route_text(text.split() + [self.eos], [_Feed(streams[0]), _Feed(streams[1])], eos=self.eos)
-            else:  # the LLM's reply, routed as it streams (text_streamer_producer on its own thread)
-                threading.Thread(target=self._produce, args=(text, streams), name="lvx-llm-producer",
-                                 daemon=True).start()
-            s = _Session(streams, queues)
-            self.sessions.append(s)
-            self.lock.notify_all()
-        return s
-
-    def _produce(self, prompt: str, streams):
-        from .llm_streaming import text_streamer_producer
-        svc = self
-
-        class _LockedFeed:
-            def __init__(self, st):
-                self.st = st
-
-            def put(self, w):
-                with svc.lock:
-                    self.st.feed(w)
-                    svc.lock.notify_all()
-
-        try:
-            text_streamer_producer(prompt, self.stream_model, _LockedFeed(streams[0]), _LockedFeed(streams[1]),
-                                   {"system_prompt": self.system_prompt, "eos_token": self.eos})
-        except BaseException as e:  # an LLM failure ends the service's requests like a scheduler failure
-            self.error = e
-
-    def chunks(self, session: _Session, timeout: float = 0.05):
-        try:
-            for item in audio_chunks(session.queues[0], session.queues[1], timeout=timeout,
-                                     stop=lambda: self.error is not None):
-                yield item
-        finally:
-            self.close(session)
-        if self.error is not None:
-            raise RuntimeError("TTS scheduler thread failed") from self.error
-        if session.error is not None:
-            raise RuntimeError("request ended by a KV-capacity error") from session.error
-
-    def close(self, session: _Session):
-        with self.lock:
-            if session in self.sessions:
-                self.sessions.remove(session)
-            for st in session.streams:
-                if st in self.sched.streams:
-                    self.sched.close_stream(st)
-
-    def shutdown(self):
-        with self.lock:
-            self.running = False
-            self.lock.notify_all()
-        self.thread.join(timeout=5)
-
-    # -- scheduler thread --
     def _stopped(self, st) -> bool:
         """A fed stream stops at max_tokens, or when its segment would outgrow the KV capacity
         within the next chunk; stopping closes its text side (the scheduler then skips it)."""
@@ -154,9 +80,12 @@ class TTSService:
             st.m.closed = True
         return st.m.closed
 
-    def _end(self, s: _Session, error: Optional[BaseException] = None):
-        """Decode the undumped tails of the session's fed streams, then 'end' on both queues."""
+    def end(self, s: _Session, error: Optional[BaseException] = None):
+        """Decode the undumped tails of the session's fed streams, then 'end' on both queues.
+        Caller holds the lock."""
         import torch
+        if s.done:
+            return
         s.done = True
         s.error = error
         if error is None:
@@ -181,7 +110,7 @@ class TTSService:
             stopped = [self._stopped(st) for st in fed]
             idle = [st.m.closed or st.m.next_text_id() is None for st in fed]
             if fed and any(stopped) and all(idle):
-                self._end(s)
+                self.end(s)
 
     def _loop(self):
         from ._lib import LvxCapacityError
@@ -191,22 +120,157 @@ class TTSService:
                     if not self.running:
                         return
                     n = self.sched.run_chunk() if self.sched.streams else 0
-                    if n:
-                        self._cap()
-                    else:
-                        self._cap()
+                    self._cap()
+                    if not n:
                         self.lock.wait(timeout=0.01)
-            except LvxCapacityError as e:  # only the sessions at the capacity edge fail
+            except LvxCapacityError as e:
+                # run_chunk delivered the chunk to every stream below the capacity edge and names
+                # the streams at the edge; only their sessions fail
                 with self.lock:
                     live = [s for s in self.sessions if not s.done]
-                    edge = [s for s in live
-                            if any(st.m.position + self.sched.max_chunk >= self.engine.max_positions
-                                   for st in s.streams)]
+                    edge_streams = getattr(e, "streams", None) or []
+                    edge = [s for s in live if any(st in edge_streams for st in s.streams)]
                     for s in edge or live:
-                        self._end(s, error=e)
-            except BaseException as e:  # surfaced to every waiting request
-                self.error = e
+                        self.end(s, error=e)
+            except BaseException as e:  # this device is out of service: its requests end with the error
+                with self.lock:
+                    self.error = e
+                    for s in self.sessions:
+                        if not s.done:
+                            s.done = True
+                            s.error = e
+                            for q in s.queues:
+                                q.put("end")
                 return
+
+
+class TTSService:
+    """Owns one scheduler thread per engine (device). ``submit(text)`` returns a session whose two
+    queues carry the replica outputs (bytes and 0 / 1 / 'end' signals); ``chunks(session)`` yields
+    the PCM bytes in speaking order (audio_generator_async semantics) and closes the session at
+    the end."""
+
+    def __init__(self, engine, max_chunk: int = 64, max_tokens: Optional[int] = None, eos: str = C.EOS_TOKEN,
+                 eoa_id: int = C.EOA_TOKEN_ID, dumps=(C.INITIAL_DUMP_SIZE_1, C.INITIAL_DUMP_SIZE_2),
+                 stream_model=None, system_prompt: str = C.SYSTEM_PROMPT):
+        """engine: one Engine or a list of them (one per GPU). stream_model: an
+        llm_streaming.StreamModel (or anything with its predict()): the request text is then the
+        LLM prompt and its streamed reply is spoken, as the reference's /tts does
+        (streaming_server.py:184-248, 494-540); None speaks the request text itself."""
+        engines = list(engine) if isinstance(engine, (list, tuple)) else [engine]
+        if not engines:
+            raise ValueError("TTSService needs at least one engine")
+        self.engine = engines[0]
+        self.stream_model = stream_model
+        self.system_prompt = system_prompt
+        self.eos = eos
+        self.eoa_id = eoa_id
+        self.dumps = dumps
+        self.workers = [_Worker(self, e, i, max_chunk, max_tokens) for i, e in enumerate(engines)]
+        self.sched = self.workers[0].sched
+        self.max_tokens = self.workers[0].max_tokens
+        self._next = 0
+        self._rr = threading.Lock()
+
+    @property
+    def sessions(self) -> List[_Session]:
+        return [s for w in self.workers for s in w.sessions]
+
+    @property
+    def error(self) -> Optional[BaseException]:
+        """The first scheduler-thread failure when no device is left in service, else None."""
+        errs = [w.error for w in self.workers]
+        return errs[0] if all(e is not None for e in errs) else None
+
+    # -- request side --
+    def _place(self) -> _Worker:
+        """Request k goes to device k mod G (skipping devices out of service)."""
+        with self._rr:
+            for _ in range(len(self.workers)):
+                w = self.workers[self._next % len(self.workers)]
+                self._next += 1
+                if w.error is None:
+                    return w
+        raise RuntimeError("TTS scheduler thread failed") from self.workers[0].error
+
+    def submit(self, text: str) -> _Session:
+        w = self._place()
+        queues = [Queue(), Queue()]
+        with w.lock:
+            if len(w.sched.free_slots) < 2:
+                raise RuntimeError("no free KV slots: too many concurrent requests")
+            streams = [w.sched.open_stream(index=i, dump_size=self.dumps[i], sink=queues[i], eoa_id=self.eoa_id)
+                       for i in range(2)]
+            s = _Session(streams, queues, w)
+
+            class _Feed:  # route_text puts words on "queues"; here they go straight to the streams
+                def __init__(self, st):
+                    self.st = st
+
+                def put(self, word):
+                    self.st.feed(word)
+
+            if self.stream_model is None:
+                route_text(text.split() + [self.eos], [_Feed(streams[0]), _Feed(streams[1])], eos=self.eos)
+            else:  # the LLM's reply, routed as it streams (text_streamer_producer on its own thread)
+                threading.Thread(target=self._produce, args=(text, s), name="lvx-llm-producer",
+                                 daemon=True).start()
+            w.sessions.append(s)
+            w.lock.notify_all()
+        return s
+
+    def _produce(self, prompt: str, s: _Session):
+        from .llm_streaming import text_streamer_producer
+        w = s.worker
+
+        class _LockedFeed:
+            def __init__(self, st):
+                self.st = st
+
+            def put(self, word):
+                with w.lock:
+                    if not s.done:
+                        self.st.feed(word)
+                    w.lock.notify_all()
+
+        try:
+            text_streamer_producer(prompt, self.stream_model, _LockedFeed(s.streams[0]), _LockedFeed(s.streams[1]),
+                                   {"system_prompt": self.system_prompt, "eos_token": self.eos})
+        except BaseException as e:  # an LLM failure ends this request only
+            with w.lock:
+                w.end(s, error=e)
+                w.lock.notify_all()
+
+    def chunks(self, session: _Session, timeout: float = 0.05):
+        w = session.worker
+        try:
+            for item in audio_chunks(session.queues[0], session.queues[1], timeout=timeout,
+                                     stop=lambda: w.error is not None):
+                yield item
+        finally:
+            self.close(session)
+        if session.error is not None:
+            raise RuntimeError(f"request failed: {session.error!r}") from session.error
+        if w.error is not None:
+            raise RuntimeError("TTS scheduler thread failed") from w.error
+
+    def close(self, session: _Session):
+        w = session.worker
+        with w.lock:
+            if session in w.sessions:
+                w.sessions.remove(session)
+            for st in session.streams:
+                if st in w.sched.streams:
+                    w.sched.close_stream(st)
+
+    def shutdown(self):
+        for w in self.workers:
+            with w.lock:
+                w.running = False
+                w.lock.notify_all()
+        for w in self.workers:
+            w.thread.join(timeout=5)
+
 
 def create_app(service):
     """FastAPI app with the reference's /tts contract (TTSRequest {text} -> octet-stream)."""
@@ -241,6 +305,8 @@ def main(argv=None):
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=8000)
     ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--devices", default=None,
+                    help="comma-separated GPU ordinals, one scheduler per GPU (default: --device only)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--kv-dtype", default=None, choices=["bf16", "fp32", "fp8"])
     ap.add_argument("--max-streams", type=int, default=64)
@@ -266,14 +332,16 @@ def main(argv=None):
         sd = torch.load(a.text_embed, map_location="cpu", weights_only=True)
         tt = W.load_text_embed_from_t5({k: v.float().numpy() for k, v in sd.items()})
     weights = (gw, cw, tt)
-    eng = build_engine(a.device, a.dtype, a.kv_dtype or a.dtype, seed=a.seed, max_streams=a.max_streams,
-                       max_positions=a.max_positions, max_codec_frames=C.MAX_DUMP_SIZE * 2, weights=weights)
+    devices = [int(d) for d in a.devices.split(",")] if a.devices else [a.device]
+    engines = [build_engine(d, a.dtype, a.kv_dtype or a.dtype, seed=a.seed, max_streams=a.max_streams,
+                            max_positions=a.max_positions, max_codec_frames=C.MAX_DUMP_SIZE * 2, weights=weights)
+               for d in devices]
     sm = None
     if a.llm_checkpoint:
         from .llm_streaming import StreamModel
         sm = StreamModel({"llm_checkpoint": a.llm_checkpoint, "llm_device": f"cuda:{a.device}",
                           "llm_max_tokens": a.llm_max_tokens}).load()
-    svc = TTSService(eng, stream_model=sm)
+    svc = TTSService(engines, stream_model=sm)
     import uvicorn
     uvicorn.run(create_app(svc), host=a.host, port=a.port)
 

@@ -457,9 +457,26 @@ class FusedScheduler:
         self.engine.ar_steps(n, self.slots_d[:B], self.plan_d[:B], self.rowstep_d[:B], self.tok_d[:B])
         self.flush()  # the previous chunk's audio, decoded while this chunk's AR steps run
         toks = self.tok_d[:B, :n].cpu().numpy()
+        # a KV-capacity error concerns only the rows that reached max_positions in this chunk (their
+        # last positions were clamped); every other row's tokens are valid and are consumed, decoded
+        # and delivered below before the error is raised, naming the streams at the edge
+        cap_err, edge = None, set()
+        try:
+            self.engine.check_errors()
+        except Exception as e:
+            from ._lib import LvxCapacityError
+            if not isinstance(e, LvxCapacityError):
+                raise
+            edge = {st for st in ready if st.m.position + n >= self.engine.max_positions}
+            if not edge:  # not a position overflow of a known row (e.g. a plan overrun): nothing is trusted
+                raise
+            cap_err = e
+            cap_err.streams = sorted(edge, key=lambda st: st.slot)
         dumps = []  # (stream, tokens)
         order: Dict[FusedStream, List[tuple]] = {st: [] for st in ready}
         for r, st in enumerate(ready):
+            if st in edge:
+                continue
             for j in range(n):
                 tok = int(toks[r, j])
                 st.tokens.append(tok)
@@ -475,11 +492,13 @@ class FusedScheduler:
                     # run-ahead past end-of-audio: drop the rest, restart the slot at position 0
                     self.engine.set_slot(st.slot, 0, 0)
                     break
-        self.engine.check_errors()
         if self.overlap:
             self._launch_decode(dumps, order, ready)
         else:
             self._deliver(self._decode(dumps), order, ready)
+        if cap_err is not None:
+            self.flush()
+            raise cap_err
         return n
 
     def _deliver(self, pcm, order, ready):

@@ -39,7 +39,7 @@ def _run(e, order, texts, prefix_rows, n_prefix, n_main, between=None):
     dev = e.device
     B = len(order)
     n = n_prefix + n_main
-    for s in range(64):
+    for s in range(e.max_streams):
         e.reset_slot(s)
     out_tok = np.zeros((B, n), dtype=np.int32)
     out_tok[:] = -1
@@ -170,6 +170,29 @@ def test_fragment_packed_weights_match_row_major(B, bit):
         for exp in (0, bit):
             e.set_option("exp", exp)
             res.append(_run(e, order, texts, set(range(0, B, 4)), 24, 40))
+        e.set_option("exp", 0)
+        e.set_option("fuse_mlp", 1)
+        np.testing.assert_array_equal(res[0][0], res[1][0])
+        np.testing.assert_array_equal(res[0][1], res[1][1])
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("S", [12, 20])
+def test_fragment_packed_rows_with_odd_engine_size(S):
+    """max_streams not a multiple of 16: the fragment-packed operand rows (xn, xb, hb) are
+    written and read in whole 16-row tiles, so the engine allocates them rounded up to 16 rows. B = S
+    with packed rows must equal row-major rows (exp bit 4) bit for bit, and nothing may fault."""
+    from llmvox_amd.engine import build_engine
+    e = build_engine(0, "bf16", "bf16", max_streams=S, max_positions=256, max_codec_frames=256)
+    try:
+        e.set_option("fuse_mlp", 0)
+        texts = _texts(S, 64, seed=S)
+        order = list(np.random.default_rng(S).permutation(S))
+        res = []
+        for exp in (0, 4):
+            e.set_option("exp", exp)
+            res.append(_run(e, order, texts, set(range(0, S, 3)), 20, 36))
         e.set_option("exp", 0)
         e.set_option("fuse_mlp", 1)
         np.testing.assert_array_equal(res[0][0], res[1][0])

@@ -1,0 +1,243 @@
+"""The service layer on a stand-in engine (CPU, no GPU): multi-device placement of requests
+(one scheduler thread per engine, request k on device k mod G), failure isolation (a KV-capacity
+error ends only the requests at the capacity edge, an LLM producer failure only its own request)
+and the KV capacity bound of a checkpoint's block_size."""
+import threading
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from llmvox_amd import streaming as S
+from llmvox_amd._lib import LvxCapacityError
+
+
+class StateEngine:
+    """Stands in for llmvox_amd.Engine with the fused step's per-slot state: a row's token is a
+    function of (text id, previous token, position) only, so a stream's tokens do not depend on its
+    slot, its batch row or the device; the position advances per step and a row past
+    max_positions sets the capacity flag that check_errors raises (as lvx_check_errors does).
+    decode_codes returns each code repeated 320 times (readable PCM)."""
+
+    def __init__(self, max_streams=8, max_positions=4096, name="dev", eoa=None):
+        self.device = torch.device("cpu")
+        self.max_streams = max_streams
+        self.max_positions = max_positions
+        self.max_codec_frames = 1 << 16
+        self.pos = [0] * max_streams
+        self.prev = [0] * max_streams
+        self.err = False
+        self.name = name
+        self.eoa = eoa
+        self.calls = 0
+
+    def reset_slot(self, slot):
+        self.pos[slot] = 0
+
+    def set_slot(self, slot, pos, prev=0):
+        self.pos[slot], self.prev[slot] = pos, prev
+
+    def _tok(self, text, prev, pos):
+        t = ((prev if pos > 0 else 0) * 31 + text * 7 + pos * 13 + 1) % 4096  # no previous token at 0
+        if self.eoa is not None and pos > 0 and pos % 41 == 0:
+            return self.eoa
+        return t if t != 453 else 454
+
+    def ar_steps(self, n, slots, plan, rowstep, tok, margin=None):
+        self.calls += 1
+        time.sleep(0.001)  # a device call takes time: lets the other scheduler threads interleave
+        for r, s in enumerate(slots.tolist()):
+            if s < 0:
+                continue
+            j0 = int(rowstep[r])
+            for j in range(j0, j0 + n):
+                p = self.pos[s]
+                if p + 1 >= self.max_positions:
+                    self.err = True
+                p = min(p, self.max_positions - 1)
+                t = self._tok(int(plan[r, j]), self.prev[s], p)
+                tok[r, j] = t
+                self.prev[s] = t
+                self.pos[s] = p + 1
+            rowstep[r] = j0 + n
+
+    def check_errors(self):
+        if self.err:
+            self.err = False
+            raise LvxCapacityError(-3, "a stream exceeded its KV capacity (max_positions)")
+
+    def decode_codes(self, codes, bandwidth_id=0, out=None):
+        return codes.float().repeat_interleave(320, dim=1)
+
+
+TEXTS = ["The quick brown fox. Jumps over the dog.", "Hello there, how are you today?",
+         "One sentence. Two sentences. Three.", "a b c d e f g h i j k l m n o p.", "Short."]
+
+
+def _serve(engines, texts, max_tokens=150, max_chunk=16, **kw):
+    from llmvox_amd.server import TTSService
+    svc = TTSService(engines, max_chunk=max_chunk, max_tokens=max_tokens, **kw)
+    out = [None] * len(texts)
+    try:
+        sessions = [svc.submit(t) for t in texts]
+        placed = [s.worker.index for s in sessions]
+
+        def read(i):
+            out[i] = b"".join(svc.chunks(sessions[i], timeout=0.01))
+
+        th = [threading.Thread(target=read, args=(i,)) for i in range(len(texts))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=60)
+        assert not any(t.is_alive() for t in th), "a request never ended"
+    finally:
+        svc.shutdown()
+    return out, placed
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_multidevice_service_matches_single_device_bytes(G):
+    """Every request's byte stream is the same whether the service runs one engine or G (requests
+    placed on device k mod G, decoded concurrently by G scheduler threads)."""
+    ref, placed1 = _serve(StateEngine(max_streams=16), TEXTS)
+    engines = [StateEngine(max_streams=16, name=f"dev{g}") for g in range(G)]
+    got, placed = _serve(engines, TEXTS)
+    assert placed1 == [0] * len(TEXTS)
+    assert placed == [k % G for k in range(len(TEXTS))]
+    assert all(e.calls > 0 for e in engines)
+    for a, b in zip(ref, got):
+        assert len(a) > 0 and a == b
+
+
+def test_multidevice_service_with_end_of_audio_switches():
+    """With an end-of-audio id the segments end and the replicas switch (chunk -> switch -> other
+    replica -> switch back -> end): still the same bytes on 1 and on 2 devices."""
+    ref, _ = _serve(StateEngine(max_streams=16, eoa=453), TEXTS, max_tokens=400)
+    got, _ = _serve([StateEngine(max_streams=16, eoa=453), StateEngine(max_streams=16, eoa=453)], TEXTS,
+                    max_tokens=400)
+    assert ref == got and all(len(r) > 0 for r in ref)
+
+
+def test_capacity_error_keeps_the_other_streams_complete():
+    """FusedScheduler.run_chunk: one stream reaches max_positions inside a chunk; the chunk's dumps of
+    every other stream are still delivered (no gap) and the error names the stream at the edge."""
+    eng = StateEngine(max_streams=4, max_positions=64)
+    sch = S.FusedScheduler(eng, max_chunk=8, to_bytes=False)
+    a = sch.open_stream(index=0, dump_size=4)
+    b = sch.open_stream(index=1, dump_size=4)
+    for w in "some words that keep going for a long while and then some more words.".split():
+        a.feed(w)
+        b.feed(w)
+    eng.set_slot(a.slot, 60, 0)  # a is 4 positions from its capacity, b starts at 0
+    a.m.gen_index = 60
+    with pytest.raises(LvxCapacityError) as ei:
+        for _ in range(4):
+            sch.run_chunk()
+    assert ei.value.streams == [a]
+    # b consumed every token of the failing chunk and got its dumps: 4 tokens per dump, none missing
+    assert len(b.tokens) % 4 == 0 and len(b.tokens) > 0
+    pcm_b = [x for x in b.events if isinstance(x, np.ndarray)]
+    assert sum(len(x) for x in pcm_b) == 320 * len(b.tokens)
+    # and its tokens are the ones a fresh run of the same text gives (nothing skipped on the device)
+    eng2 = StateEngine(max_streams=4)
+    sch2 = S.FusedScheduler(eng2, max_chunk=8, to_bytes=False)
+    c = sch2.open_stream(index=1, dump_size=4)
+    for w in "some words that keep going for a long while and then some more words.".split():
+        c.feed(w)
+    while len(c.tokens) < len(b.tokens):
+        sch2.run_chunk()
+    assert c.tokens[:len(b.tokens)] == b.tokens
+
+
+def test_capacity_edge_ends_only_its_request():
+    """Two requests on one device; one is moved to the capacity edge: it ends with the error, the
+    other completes with the same bytes as when served alone."""
+    from llmvox_amd.server import TTSService
+    alone, _ = _serve(StateEngine(max_streams=8, max_positions=400), TEXTS[1:2], max_tokens=120)
+    eng = StateEngine(max_streams=8, max_positions=400)
+    svc = TTSService(eng, max_chunk=16, max_tokens=120)
+    try:
+        w = svc.workers[0]
+        with w.lock:
+            s0 = svc.submit(TEXTS[0])
+            s1 = svc.submit(TEXTS[1])
+            # s0's replica 0 jumps to 8 positions below the capacity, past the service's own cap check
+            st = s0.streams[0]
+            eng.set_slot(st.slot, 392, 0)
+            st.m.gen_index = 392  # (the next chunk runs before the service's cap check sees it)
+        out = {}
+
+        def read(name, s):
+            try:
+                out[name] = b"".join(svc.chunks(s, timeout=0.01))
+            except RuntimeError as e:
+                out[name] = e
+
+        th = [threading.Thread(target=read, args=(n, s)) for n, s in (("s0", s0), ("s1", s1))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=60)
+    finally:
+        svc.shutdown()
+    assert isinstance(out["s0"], RuntimeError) and isinstance(out["s0"].__cause__, LvxCapacityError)
+    assert out["s1"] == alone[0]
+    assert svc.error is None
+
+
+class _FailingLLM:
+    def __init__(self, fail_on):
+        self.fail_on = fail_on
+
+    def predict(self, request):
+        def gen():
+            yield "Hello"
+            yield " world."
+            if request["prompt"] == self.fail_on:
+                raise MemoryError("LLM out of memory")
+            yield " Fine."
+            yield "<|eot_id|>"
+        return gen()
+
+
+def test_llm_failure_ends_only_its_request():
+    from llmvox_amd.server import TTSService
+    svc = TTSService([StateEngine(max_streams=8)], max_chunk=16, max_tokens=80, stream_model=_FailingLLM("bad"))
+    try:
+        bad = svc.submit("bad")
+        good = svc.submit("good")
+        with pytest.raises(RuntimeError) as ei:
+            b"".join(svc.chunks(bad, timeout=0.01))
+        assert isinstance(ei.value.__cause__, MemoryError)
+        body = b"".join(svc.chunks(good, timeout=0.01))
+        assert len(body) > 0 and svc.error is None
+        again = b"".join(svc.chunks(svc.submit("good"), timeout=0.01))  # the service keeps serving
+        assert again == body
+    finally:
+        svc.shutdown()
+
+
+def test_build_engine_caps_kv_capacity_at_block_size(monkeypatch):
+    """A checkpoint with block_size < 8192 (zero-padded wpe rows past it): the engine's KV capacity
+    is clamped to block_size, so a position there raises instead of using a zero embedding."""
+    from llmvox_amd import engine as E
+
+    made = {}
+
+    class _Eng:
+        def __init__(self, dev, wd, kd, ms, mp, mcf, cd):
+            made["max_positions"] = mp
+
+        def load_weights(self, *a):
+            pass
+
+    class _GW(dict):
+        block_size = 1024
+
+    monkeypatch.setattr(E, "Engine", _Eng)
+    E.build_engine(0, "bf16", "bf16", max_positions=8192, weights=(_GW(), {}, None))
+    assert made["max_positions"] == 1024
+    E.build_engine(0, "bf16", "bf16", max_positions=512, weights=(_GW(), {}, None))
+    assert made["max_positions"] == 512
