@@ -1927,6 +1927,177 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_bt_kernel(GemvArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Batched fp32 parity mode (fp32 weights, 3 <= B <= 64; option "f32b"): the same five ops per layer
+// as v3, on exact-fp32 MFMA (v_mfma_f32_16x16x4_f32: fp32 products and fp32 accumulation, no
+// reduced-precision operands). A block owns 16 weight rows (blockIdx.x) x R = NT * 16 batch rows
+// (blockIdx.y); K is split over its waves (192 columns = 48 MFMA k-steps each). Weights come from
+// an MFMA-fragment-packed fp32 copy ([N / 16][K / 16][64 lanes][4]: one wave-wide 16-B load = one
+// contiguous KB): lane l holds W[n0 + l % 16][16 j + 4 (l / 16) .. + 3], and MFMA k-step 4 j + e
+// multiplies element e, so the operand row supplies the same k from its float4 at 16 j + 4 (l / 16).
+// The per-row prologue (LayerNorm, layer 0's embedding, the split-KV merge) builds an fp32 operand
+// tile in LDS once per block; mlp c_proj (K = 3072) reads the fp32 h rows from global. Wave partials
+// are summed through LDS in wave order: deterministic, and a row's result never depends on its batch
+// position (an MFMA column's dot product uses only that column's data).
+// ---------------------------------------------------------------------------------
+template <int K, int NT, int IN, int OUT>
+__global__ __launch_bounds__(K / 192 * 64) void ar_f32b_kernel(GemvArgs a) {
+  constexpr int NW = K / 192, R = NT * 16, NTH = NW * 64;
+  constexpr bool STAGE = IN != 1;  // K == 768: the operand tile in LDS
+  static_assert(!STAGE || K == 768, "the LDS operand tile holds K = 768 rows");
+  constexpr int LDX = D + 4;  // fp32 row stride: 16 rows x 4 banks apart, conflict-free 16-B reads
+  __shared__ __attribute__((aligned(16))) float xs[STAGE ? R * LDX : 4];
+  __shared__ float red[NW][16 * R];
+  __shared__ float cf_s[IN == 2 ? R * N_HEAD * NSPLIT : 1];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int n0 = blockIdx.x * 16, r0 = blockIdx.y * R;
+  const int B = a.B;
+  // weights (fragment-packed, the wave's 12 contiguous KB), issued first for IN 1 / IN 2; behind the
+  // first row inputs for the LayerNorm modes (their statistics then overlap the weight stream)
+  const float4* wsrc = reinterpret_cast<const float4*>(a.Wf) + ((size_t)(n0 >> 4) * (K / 16) + wave * 12) * 64 + lane;
+  float4 wf[12];
+  if constexpr (IN == 1 || IN == 2) {
+#pragma unroll
+    for (int j = 0; j < 12; ++j) wf[j] = wsrc[j * 64];
+    // all 12 in flight before anything else (left to itself the scheduler interleaved each load with
+    // the MFMA that uses it: one memory latency per k group)
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (IN == 0 || IN == 3) {
+    constexpr int RPW = R / NW;  // rows per wave (4 or 8), all inputs in flight at once
+    float4 xv[RPW][3];
+    int4 ri[RPW];
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int b = min(r0 + wave * RPW + i, B - 1);  // clamped: no load under a branch
+      if (IN == 0) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) xv[i][j] = *reinterpret_cast<const float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4);
+      } else {
+        ri[i] = a.st.rowinfo[b];
+      }
+    }
+    float4 g[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) g[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 12; ++j) wf[j] = wsrc[j * 64];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int rr = wave * RPW + i, b = r0 + rr;
+      float* dst = xs + rr * LDX;
+      if (b < B) {
+        if (IN == 3) {
+          embed_row(a, ri[i], lane, xv[i]);
+          if (blockIdx.x == 0)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = xv[i][j];
+        }
+        wave_ln_regs(xv[i], g);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(dst + j * 256 + lane * 4) = xv[i][j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(dst + j * 256 + lane * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  } else if constexpr (IN == 2) {
+    // split-KV merge (as gemv_stage_input IN 2): coefficients per (row, head, split), then every
+    // element sums all NSPLIT partials (part_o is zeroed at allocation: unused splits are finite)
+    for (int q = tid; q < R * N_HEAD; q += NTH) {
+      const int bb = q / N_HEAD, head = q - bb * N_HEAD, b = min(r0 + bb, B - 1);
+      const int4 ri = a.st.rowinfo[b];
+      float* cf = cf_s + q * NSPLIT;
+      const int t = ri.y + 1;
+      const int ns = (ri.x < 0 || r0 + bb >= B) ? 0 : min(NSPLIT, (t + 63) / 64);
+      const float* ml = a.st.part_ml + ((size_t)(b * N_HEAD + head) * NSPLIT) * 2;
+      float m[NSPLIT], l[NSPLIT];
+#pragma unroll
+      for (int i = 0; i < NSPLIT; ++i) { m[i] = ml[2 * i]; l[i] = ml[2 * i + 1]; }
+      float M = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < NSPLIT; ++i) if (i < ns) M = fmaxf(M, m[i]);
+      float den = 0.f;
+#pragma unroll
+      for (int i = 0; i < NSPLIT; ++i) {
+        const float f = (i < ns && m[i] != -INFINITY) ? expf(m[i] - M) : 0.f;
+        m[i] = f;
+        den += f * l[i];
+      }
+      const float inv = ns ? 1.0f / den : 0.f;
+#pragma unroll
+      for (int i = 0; i < NSPLIT; ++i) cf[i] = m[i] * inv;
+    }
+    __syncthreads();
+    for (int e = tid; e < R * D; e += NTH) {
+      const int bb = e / D, c = e - bb * D;
+      const int b = min(r0 + bb, B - 1);
+      const int head = c / HD, d = c - head * HD;
+      const float* cf = cf_s + (bb * N_HEAD + head) * NSPLIT;
+      const float* po = a.st.part_o + ((size_t)(b * N_HEAD + head) * NSPLIT) * HD + d;
+      float pv[NSPLIT];
+#pragma unroll
+      for (int i = 0; i < NSPLIT; ++i) pv[i] = po[(size_t)i * HD];
+      float y = 0.f;
+#pragma unroll
+      for (int i = 0; i < NSPLIT; ++i) y += cf[i] * pv[i];
+      xs[bb * LDX + c] = y;
+    }
+  }
+  if constexpr (STAGE) __syncthreads();
+  f32x4_t acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int kq = 4 * (lane >> 4);  // this lane's k offset inside each 16-wide k group
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    float4 xf[12];
+    if constexpr (STAGE) {
+      const float* xr = xs + (t * 16 + (lane & 15)) * LDX + wave * 192 + kq;
+#pragma unroll
+      for (int j = 0; j < 12; ++j) xf[j] = *reinterpret_cast<const float4*>(xr + 16 * j);
+    } else {
+      const int b = min(r0 + t * 16 + (lane & 15), B - 1);  // padded columns recompute row B-1, never stored
+      const float* xr = a.st.h + (size_t)b * K + wave * 192 + kq;
+#pragma unroll
+      for (int j = 0; j < 12; ++j) xf[j] = *reinterpret_cast<const float4*>(xr + 16 * j);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // the tile's 12 operand loads in flight together
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[j].x, xf[j].x, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[j].y, xf[j].y, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[j].z, xf[j].z, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[j].w, xf[j].w, acc[t], 0, 0, 0);
+    }
+  }
+  // lane: C[n0 + 4 (lane >> 4) + i][t * 16 + (lane & 15)]
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[wave][(4 * (lane >> 4) + i) * R + t * 16 + (lane & 15)] = acc[t][i];
+  __syncthreads();
+  for (int e = tid; e < 16 * R; e += NTH) {
+    const int r = e / R, c = e - r * R, n = n0 + r, b = r0 + c;
+    if (b >= B || n >= a.N) continue;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[w][e];
+    gemv_store<OUT>(a, n, b, v);
+  }
+}
+
+int g_opt_f32b = 1;  // 1: batched fp32 parity steps (3 <= B <= 64) on exact-fp32 MFMA; 0: the GEMV family
+
+template <int K, int IN, int OUT>
+static void launch_f32b(const GemvArgs& a, hipStream_t s) {
+  dim3 grid((a.N + 15) / 16, a.B <= 16 ? 1 : (a.B + 31) / 32), block(K / 192 * 64);
+  if (a.B <= 16) hipLaunchKernelGGL((ar_f32b_kernel<K, 1, IN, OUT>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((ar_f32b_kernel<K, 2, IN, OUT>), grid, block, 0, s, a);
+}
+
 // Measured (round-1 sweep, us per step at positions 256-511): v3 saves kernels but every block
 // re-reads the fp32 x rows of its batch tile, and per-CU load bandwidth (not launch count) sets the
 // time of these short GEMMs: B = 8 / 16 / 32 v2 149 / 162 / 191 vs v3 172 / 181 / 203 (16-row
@@ -2042,9 +2213,40 @@ static void launch_qkv_ksplit(const GemvArgs& a, hipStream_t s) {
   else hipLaunchKernelGGL(ar_qkv_ksplit_kernel<2>, dim3(36, 4), dim3(256), 0, s, a);
 }
 
+template <typename TW>
+static bool use_f32b(int B) {
+  return sizeof(TW) == 4 && g_opt_f32b && B >= MFMA_BATCH_MIN && B <= 64;
+}
+
+// batched fp32 parity steps: five exact-fp32 MFMA kernels + the attention per layer, x final at
+// every boundary; the split-KV partials are merged in c_proj's prologue; the select is the argmax
+// kernel after lm_head
+static void launch_op_f32b(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtype, int B, hipStream_t s) {
+  a.layer = l;
+  a.yacc = nullptr;
+  a.add_y = 0;
+  a.xpk = 0;
+  switch (op) {
+    case 0:
+      a.W = w.w_attn[l]; a.Wf = w.f_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
+      if (l == 0) launch_f32b<768, 3, 0>(a, s);
+      else launch_f32b<768, 0, 0>(a, s);
+      break;
+    case 1: launch_attn(a.st, kvdtype, B, l, s, attn_ns_max(B)); break;
+    case 2: a.W = w.w_aproj[l]; a.Wf = w.f_aproj[l]; a.N = D; launch_f32b<768, 2, 1>(a, s); break;
+    case 3: a.W = w.w_fc[l]; a.Wf = w.f_fc[l]; a.N = DFF; a.ln_w = w.ln2[l]; launch_f32b<768, 0, 2>(a, s); break;
+    case 4: a.W = w.w_mproj[l]; a.Wf = w.f_mproj[l]; a.N = D; launch_f32b<3072, 1, 1>(a, s); break;
+    case 5: a.W = w.w_lm; a.Wf = w.f_lm; a.N = VOCAB; a.ln_w = w.lnf; launch_f32b<768, 0, 3>(a, s); break;
+  }
+}
+
 // returns false when the op has no kernel of its own at this B (mlp c_proj inside the fused MLP)
 template <typename TW>
 static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtype, int B, hipStream_t s) {
+  if (use_f32b<TW>(B) && !a.emb_row) {
+    launch_op_f32b(op, a, w, l, kvdtype, B, s);
+    return true;
+  }
   if (use_bt<TW>(B) && !a.emb_row) {
     launch_op_bt(op, a, w, l, kvdtype, B, s);
     return true;

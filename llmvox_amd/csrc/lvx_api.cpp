@@ -252,6 +252,19 @@ static std::vector<float> pack_frag(const std::vector<float>& w, int N, int K) {
   return o;
 }
 
+// fp32 [N][K] -> [N / 16][K / 16][64 lanes][4]: lane l of fragment (T, j) holds
+// W[16 T + l % 16][16 j + 4 (l / 16) .. +4] (ar_f32b_kernel: v_mfma_f32_16x16x4_f32 k-step 4 j + e takes
+// element e)
+static std::vector<float> pack_frag32(const std::vector<float>& w, int N, int K) {
+  std::vector<float> o((size_t)N * K);
+  size_t q = 0;
+  for (int t = 0; t < N / 16; ++t)
+    for (int j = 0; j < K / 16; ++j)
+      for (int l = 0; l < 64; ++l)
+        for (int e = 0; e < 4; ++e) o[q++] = w[(size_t)(16 * t + l % 16) * K + 16 * j + 4 * (l / 16) + e];
+  return o;
+}
+
 extern "C" {
 
 int lvx_version(void) { return 1; }
@@ -368,11 +381,20 @@ int lvx_finalize(lvx_ctx* c) {
         gs[n] = (float)acc;
       }
       if ((r = c->upload_f32(gs, &w.fc_gsum[i]))) return r;
+    } else {  // fp32 parity mode: packed copies for the batched exact-fp32 MFMA GEMMs (ar_f32b_kernel)
+      UP_W(pack_frag32(c->H(p + "attn.c_attn.weight"), 3 * D, D), w.f_attn[i]);
+      UP_W(pack_frag32(c->H(p + "attn.c_proj.weight"), D, D), w.f_aproj[i]);
+      UP_W(pack_frag32(c->H(p + "mlp.c_fc.weight"), DFF, D), w.f_fc[i]);
+      UP_W(pack_frag32(c->H(p + "mlp.c_proj.weight"), D, DFF), w.f_mproj[i]);
     }
   }
   UP_F("transformer.ln_f.weight", w.lnf);
   UP_W(c->H("lm_head.weight"), w.w_lm);
-  if (c->cfg.weight_dtype == LVX_DTYPE_BF16) UP_W(pack_frag(c->H("lm_head.weight"), VOCAB, D), w.f_lm);
+  if (c->cfg.weight_dtype == LVX_DTYPE_BF16) {
+    UP_W(pack_frag(c->H("lm_head.weight"), VOCAB, D), w.f_lm);
+  } else {
+    UP_W(pack_frag32(c->H("lm_head.weight"), VOCAB, D), w.f_lm);
+  }
   // ---- codec ----
   CodecWeights& cw = c->cw;
   cw.codebook = w.codebook;
@@ -580,6 +602,7 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   else if (n == "codec_skinny") g_opt_codec_skinny = value != 0;
   else if (n == "codec_g3") g_opt_codec_g3 = value != 0;
   else if (n == "exp") g_opt_exp = value;
+  else if (n == "f32b") g_opt_f32b = value != 0;
   else return fail(LVX_E_NAME, "unknown option " + n);
   g_opt_epoch.fetch_add(1);  // every context's captured kernels change (checked in cached_graph)
   return LVX_OK;

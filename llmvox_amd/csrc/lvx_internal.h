@@ -24,7 +24,8 @@ __host__ __device__ inline size_t kv_at(size_t layer, size_t chunks, size_t stre
 #endif
 constexpr int YCOPIES = LVX_YCOPIES;  // accumulator copies of the fused MLP (spreads atomic contention)
 constexpr int LM_MAX_BLOCKS = 1024;  // lm_head blocks of the fused argmax tail (4096 rows / 8 per block = 512)
-extern int g_opt_defer_select, g_opt_fuse_mlp, g_opt_bt, g_opt_codec_g2, g_opt_codec_skinny, g_opt_codec_g3, g_opt_exp;  // cross-check switches (lvx_set_option)
+extern int g_opt_defer_select, g_opt_fuse_mlp, g_opt_bt, g_opt_codec_g2, g_opt_codec_skinny, g_opt_codec_g3, g_opt_exp,
+    g_opt_f32b;  // cross-check switches (lvx_set_option)
 
 // Device-resident AR weights. Matrices are [out][in] row-major (torch Linear layout),
 // in the context's weight dtype; vectors and gathered tables are fp32.
@@ -43,8 +44,9 @@ struct ArWeights {
   const float* fc_gsum[N_LAYER] = {};    // bf16 only: G[n] = sum_k ln_2.weight[k] * bf16(c_fc W[n][k]) (batched
                                          // c_fc: LayerNorm applied after the GEMM, ar_mfma2_kernel XM 1)
   const void* w_lm = nullptr;         // [4096][768]
-  // bf16 only: MFMA-fragment-packed copies for the batched GEMMs (pack_frag): [N / 16][K / 32][64][8],
-  // fragment (tile, k-step) = the 1 KB one wave-wide 16-B load of v_mfma_f32_16x16x32_bf16's A operand
+  // MFMA-fragment-packed copies for the batched GEMMs, one contiguous KB per wave-wide 16-B load of
+  // the A operand: bf16 [N / 16][K / 32][64][8] for v_mfma_f32_16x16x32_bf16 (pack_frag); fp32
+  // [N / 16][K / 16][64][4] for v_mfma_f32_16x16x4_f32 (pack_frag32, the fp32 parity mode)
   const void* f_attn[N_LAYER] = {};
   const void* f_aproj[N_LAYER] = {};
   const void* f_fc[N_LAYER] = {};

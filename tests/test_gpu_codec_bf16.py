@@ -160,3 +160,23 @@ def test_fp8_codec_weights_close_to_fp32(engs, eng_fp8, S, L):
     print("fp8 codec rel RMS", max(errs))
     assert max(errs) < 0.08
 
+
+
+def test_bf16_decode_at_the_bench_shape():
+    """configs[2]'s codec call exactly as bench.py makes it: 32 streams x 256 frames = 8,192 frames
+    in one batched decode (gemm_glds_kernel at 2 blocks per CU). Every stream within 2 % relative RMS
+    of the fp32 parity engine's decode of the same codes (this shape was never compared)."""
+    from llmvox_amd.engine import build_engine
+    e16 = build_engine(0, "bf16", "bf16", max_streams=2, max_positions=64, max_codec_frames=32 * 256)
+    e32 = build_engine(0, "fp32", "fp32", max_streams=2, max_positions=64, max_codec_frames=32 * 256)
+    try:
+        g = torch.Generator().manual_seed(3256)
+        codes = torch.randint(0, 4096, (32, 256), generator=g).to(torch.int32).to(e16.device)
+        p16 = e16.decode_codes(codes).cpu().numpy()
+        p32 = e32.decode_codes(codes).cpu().numpy()
+    finally:
+        e16.close()
+        e32.close()
+    errs = [_rel_rms(p16[b], p32[b]) for b in range(32)]
+    print(f"bf16 codec 32 x 256 frames: max rel RMS vs fp32 {max(errs):.4f}, mean {np.mean(errs):.4f}")
+    assert max(errs) < 0.02

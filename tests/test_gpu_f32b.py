@@ -1,0 +1,112 @@
+"""Batched fp32 parity mode on exact-fp32 MFMA (ar_f32b_kernel, 3 <= B <= 64).
+
+The fp32 mode is the bit-exact mode: its greedy ids must equal the reference's. With B rows all
+speaking the reference's sentence from position 0, every row must reproduce the reference's own
+ids: the 256 golden decode steps (ar_golden.npz) and the reference's 2,490-step replica-0 stream
+(stream_long_golden.npz, through its 2.1e-6 top1-top2 margin at step 498), and the last step's
+logits must lie within the fp32 parity bar (2e-5) of the reference's. The MFMA path is also held
+against the fp32 GEMV family (option f32b = 0) and for batch-position independence."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from llmvox_amd.engine import build_engine
+    e = build_engine(0, "fp32", "fp32", max_streams=64, max_positions=2560, max_codec_frames=16)
+    yield e
+    e.close()
+
+
+def _free_run(e, B, text, n):
+    dev = e.device
+    for s in range(B):
+        e.reset_slot(s)
+    plan = np.full((B, n), 384, dtype=np.int32)
+    plan[:, :min(n, len(text))] = np.asarray(text[:n], dtype=np.int32)
+    plan = torch.from_numpy(plan).to(dev)
+    slots = torch.arange(B, dtype=torch.int32, device=dev)
+    rowstep = torch.zeros(B, dtype=torch.int32, device=dev)
+    tok = torch.zeros(B, n, dtype=torch.int32, device=dev)
+    e.ar_steps(n, slots, plan, rowstep, tok)
+    e.check_errors()
+    return tok.cpu().numpy(), e.last_logits(B).cpu().numpy()
+
+
+@pytest.mark.parametrize("B", [3, 32, 48])
+def test_f32b_ids_bit_exact_256_golden_steps(eng, B):
+    g = np.load(os.path.join(GOLDEN, "ar_golden.npz"))
+    ids, text = g["ids"], g["text_ids"].tolist()
+    tok, lg = _free_run(eng, B, text, len(ids))
+    for b in range(B):
+        np.testing.assert_array_equal(tok[b], ids, err_msg=f"row {b}")
+    err = float(np.abs(lg - g["logits"][-1]).max())
+    print(f"\n[f32b B={B}] 256 steps bit-exact; step-255 max |dlogit| {err:.3g}")
+    assert err < 2e-5
+
+
+def test_f32b_ids_bit_exact_2490_step_reference_stream(eng):
+    """B = 32 rows, the reference's own audio_generator_sync stream of replica 0 (one segment: dumps
+    10 + 30 + 90 + 270 + 810 + 1280 = 2,490 model calls), every row every id."""
+    g = np.load(os.path.join(GOLDEN, "stream_long_golden.npz"))
+    ids, text = g["ids"], g["text_ids"].tolist()
+    tok, _ = _free_run(eng, 32, text, len(ids))
+    bad = [(b, int(np.nonzero(tok[b] != ids)[0][0])) for b in range(32) if (tok[b] != ids).any()]
+    assert not bad, f"(row, first mismatching step): {bad[:4]}"
+
+
+def test_f32b_matches_gemv_family(eng):
+    """One ragged batch (rows at different positions, distinct texts) stepped on the MFMA path and on
+    the GEMV family (option f32b = 0): same ids, logits within fp32 summation-order noise."""
+    rng = np.random.default_rng(4)
+    B, n = 12, 40
+    texts = rng.integers(3, 384, size=(B, n)).astype(np.int32)
+    res = []
+    for opt in (1, 0):
+        eng.set_option("f32b", opt)
+        try:
+            dev = eng.device
+            for s in range(B):
+                eng.reset_slot(s)
+            pre = torch.from_numpy(texts[::2].copy()).to(dev)  # even rows first run 16 steps alone
+            Bp = pre.shape[0]
+            eng.ar_steps(16, torch.arange(0, B, 2, dtype=torch.int32, device=dev), pre,
+                         torch.zeros(Bp, dtype=torch.int32, device=dev), torch.zeros(Bp, n, dtype=torch.int32, device=dev))
+            plan = torch.from_numpy(texts).to(dev)
+            rowstep = torch.tensor([16 if b % 2 == 0 else 0 for b in range(B)], dtype=torch.int32, device=dev)
+            tok = torch.zeros(B, n, dtype=torch.int32, device=dev)
+            eng.ar_steps(20, torch.arange(B, dtype=torch.int32, device=dev), plan, rowstep, tok)
+            eng.check_errors()
+            res.append((tok.cpu().numpy(), eng.last_logits(B).cpu().numpy()))
+        finally:
+            eng.set_option("f32b", 1)
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    d = float(np.abs(res[0][1] - res[1][1]).max())
+    print(f"\n[f32b vs GEMV] max |dlogit| {d:.3g}")
+    assert d < 1e-5
+
+
+def test_f32b_rows_independent_of_batch_position(eng):
+    rng = np.random.default_rng(9)
+    B, n = 20, 24
+    texts = rng.integers(3, 384, size=(B, n)).astype(np.int32)
+    dev = eng.device
+    out = []
+    for order in (list(range(B)), list(rng.permutation(B))):
+        for s in range(B):
+            eng.reset_slot(s)
+        plan = torch.from_numpy(texts[order]).to(dev)
+        tok = torch.zeros(B, n, dtype=torch.int32, device=dev)
+        eng.ar_steps(n, torch.tensor(order, dtype=torch.int32, device=dev), plan,
+                     torch.zeros(B, dtype=torch.int32, device=dev), tok)
+        eng.check_errors()
+        inv = np.argsort(order)
+        out.append((tok.cpu().numpy()[inv], eng.last_logits(B).cpu().numpy()[inv]))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])

@@ -21,49 +21,44 @@ GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 BOUNDS = {("bf16", "bf16"): 0.03, ("bf16", "fp8"): 0.15}
 
 
-# B: rows per step. B = 1 runs the single-stream kernels (configs[1]); B = 32 the batched MFMA path
-# of the bench's default workload (configs[2]); B = 8 the fp8-KV batched path of configs[4]. Every
-# row of a step gets the same teacher-forced history (its own slot), so all rows must also agree.
-@pytest.mark.parametrize("wd,kvd,B", [("bf16", "bf16", 1), ("bf16", "bf16", 32), ("bf16", "fp8", 1), ("bf16", "fp8", 8)],
-                         ids=["bf16-B1", "bf16-B32", "bf16-kvfp8-B1", "bf16-kvfp8-B8"])
-def test_teacher_forced_256_steps(wd, kvd, B):
+def _teacher_forced(wd, kvd, B, ids, text, keep, max_positions):
+    """Run len(ids) teacher-forced steps; returns (picks [n][B], logits at the `keep` steps (row 0),
+    whether every row of a kept step agreed with row 0 to 1e-5)."""
     from llmvox_amd.engine import build_engine
-    g = np.load(os.path.join(GOLDEN, "ar_golden.npz"))
-    ids, margins, text = g["ids"], g["margins"], g["text_ids"].tolist()
     n = len(ids)
-    e = build_engine(0, wd, kvd, max_streams=B, max_positions=512, max_codec_frames=16)
+    e = build_engine(0, wd, kvd, max_streams=B, max_positions=max_positions, max_codec_frames=16)
     dev = e.device
     try:
         slots = torch.arange(B, dtype=torch.int32, device=dev)
         plan = torch.zeros(B, 2, dtype=torch.int32, device=dev)
         rowstep = torch.zeros(B, dtype=torch.int32, device=dev)
         tok = torch.zeros(B, 2, dtype=torch.int32, device=dev)
-        marg = torch.zeros(B, 2, dtype=torch.float32, device=dev)
-        picks, gm, kept, rows_ok = [], [], {}, True
-        keep = g["logit_steps"].tolist()
+        picks, kept, rows_ok = [], {}, True
         for i in range(n):
             for b in range(B):
                 e.set_slot(b, i, int(ids[i - 1]) if i > 0 else 0)
             plan.fill_(text[i] if i < len(text) else 384)
             rowstep.zero_()
-            e.ar_steps(1, slots, plan, rowstep, tok, marg)
+            e.ar_steps(1, slots, plan, rowstep, tok)
             if i in keep:
                 lg = e.last_logits(B).cpu().numpy()
                 kept[i] = lg[0]
                 rows_ok &= bool(np.abs(lg - lg[0]).max() < 1e-5)
             picks.append(tok[:, 0].clone())
-            gm.append(marg[0, 0].clone())
         e.check_errors()
         allp = torch.stack(picks).cpu().numpy()  # [n][B]
-        picks = allp[:, 0]
-        gm = torch.stack(gm).cpu().numpy()
     finally:
         e.close()
-    bound = BOUNDS[(wd, kvd)]
-    err = max(float(np.abs(kept[s] - g["logits"][k]).max()) for k, s in enumerate(keep))
+    return allp, kept, rows_ok
+
+
+def _check(tag, allp, kept, rows_ok, ids, margins, ref_logits, keep, bound):
+    picks = allp[:, 0]
+    n = len(ids)
+    err = max(float(np.abs(kept[s] - ref_logits[k]).max()) for k, s in enumerate(keep))
     agree = float((picks == ids).mean())
     must = margins > 2 * bound
-    print(f"\n[teacher-forced {wd}/kv {kvd} B={B}] agreement {agree:.4f} over {n} steps; "
+    print(f"\n[teacher-forced {tag}] agreement {agree:.4f} over {n} steps; "
           f"max |dlogit| at recorded steps {err:.4g} (bound {bound}); steps with margin > {2 * bound}: "
           f"{int(must.sum())}, mismatches there: {int((picks != ids)[must].sum())}; "
           f"mismatch steps {np.nonzero(picks != ids)[0].tolist()} (golden margins "
@@ -72,3 +67,37 @@ def test_teacher_forced_256_steps(wd, kvd, B):
     assert rows_ok and (allp == allp[:, :1]).all(), "rows with the same history disagree"
     np.testing.assert_array_equal(picks[must], ids[must])
     assert agree >= 0.95
+
+
+# B: rows per step. B = 1 runs the single-stream kernels (configs[1]); B = 32 the batched MFMA path
+# of the bench's default workload (configs[2]); B = 8 the fp8-KV batched path of configs[4]. Every
+# row of a step gets the same teacher-forced history (its own slot), so all rows must also agree.
+@pytest.mark.parametrize("wd,kvd,B", [("bf16", "bf16", 1), ("bf16", "bf16", 32), ("bf16", "fp8", 1), ("bf16", "fp8", 8)],
+                         ids=["bf16-B1", "bf16-B32", "bf16-kvfp8-B1", "bf16-kvfp8-B8"])
+def test_teacher_forced_256_steps(wd, kvd, B):
+    g = np.load(os.path.join(GOLDEN, "ar_golden.npz"))
+    ids, margins, text = g["ids"], g["margins"], g["text_ids"].tolist()
+    keep = g["logit_steps"].tolist()
+    allp, kept, rows_ok = _teacher_forced(wd, kvd, B, ids, text, keep, 512)
+    _check(f"{wd}/kv {kvd} B={B}", allp, kept, rows_ok, ids, margins, g["logits"], keep, BOUNDS[(wd, kvd)])
+
+
+# the bench's whole KV range: configs[2] decodes positions 0..1,023 of each utterance
+# (16 KV chunks of 64 positions) in an engine of 8,192 positions per slot (the bench's layout). The
+# reference's own stream (stream_long_golden.npz: its audio_generator_sync ids and top1-top2
+# margins) is teacher-forced through position 1,023; logits are held against the reference's at
+# positions 511 / 767 / 1,023 (ar_long_golden.npz) plus the first two recorded steps of ar_golden.
+@pytest.mark.parametrize("wd,kvd,B", [("bf16", "bf16", 32), ("bf16", "fp8", 8), ("bf16", "bf16", 1)],
+                         ids=["bf16-B32", "bf16-kvfp8-B8", "bf16-B1"])
+def test_teacher_forced_through_position_1023(wd, kvd, B):
+    lg = np.load(os.path.join(GOLDEN, "stream_long_golden.npz"))
+    ll = np.load(os.path.join(GOLDEN, "ar_long_golden.npz"))
+    g = np.load(os.path.join(GOLDEN, "ar_golden.npz"))
+    n = 1024
+    ids, margins, text = lg["ids"][:n], lg["margins"][:n], lg["text_ids"].tolist()
+    np.testing.assert_array_equal(ll["ids"], ids)
+    keep = g["logit_steps"].tolist()[:2] + ll["logit_steps"].tolist()
+    ref = np.concatenate([g["logits"][:2], ll["logits"]])
+    allp, kept, rows_ok = _teacher_forced(wd, kvd, B, ids, text, keep, 8192)
+    _check(f"{wd}/kv {kvd} B={B}, positions 0..{n - 1}", allp, kept, rows_ok, ids, margins, ref, keep,
+           BOUNDS[(wd, kvd)])
