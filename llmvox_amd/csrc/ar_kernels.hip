@@ -2358,6 +2358,10 @@ static GemvArgs make_args(const ArWeights& w, const ArState& st, int kvdtype, in
   return a;
 }
 
+#include "ar_persist.inc"
+
+size_t persist_ctr_words() { return PG_CTR_WORDS; }
+
 // returns whether the greedy select is deferred into the next step (no argmax kernel after lm_head)
 template <typename TW>
 static bool ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B, const float* emb_row, int slot,
@@ -2365,6 +2369,10 @@ static bool ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B,
   GemvArgs a = make_args<TW>(w, st, kvdtype, B, emb_row);
   a.defer_sel = (select && !emb_row) ? (defer_select<TW>(B) ? 1 : defer_select_batched<TW>(B) ? 2 : 0) : 0;
   if (emb_row) hipLaunchKernelGGL(ar_row_state_kernel, dim3(1), dim3(1), 0, s, st, slot, pos);
+  if (!emb_row && a.defer_sel == 2 && logits_dst == st.logits && use_persist<TW>(B, kvdtype, st)) {
+    launch_persist(w, st, B, s);  // the whole step as one dataflow launch
+    return true;
+  }
   for (int l = 0; l < N_LAYER; ++l)
     for (int op = 0; op < 5; ++op) launch_op<TW>(op, a, w, l, kvdtype, B, s);
   a.dst = logits_dst;

@@ -493,8 +493,19 @@ int lvx_finalize(lvx_ctx* c) {
       (r = c->dalloc(&st.xn, (size_t)S16 * D)) || (r = c->dalloc(&st.hb, (size_t)S16 * DFF)) ||
       (r = c->dalloc(&st.xb, (size_t)S16 * D)) || (r = c->dalloc(&st.xstat, (size_t)(D / 16) * S * 2)) ||
       (r = c->dalloc(&st.lmbest, (size_t)LM_MAX_BLOCKS * 4 * 2)) ||
-      (r = c->dalloc(&st.yacc, (size_t)YCOPIES * S * D)) || (r = c->dalloc(&st.qkvp, (size_t)4 * S * 3 * D)))
+      (r = c->dalloc(&st.yacc, (size_t)YCOPIES * S * D)) || (r = c->dalloc(&st.qkvp, (size_t)4 * S * 3 * D)) ||
+      (r = c->dalloc(&st.xa, (size_t)S16 * D)) || (r = c->dalloc(&st.pctr, persist_ctr_words())) ||
+      (r = c->dalloc(&st.pdone, 4)) || (r = c->dalloc(&st.ptmo, 4)))
     return r;
+  HIP_TRY(hipMemset(st.pctr, 0, persist_ctr_words() * 4));
+  HIP_TRY(hipMemset(st.pdone, 0, 16));
+  HIP_TRY(hipMemset(st.ptmo, 0, 16));
+  HIP_TRY(hipMemset(st.xa, 0, (size_t)S16 * D * 2));
+  {  // the persistent step's grid: one workgroup per CU (every workgroup resident at once)
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, c->cfg.device));
+    st.pgrid = prop.multiProcessorCount;
+  }
   HIP_TRY(hipMemset(st.yacc, 0, (size_t)YCOPIES * S * D * 4));
   HIP_TRY(hipMemset(st.selp, 0, 16));
   HIP_TRY(hipMemset(st.part_o, 0, (size_t)S * N_HEAD * NSPLIT * HD * 4));
@@ -603,6 +614,7 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   else if (n == "codec_g3") g_opt_codec_g3 = value != 0;
   else if (n == "exp") g_opt_exp = value;
   else if (n == "f32b") g_opt_f32b = value != 0;
+  else if (n == "persist") g_opt_persist = value != 0;
   else return fail(LVX_E_NAME, "unknown option " + n);
   g_opt_epoch.fetch_add(1);  // every context's captured kernels change (checked in cached_graph)
   return LVX_OK;
@@ -767,6 +779,13 @@ int lvx_check_errors(lvx_ctx* c, void* stream) {
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   if (v) {
     (void)hipMemsetAsync(c->st.err, 0, 4, (hipStream_t)stream);
+    if (v & 16) {  // a persistent step's wait timed out: its counters are in an unknown state
+      (void)hipMemsetAsync(c->st.pctr, 0, persist_ctr_words() * 4, (hipStream_t)stream);
+      (void)hipMemsetAsync(c->st.pdone, 0, 4, (hipStream_t)stream);
+      (void)hipMemsetAsync(c->st.ptmo, 0, 4, (hipStream_t)stream);
+      (void)hipStreamSynchronize((hipStream_t)stream);
+      return fail(LVX_E_HIP, "a persistent decode step's dependency wait timed out (results of that call are invalid)");
+    }
     if (v & 4) return fail(LVX_E_INDEX, "index out of range in self (a text id outside [0, 386) or a code "
                                          "outside [0, 4096) given to lvx_text_embed / lvx_codes_to_features / lvx_codec_decode_codes)");
     if (v & 8) return fail(LVX_E_STATE, "ISTFT window envelope <= 1e-11 (spectral_ops.py:72 assertion)");

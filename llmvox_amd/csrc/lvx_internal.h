@@ -25,7 +25,8 @@ __host__ __device__ inline size_t kv_at(size_t layer, size_t chunks, size_t stre
 constexpr int YCOPIES = LVX_YCOPIES;  // accumulator copies of the fused MLP (spreads atomic contention)
 constexpr int LM_MAX_BLOCKS = 1024;  // lm_head blocks of the fused argmax tail (4096 rows / 8 per block = 512)
 extern int g_opt_defer_select, g_opt_fuse_mlp, g_opt_bt, g_opt_codec_g2, g_opt_codec_skinny, g_opt_codec_g3, g_opt_exp,
-    g_opt_f32b;  // cross-check switches (lvx_set_option)
+    g_opt_f32b, g_opt_persist;
+size_t persist_ctr_words();  // words of ArState::pctr  // cross-check switches (lvx_set_option)
 
 // Device-resident AR weights. Matrices are [out][in] row-major (torch Linear layout),
 // in the context's weight dtype; vectors and gathered tables are fp32.
@@ -86,6 +87,11 @@ struct ArState {
   float* yacc = nullptr;        // [max_streams][YCOPIES][768] fused-MLP output accumulators (fp32 atomics);
                                 // a row's copies adjacent: spaced by max_streams rows they shared
                                 // L2 channels (B = 1: 82.6 vs 69.6 us/step at max_streams 32)
+  bf16_t* xa = nullptr;         // [max_streams rounded to 16][768] attention outputs of the persistent step (xfrag)
+  uint32_t* pctr = nullptr;     // persistent step: dependency counters (PG_CTR_WORDS, zero between launches)
+  uint32_t* pdone = nullptr;    // [1] its workgroups finished
+  uint32_t* ptmo = nullptr;     // [1] sticky timeout flag of its waits (cleared by lvx_check_errors)
+  int pgrid = 0;                // its workgroups (one per CU)
   void* kc = nullptr;           // [4][kv_chunks][max_streams][8][KV_CHUNK][96] (kv_at)
   void* vc = nullptr;
   int max_pos = 0, max_streams = 0, kv_chunks = 0;
