@@ -2011,7 +2011,9 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_f32b_kernel(GemvArgs a) {
       const int4 ri = a.st.rowinfo[b];
       float* cf = cf_s + q * NSPLIT;
       const int t = ri.y + 1;
-      const int ns = (ri.x < 0 || r0 + bb >= B) ? 0 : min(NSPLIT, (t + 63) / 64);
+      int nsm = NSPLIT;  // the attention's split count at this B (attn_ns_max)
+      while (nsm > 1 && nsm * N_HEAD * B > 256) nsm >>= 1;
+      const int ns = (ri.x < 0 || r0 + bb >= B) ? 0 : min(nsm, (t + 63) / 64);
       const float* ml = a.st.part_ml + ((size_t)(b * N_HEAD + head) * NSPLIT) * 2;
       float m[NSPLIT], l[NSPLIT];
 #pragma unroll
