@@ -694,6 +694,8 @@ def main():
     ap.add_argument("--utterance", type=int, default=1024,
                     help="configs[1]/[2]/[4]: tokens per utterance (SURVEY 8(d) N = 1024; a multiple of --chunk): "
                          "KV reset and a new sentence at every utterance start; 0 = one utterance for the whole run")
+    ap.add_argument("--opt", default="",
+                    help="library options for A/B runs, name=value[,name=value] (lvx_set_option; default: production)")
     ap.add_argument("--rehearse", action="store_true",
                     help="CPU-only rehearsal of the multi-rank skeleton (gloo; tests/test_bench_launcher.py)")
     args = ap.parse_args()
@@ -741,6 +743,9 @@ def main():
                        codec_dtype=args.codec_dtype)
     dev = eng.device
     torch.cuda.set_device(dev)
+    for kv in filter(None, args.opt.split(",")):
+        k, v = kv.split("=")
+        eng.set_option(k, int(v))
     if args.no_graphs:
         eng.set_graphs(False)
     if args.graph_stream:

@@ -2530,6 +2530,17 @@ void launch_codes_to_features(const float* codebook, const int64_t* codes, int B
 }  // namespace lvx
 
 #ifdef LVX_TIMING
+// timing build only (tools/persist_timeline.py): copy / clear the persistent step's task records
+extern "C" int lvx_debug_persist(void* dst, size_t bytes, int clear) {
+  if (bytes > sizeof(lvx::g_pg_ts)) bytes = sizeof(lvx::g_pg_ts);
+  if (dst && hipMemcpyFromSymbol(dst, HIP_SYMBOL(lvx::g_pg_ts), bytes) != hipSuccess) return -3;
+  if (clear) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(lvx::g_pg_ts)) != hipSuccess) return -3;
+    if (hipMemset(p, 0, sizeof(lvx::g_pg_ts)) != hipSuccess) return -3;
+  }
+  return (int)bytes;
+}
 // timing build only (tools/step_timeline.py): copy / clear the step timeline records
 extern "C" int lvx_debug_timeline(void* dst, size_t bytes, int clear) {
   if (bytes > sizeof(lvx::g_lvx_ts)) bytes = sizeof(lvx::g_lvx_ts);
