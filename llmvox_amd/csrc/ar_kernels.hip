@@ -946,12 +946,50 @@ template <> struct KvPiece<fp8_t> {
 // summed its waves (bit-identical), q goes through LDS, and the split holding key t - 1 appends the
 // new key's K / V to the cache and takes them from LDS in its last tile (its own store is not read
 // back).
+// Online softmax kept PER KEY SLOT (bf16 / fp8 KV; round 3): each lane quad owns one key slot of the
+// tile (4 lanes x 24 dims) and keeps its own (m, l, o[24]) over the keys it sees, so a tile needs no
+// wave-wide reduction (the wave-uniform form spent two DPP + readlane reductions and a 24-deep FMA
+// chain per 64-key tile: the tile loop, not the KV stream, bounded the decode attention, ~0.65 us
+// per tile whether the keys came from HBM or from LDS, tools/persist_timeline.py). The score is
+// four 6-term FMA chains summed pairwise. The slots are folded into the wave (max, rescale, DPP
+// sums) once at the end. fp32 KV (the bit-exact parity mode) keeps the wave-uniform form.
+__device__ __forceinline__ void slot_softmax_step(float& m, float& l, float (&o)[24], const float (&q)[24],
+                                                  const float (&kf)[24], const float (&vf)[24], bool valid) {
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    s0 = fmaf(q[i], kf[i], s0);
+    s1 = fmaf(q[6 + i], kf[6 + i], s1);
+    s2 = fmaf(q[12 + i], kf[12 + i], s2);
+    s3 = fmaf(q[18 + i], kf[18 + i], s3);
+  }
+  const float sc = quad_sum((s0 + s1) + (s2 + s3));  // every lane of the quad: the same bits
+  if (!valid) return;
+  const float mn = fmaxf(m, sc);
+  const float alpha = expf(m - mn);  // m = -inf (first key of the slot): 0
+  const float p = expf(sc - mn);
+  l = l * alpha + p;
+#pragma unroll
+  for (int i = 0; i < 24; ++i) o[i] = fmaf(p, vf[i], o[i] * alpha);
+  m = mn;
+}
+// fold the 16 slots of a wave: returns the wave's max; o / l rescaled to it (slots that saw no key: 0)
+__device__ __forceinline__ float slot_fold_wave(float m, float& l, float (&o)[24]) {
+  const float M = wave_max(m);
+  const float f = (m == -INFINITY) ? 0.f : expf(m - M);
+  l *= f;
+#pragma unroll
+  for (int i = 0; i < 24; ++i) o[i] *= f;
+  return M;
+}
+
 template <typename TKV, int DEPTH, int NW, bool QKV = false>
 __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int layer, int ns_max, int direct,
                                                          int selcopy) {
   // NW waves: a tile is NW x 16 keys (4 lanes per key); NW = 8 doubles the bytes in flight per
   // block for long splits (batched steps)
   constexpr int TK = NW * 16;
+  constexpr bool SLOT = sizeof(TKV) < 4;  // per-key-slot online softmax (bf16 / fp8 KV)
   static_assert(!QKV || (sizeof(TKV) == 2 && NW == 4 && 3 * HD <= 2 * NW * 64), "the K-split c_attn path: bf16 keys, 256 threads");
   __shared__ float wm_s[NW], wl_s[NW];
   __shared__ float wo_s[NW][4][HD];  // [wave][16-lane row][part * 24 + i]
@@ -1054,6 +1092,10 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
 #pragma unroll
       for (int i = 0; i < 3; ++i) { kp[i].get(kf + 8 * i); vp[i].get(vf + 8 * i); }
     }
+    if constexpr (SLOT) {
+      slot_softmax_step(m, l, o, q, kf, vf, valid);
+      return;
+    }
     float sc = 0.f;
 #pragma unroll
     for (int i = 0; i < 24; ++i) sc = fmaf(q[i], kf[i], sc);
@@ -1106,6 +1148,10 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
       issue(kb + (d + DEPTH) * TK, kpr[d], vpr[d]);
       if (DEPTH > 2) __builtin_amdgcn_sched_barrier(0);  // keep the refill right behind its tile
     }
+  }
+  if constexpr (SLOT) {  // the slots' states folded into the wave's (m, l, o)
+    m = slot_fold_wave(m, l, o);
+    l = wave_sum(part == 0 ? l : 0.f);
   }
   // sum o over the 16 key slots of the wave (lanes with equal part): within each 16-lane row by
   // DPP (row_ror 8, 4), the four rows through LDS
@@ -2531,6 +2577,11 @@ void launch_codes_to_features(const float* codebook, const int64_t* codes, int B
 
 #ifdef LVX_TIMING
 // timing build only (tools/persist_timeline.py): copy / clear the persistent step's task records
+extern "C" int lvx_debug_persist_att(void* dst, size_t bytes) {
+  if (bytes > sizeof(lvx::g_pg_att)) bytes = sizeof(lvx::g_pg_att);
+  if (dst && hipMemcpyFromSymbol(dst, HIP_SYMBOL(lvx::g_pg_att), bytes) != hipSuccess) return -3;
+  return (int)bytes;
+}
 extern "C" int lvx_debug_persist(void* dst, size_t bytes, int clear) {
   if (bytes > sizeof(lvx::g_pg_ts)) bytes = sizeof(lvx::g_pg_ts);
   if (dst && hipMemcpyFromSymbol(dst, HIP_SYMBOL(lvx::g_pg_ts), bytes) != hipSuccess) return -3;

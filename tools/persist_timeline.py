@@ -28,7 +28,7 @@ dev = e.device
 plan = torch.full((B, 64), 100, dtype=torch.int32, device=dev)
 slots = torch.arange(B, dtype=torch.int32, device=dev)
 tok = torch.zeros(B, 64, dtype=torch.int32, device=dev)
-buf = np.zeros(4096 * 4, dtype=np.uint64)
+buf = np.zeros(8192 * 4, dtype=np.uint64)
 stream = torch.cuda.Stream(device=dev)
 spans = []
 with torch.cuda.stream(stream):
@@ -42,7 +42,7 @@ with torch.cuda.stream(stream):
         e.ar_steps(1, slots, plan, rowstep, tok)
         torch.cuda.synchronize()
 assert lib.lvx_debug_persist(buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes, 0) > 0
-r = buf.reshape(4096, 4).astype(np.int64)
+r = buf.reshape(8192, 4).astype(np.int64)
 r = r[r[:, 0] != 0]
 base = r[:, 0].min()
 ph = r[:, 3] >> 32
@@ -61,3 +61,20 @@ for p in sorted(set(ph.tolist())):
     mwork = ((v[:, 2] - v[:, 1]) / 100).max()
     print(f"{name:9s} L{l if p < 24 else '-'} {len(v):5d} {fs:11.2f} {lw:13.2f} {le:9.2f} {wait:9.2f} {work:9.2f} {mwork:9.2f}")
 print(f"step span {(r[:, 2].max() - base) / 100:.2f} us")
+
+# attention tasks of layer 3: wait done -> q barrier (DMA landed) -> LDS tiles -> HBM tiles
+lib.lvx_debug_persist_att.restype = ctypes.c_int
+lib.lvx_debug_persist_att.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+att = np.zeros(1024 * 4, dtype=np.uint64)
+lib.lvx_debug_persist_att(att.ctypes.data_as(ctypes.c_void_p), att.nbytes)
+att = att.reshape(1024, 4).astype(np.int64)
+v3 = r[(r[:, 3] >> 32) == 20]
+wd = {int((x[3] >> 8) & 0xffffff): x[1] for x in v3}
+sp = []
+for blk, (a0, a1, a2, _) in enumerate(att[:256]):
+    if a0 and blk in wd:
+        sp.append(((a0 - wd[blk]) / 100, (a1 - a0) / 100, (a2 - a1) / 100))
+if sp:
+    sp = np.array(sp)
+    print("attention L3 (median / max us): wait-done -> q barrier %.2f / %.2f, LDS tiles %.2f / %.2f, HBM tiles %.2f / %.2f"
+          % (np.median(sp[:, 0]), sp[:, 0].max(), np.median(sp[:, 1]), sp[:, 1].max(), np.median(sp[:, 2]), sp[:, 2].max()))
