@@ -344,6 +344,11 @@ class _HostCollectives:
         self.d.all_reduce(h, op=op)
         t.copy_(h)
 
+    def broadcast(self, t, src=0):
+        h = t.cpu()
+        self.d.broadcast(h, src=src)
+        t.copy_(h)
+
 
 # ---------------------------------------------------------------------------------------
 def run_config3(args, eng, world, rank, local, dist):
@@ -353,19 +358,24 @@ def run_config3(args, eng, world, rank, local, dist):
     host). Stream g uses replica index g % 2 (initial dump 10 / 160, x3 to 1280,
     streaming_server.py:357-422). One step = one utterance of --utt-tokens tokens per stream; the
     utterance's tail below the dump size is flushed (the reference flushes it at end-of-audio)."""
+    from llmvox_amd.parallel import gather_bytes, scatter_texts
     from llmvox_amd.streaming import FusedScheduler
     dev = eng.device
     S, N, K, Wm = args.streams, args.utt_tokens, args.steps, args.warmup
     sched = FusedScheduler(eng, max_chunk=256, to_bytes=True)
-    rng = np.random.default_rng(1234 + rank)
+    rng = np.random.default_rng(1234)  # rank 0 draws every rank's request texts
+    pcm_bytes = [0]
 
     def utterance():
         streams = []
         t0 = time.perf_counter()  # first text word enqueued (p50 first-chunk latency starts here)
+        # the path's inbound exchange: rank 0 (the LLM host side) scatters the world*S request texts
+        texts = ([SENTENCE if g == 0 else random_sentence(rng) for g in range(world * S)] if rank == 0 else None)
+        mine = scatter_texts(texts, S, dev, dist, rank, world)
         for s in range(S):
             g = rank * S + s
             st = sched.open_stream(index=g % 2, dump_size=10 if g % 2 == 0 else 160)
-            for w in (SENTENCE if g == 0 else random_sentence(rng)).split(" "):
+            for w in mine[s].split(" "):
                 st.feed(w)
             streams.append(st)
         first = None
@@ -375,17 +385,19 @@ def run_config3(args, eng, world, rank, local, dist):
             if first is None and any(st.events for st in streams):
                 first = (time.perf_counter() - t0) * 1e3
         sched.flush()
-        rest = []  # the tail below the current dump size: flushed as one last dump (end of audio)
-        for st in streams:
-            if st.m.speech_outputs:
-                rest.append(st.m.speech_outputs)
+        tails = {}  # the tail below the current dump size: flushed as one last dump (end of audio)
+        rest = [st for st in streams if st.m.speech_outputs]
+        for L in sorted({len(st.m.speech_outputs) for st in rest}):
+            grp = [st for st in rest if len(st.m.speech_outputs) == L]
+            codes = torch.tensor([st.m.speech_outputs for st in grp], dtype=torch.int32, device=dev)
+            for st, row in zip(grp, eng.decode_codes(codes).cpu().numpy()):
+                tails[st] = row.astype("float32").tobytes()
                 st.m.speech_outputs = []
-        if rest:
-            for L in sorted({len(r) for r in rest}):
-                grp = [r for r in rest if len(r) == L]
-                codes = torch.tensor(grp, dtype=torch.int32, device=dev)
-                for row in eng.decode_codes(codes).cpu().numpy():
-                    _ = row.astype("float32").tobytes()
+        # the outbound exchange: every stream's f32le bytes (its dumps in order + the tail) to rank 0
+        out = [b"".join(x for x in st.events if isinstance(x, bytes)) + tails.get(st, b"") for st in streams]
+        got = gather_bytes(out, dev, dist, rank, world)
+        if rank == 0:
+            pcm_bytes[0] += sum(len(x) for r in got for x in r)
         n_tok = sum(len(st.tokens) for st in streams)
         for st in streams:
             sched.close_stream(st)
@@ -393,6 +405,7 @@ def run_config3(args, eng, world, rank, local, dist):
 
     for _ in range(Wm):
         utterance()
+    pcm_bytes[0] = 0
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -445,7 +458,9 @@ def run_config3(args, eng, world, rank, local, dist):
                                    "one codec call per dump, f32le bytes on the host",
                        "streams_per_gpu": S, "utterance_tokens": N, "dump_schedule_replica0": dump_schedule(N, 10),
                        "dump_schedule_replica1": dump_schedule(N, 160),
-                       "parallelism": f"streams sharded over {world} GPU(s)"},
+                       "parallelism": f"streams sharded over {world} GPU(s); rank 0 scatters the request texts and "
+                                      "gathers every stream's PCM bytes (sizes first) over RCCL"},
+            "pcm_bytes_gathered_rank0": pcm_bytes[0],
             "audio_samples_per_s": round(320 * value, 1),
             "realtime_factor_per_stream": round(value / (world * S) / 75.0, 1),
             "p50_first_chunk_latency_ms": round(statistics.median(firsts), 3),
