@@ -973,6 +973,60 @@ __device__ __forceinline__ void slot_softmax_step(float& m, float& l, float (&o)
   for (int i = 0; i < 24; ++i) o[i] = fmaf(p, vf[i], o[i] * alpha);
   m = mn;
 }
+// bf16 KV: the same step on the raw bf16 pairs. The score is v_dot2_f32_bf16 of the key pairs with q
+// split into bf16 hi + lo parts (q = hi + lo to ~2^-17: the products keep fp32-level accuracy) in
+// four independent chains, and o is updated with packed fp32 math (v_pk_mul / v_pk_fma_f32): about
+// half the VALU instructions per 64-key tile of the float form (no key conversions).
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+struct QSplit {
+  uint32_t hi[12], lo[12];  // bf16 pairs (dims 2j, 2j + 1)
+};
+__device__ __forceinline__ void qsplit_make(const float (&q)[24], QSplit& qs) {
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    const bf16_t h0 = f32_to_bf16(q[2 * j]), h1 = f32_to_bf16(q[2 * j + 1]);
+    const bf16_t l0 = f32_to_bf16(q[2 * j] - bf16_to_f32(h0)), l1 = f32_to_bf16(q[2 * j + 1] - bf16_to_f32(h1));
+    qs.hi[j] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+    qs.lo[j] = (uint32_t)l0 | ((uint32_t)l1 << 16);
+  }
+}
+__device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float c) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a), __builtin_bit_cast(bf16x2_t, b), c, false);
+}
+__device__ __forceinline__ void slot_softmax_step_bf16(float& m, float& l, f32x2_t (&o)[12], const QSplit& qs,
+                                                       const uint4 (&kp)[3], const uint4 (&vp)[3], bool valid) {
+  uint32_t k[12], v[12];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    k[4 * i] = kp[i].x; k[4 * i + 1] = kp[i].y; k[4 * i + 2] = kp[i].z; k[4 * i + 3] = kp[i].w;
+    v[4 * i] = vp[i].x; v[4 * i + 1] = vp[i].y; v[4 * i + 2] = vp[i].z; v[4 * i + 3] = vp[i].w;
+  }
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    s0 = dot2_bf16(qs.hi[j], k[j], s0);
+    s1 = dot2_bf16(qs.hi[6 + j], k[6 + j], s1);
+    s2 = dot2_bf16(qs.lo[j], k[j], s2);
+    s3 = dot2_bf16(qs.lo[6 + j], k[6 + j], s3);
+  }
+  const float sc = quad_sum((s0 + s1) + (s2 + s3));
+  if (!valid) return;
+  const float mn = fmaxf(m, sc);
+  // 2^(x log2 e) on v_exp_f32 (arguments <= 0; m = -inf gives 0): ~1 ulp, two instructions instead
+  // of expf's range-reduced sequence
+  const float alpha = __builtin_amdgcn_exp2f((m - mn) * 1.4426950408889634f);
+  const float p = __builtin_amdgcn_exp2f((sc - mn) * 1.4426950408889634f);
+  l = l * alpha + p;
+  const f32x2_t a2 = f32x2_t{alpha, alpha}, p2 = f32x2_t{p, p};
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    const f32x2_t vv = f32x2_t{__uint_as_float(v[j] << 16), __uint_as_float(v[j] & 0xffff0000u)};
+    o[j] = __builtin_elementwise_fma(p2, vv, o[j] * a2);
+  }
+  m = mn;
+}
+
 // fold the 16 slots of a wave: returns the wave's max; o / l rescaled to it (slots that saw no key: 0)
 __device__ __forceinline__ float slot_fold_wave(float m, float& l, float (&o)[24]) {
   const float M = wave_max(m);
@@ -1035,7 +1089,10 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
   const int t = ri.y + 1;
   const int ns = min(ns_max, (t + ATK - 1) / ATK);
   if (sp >= ns) return;
-  const int chunk = (t + ns - 1) / ns;
+  // SLOT (bf16 / fp8 KV): split ranges on whole 64-key tiles, so every tile is one KV chunk and a
+  // lane's key address is the chunk base (wave-uniform) + a fixed lane offset (a trailing split
+  // may be empty: it writes m = -inf, l = 0). fp32 KV keeps the unrounded ranges of the parity mode.
+  const int chunk = SLOT ? (((t + ns - 1) / ns + ATK - 1) / ATK) * ATK : (t + ns - 1) / ns;
   const int k0 = sp * chunk, k1 = min(t, k0 + chunk);
   // key k of this (slot, head): chunk k / KV_CHUNK (cstride elements apart), row k % KV_CHUNK
   const size_t base = kv_at(layer, st.kv_chunks, st.max_streams, s, head, 0);
@@ -1064,7 +1121,17 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
   // sits under a branch: the compiler's vmcnt for "this set has landed" then leaves the other sets
   // in flight instead of draining every outstanding load.
   KvPiece<TKV> kpr[DEPTH][3], vpr[DEPTH][3];
+  const int klast = ((k1 - 1) / ATK) * ATK;  // SLOT: start of the last tile (a tile past it is clamped to it)
   auto issue = [&](int kb, KvPiece<TKV>(&kp)[3], KvPiece<TKV>(&vp)[3]) {
+    if constexpr (SLOT) {  // keys past k1 in the last chunk: allocated rows, masked by `valid`
+      const size_t off = (size_t)(min(kb, klast) / KV_CHUNK) * cstride + (size_t)kq * HD + part * 24;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        kp[i].load(Kg + off + i * 8);
+        vp[i].load(Vg + off + i * 8);
+      }
+      return;
+    }
     const int key = min(kb + kq, k1 - 1);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -1072,8 +1139,33 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
       vp[i].load(Vg + krow(key) + part * 24 + i * 8);
     }
   };
+  constexpr bool BF = SLOT && sizeof(TKV) == 2;  // bf16 pairs straight into v_dot2 / packed fp32 math
+  f32x2_t o2[BF ? 12 : 1];
+  if constexpr (BF) {
+#pragma unroll
+    for (int j = 0; j < 12; ++j) o2[j] = f32x2_t{0.f, 0.f};
+  }
+  QSplit qsp;
   auto tile = [&](int kb, const KvPiece<TKV>(&kp)[3], const KvPiece<TKV>(&vp)[3]) {
     const bool valid = kb + kq < k1;
+    if constexpr (BF) {
+      uint4 ku[3], vu[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) { ku[i] = reinterpret_cast<const uint4&>(kp[i]); vu[i] = reinterpret_cast<const uint4&>(vp[i]); }
+      if constexpr (QKV) {  // the tile holding key t - 1 (wave-uniform test): that lane takes it from LDS
+        if (kb + TK >= k1) {
+          if (kb + kq == t - 1) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+              ku[i] = reinterpret_cast<const uint4*>(kvh_s[0])[part * 3 + i];
+              vu[i] = reinterpret_cast<const uint4*>(kvh_s[1])[part * 3 + i];
+            }
+          }
+        }
+      }
+      slot_softmax_step_bf16(m, l, o2, qsp, ku, vu, valid);
+      return;
+    }
     float kf[24], vf[24];
     if constexpr (QKV) {  // the tile holding key t - 1 (wave-uniform): that lane takes it from LDS
       KvPiece<TKV> kx[3], vx[3];
@@ -1136,6 +1228,7 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
 #pragma unroll
     for (int i = 0; i < 24; ++i) q[i] = qs_s[part * 24 + i] * 0.10206207261596575f;
   }
+  if constexpr (BF) qsplit_make(q, qsp);
   // DEPTH 2 (few tiles per block, the B <= 2 step): leave after the last valid tile. DEPTH >= 4
   // (long splits, batched steps): whole groups of DEPTH tiles with no exit inside a group (a tile
   // past k1 is all-invalid: alpha = 1, p = 0), which keeps the compiler from draining every
@@ -1148,6 +1241,10 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
       issue(kb + (d + DEPTH) * TK, kpr[d], vpr[d]);
       if (DEPTH > 2) __builtin_amdgcn_sched_barrier(0);  // keep the refill right behind its tile
     }
+  }
+  if constexpr (BF) {
+#pragma unroll
+    for (int j = 0; j < 12; ++j) { o[2 * j] = o2[j].x; o[2 * j + 1] = o2[j].y; }
   }
   if constexpr (SLOT) {  // the slots' states folded into the wave's (m, l, o)
     m = slot_fold_wave(m, l, o);
