@@ -563,14 +563,18 @@ def first_chunk_latency(eng, reps=12):
     return statistics.median(lat)
 
 
-def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, world=1, codec_overlap=False):
+def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, world=1, codec_overlap=False,
+               seconds=0.0, window_s=10.0):
     """W untimed then K timed bench steps (one step = `chunk` fused decode steps for the S streams,
     the batched codec decode of their codes, the PCM to the host; the PCM gathered to rank 0 when
     distributed). With reset_every R, step c is chunk c % R of utterance c // R: the streams' KV
     slots are reset at every utterance start and `mine` holds the utterances' text plans back to
     back ([S][n_utterances * R * chunk]). Returns (seconds, last token buffer, codec stream, token
-    buffers, PCM buffers)."""
+    buffers, PCM buffers). seconds > 0 (steady-state mode): chunks run until that much wall time has
+    passed instead of K (the plans are cycled), with a device sync every window_s seconds to record
+    the rate of each window (run_chunks.windows, run_chunks.k_done)."""
     from llmvox_amd.parallel import gather_pcm
+    n_plan_chunks = mine.shape[1] // chunk
     dev = eng.device
     slots = torch.arange(S, dtype=torch.int32, device=dev)
     text_plan = torch.empty(S, chunk, dtype=torch.int32, device=dev)
@@ -598,7 +602,7 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
         i = c & 1
         main = torch.cuda.current_stream(dev)
         main.wait_event(ev_codec[i])  # tok_bufs[i] is free again (its decode has read it)
-        col = c * chunk  # chunk c of the back-to-back utterance plans
+        col = (c % n_plan_chunks) * chunk  # chunk c of the back-to-back utterance plans (cycled)
         if reset_every and c % reset_every == 0:  # a new utterance: KV slots reset (a new sentence)
             for s_ in range(S):
                 eng.reset_slot(s_)
@@ -647,8 +651,26 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
     torch.cuda.synchronize()
     timing = ar_t
     t0 = time.perf_counter()
-    for c in range(K):
-        run_chunk(c)
+    run_chunks.windows = []
+    if seconds > 0:  # steady state: whole utterances until `seconds` have passed, windows of window_s
+        c, wc, wt = 0, 0, t0
+        while True:
+            run_chunk(c)
+            c += 1
+            now = time.perf_counter()
+            if now - wt >= window_s or now - t0 >= seconds:
+                torch.cuda.synchronize()
+                now = time.perf_counter()
+                run_chunks.windows.append({"chunks": c - wc, "seconds": round(now - wt, 3),
+                                           "tokens_per_s": round((c - wc) * S * chunk / (now - wt), 1)})
+                wc, wt = c, now
+                if now - t0 >= seconds and (not reset_every or c % reset_every == 0):
+                    break
+        K = c
+    else:
+        for c in range(K):
+            run_chunk(c)
+    run_chunks.k_done = K
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -709,6 +731,9 @@ def main():
     ap.add_argument("--utterance", type=int, default=1024,
                     help="configs[1]/[2]/[4]: tokens per utterance (SURVEY 8(d) N = 1024; a multiple of --chunk): "
                          "KV reset and a new sentence at every utterance start; 0 = one utterance for the whole run")
+    ap.add_argument("--seconds", type=float, default=0.0,
+                    help="steady-state mode: run whole utterances for this many seconds instead of --steps "
+                         "(configs[4]: continuous sentences with a KV reset per sentence), rate per 10 s window")
     ap.add_argument("--opt", default="",
                     help="library options for A/B runs, name=value[,name=value] (lvx_set_option; default: production)")
     ap.add_argument("--rehearse", action="store_true",
@@ -779,6 +804,10 @@ def main():
     reset_every = args.utterance // chunk if args.utterance else 0
     utt = args.utterance or max(K, Wm) * chunk
     n_utt = -(-max(K, Wm) * chunk // utt)
+    if args.seconds > 0:
+        if not reset_every:
+            raise SystemExit("--seconds needs utterances (--utterance > 0): a KV reset per sentence")
+        n_utt = max(n_utt, 16)  # a pool of 16 sentences per stream, cycled
     n_pos = n_utt * utt
     plans = np.zeros((world * S, n_pos), dtype=np.int32)
     rng = np.random.default_rng(1234)
@@ -791,7 +820,10 @@ def main():
     mine = scatter_plans(torch.from_numpy(plans), S, n_pos, dev, dist, rank)
 
     dt, last_tok, codec_stream, tok_bufs, pcm_bufs = run_chunks(
-        eng, mine, S, chunk, K, Wm, reset_every, dist, rank, world, args.codec_overlap)
+        eng, mine, S, chunk, K, Wm, reset_every, dist, rank, world, args.codec_overlap, seconds=args.seconds)
+    windows = list(run_chunks.windows)
+    if args.seconds > 0:
+        K = run_chunks.k_done
     if dist is not None:
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -912,6 +944,12 @@ def main():
                         for v in kern.values()} if kern else None,
             "tokens_head": toks_rank0[:8].tolist(),
         }
+        if args.seconds > 0:
+            rates = [w["tokens_per_s"] for w in windows if w["seconds"] >= 1.0]
+            out["steady_state"] = {"seconds": round(dt, 3), "chunks": K, "utterances_per_stream": K // reset_every,
+                                   "windows": windows,
+                                   "spread": (round((max(rates) - min(rates)) / (sum(rates) / len(rates)), 4)
+                                              if rates else None)}
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()
