@@ -162,8 +162,9 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
  *   "f32b"         1: fp32 weights, 3 <= B <= 64: batched steps on exact-fp32 MFMA (ar_f32b_kernel);
  *                     0: the fp32 GEMV family (same ids against the reference: tests/test_gpu_f32b.py);
  *   "persist"      1: bf16 weights + bf16 KV, 17 <= B <= 32: each decode step is ONE persistent dataflow
- *                     launch (ar_persist_kernel); 0: the 26 launches of the batched path (bit-identical:
- *                     tests/test_gpu_persist.py). */
+ *                     launch (ar_persist_kernel); 0 (default, measured faster): the 26 launches of the
+ *                     batched path (bit-identical: tests/test_gpu_persist.py);
+ *   "pexp"         persistent-step development bits (1: no KV-history prefetch). */
 int lvx_set_option(lvx_ctx* ctx, const char* name, int value);
 /* Enable/disable HIP-graph replay of lvx_ar_step for a given B (default on). */
 int lvx_set_graphs(lvx_ctx* ctx, int enable);

@@ -92,7 +92,9 @@ struct GemvArgs {
   const float* wpe;
   const float* emb_row;  // drop-in row mode when non-null
   // fused MLP (ar_mlp_fused_kernel): its output sits in YCOPIES accumulators until c_proj folds it in
-  float* yacc;           // non-null when the step runs the fused MLP
+  float* yacc;           // batched steps: the mlp c_proj K-slice partials (fp32, plain stores)
+  unsigned long long* yfx;  // B <= 2 fused MLP (non-null when the step runs it): its output as YCOPIES
+                            // accumulators in 2^-32 fixed point (int64 atomics: order-independent sums)
   const float* gsum;     // batched c_fc (ar_mfma2_kernel XM 1): ArWeights::fc_gsum of the layer
   int add_y;             // c_proj: fold the accumulators into x (layers >= 1; 0 at layer 0 = just clear)
   int defer_sel;         // deferred greedy select (option "defer_select"). 1: B <= 2 GEMV step, lm_head
@@ -266,17 +268,40 @@ __device__ __forceinline__ void wave_ln_to_lds(float4 (&v)[3], const float4 (&ga
 
 // x[b] (IN 0) or x[b] + sum_c yacc[b][c] (IN 4) in the lane layout k = j * 256 + lane * 4: the
 // loads are issued by xrow_issue and summed by xrow_sum, so a prefetch does not wait on them
-template <int IN>
+// The fused MLP's fixed point (B <= 2): partial t -> round(t * 2^32) as int64, added with 64-bit
+// integer atomics (exact, so the sum does not depend on the order the 192 blocks arrive in: the
+// output is reproducible run to run), read back as (float)(sum of the copies) * 2^-32
+typedef unsigned long long u64x2n __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned long long yfx_of(float t) {
+  return (unsigned long long)__float2ll_rn(t * 4294967296.0f);
+}
+__device__ __forceinline__ float yfx_to_f(unsigned long long s) {
+  return __ll2float_rn((long long)s) * 2.3283064365386963e-10f;
+}
+
+// FX = false: the batched steps' fp32 K-slice partials (ar_rows_kernel<4>); FX = true: the B <= 2
+// fused MLP's fixed-point copies (GEMV IN 4)
+template <int IN, bool FX = false>
 struct XRow {
   float4 x[3];
-  float4 y[IN == 4 ? YCOPIES : 1][3];
+  float4 y[(IN == 4 && !FX) ? YCOPIES : 1][3];
+  u64x2n yf[(IN == 4 && FX) ? YCOPIES : 1][3][2];
 };
-template <int IN>
-__device__ __forceinline__ void xrow_issue(const GemvArgs& a, int b, int lane, XRow<IN>& r) {
+template <int IN, bool FX = false>
+__device__ __forceinline__ void xrow_issue(const GemvArgs& a, int b, int lane, XRow<IN, FX>& r) {
   const float* xr = a.st.x + (size_t)b * D;
 #pragma unroll
   for (int j = 0; j < 3; ++j) r.x[j] = *reinterpret_cast<const float4*>(xr + j * 256 + lane * 4);
-  if constexpr (IN == 4) {
+  if constexpr (IN == 4 && FX) {
+#pragma unroll
+    for (int c = 0; c < YCOPIES; ++c)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const u64x2n* yp = reinterpret_cast<const u64x2n*>(a.yfx + ((size_t)b * YCOPIES + c) * D + j * 256 + lane * 4);
+        r.yf[c][j][0] = yp[0];
+        r.yf[c][j][1] = yp[1];
+      }
+  } else if constexpr (IN == 4) {
 #pragma unroll
     for (int c = 0; c < YCOPIES; ++c)
 #pragma unroll
@@ -284,12 +309,17 @@ __device__ __forceinline__ void xrow_issue(const GemvArgs& a, int b, int lane, X
         r.y[c][j] = *reinterpret_cast<const float4*>(a.yacc + ((size_t)b * YCOPIES + c) * D + j * 256 + lane * 4);
   }
 }
-template <int IN>
-__device__ __forceinline__ void xrow_sum(const XRow<IN>& r, float4 (&v)[3]) {
+template <int IN, bool FX = false>
+__device__ __forceinline__ void xrow_sum(const XRow<IN, FX>& r, float4 (&v)[3]) {
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     float4 t = r.x[j];
-    if constexpr (IN == 4) {
+    if constexpr (IN == 4 && FX) {
+      u64x2n s0 = r.yf[0][j][0], s1 = r.yf[0][j][1];
+#pragma unroll
+      for (int c = 1; c < YCOPIES; ++c) { s0 += r.yf[c][j][0]; s1 += r.yf[c][j][1]; }
+      t.x += yfx_to_f(s0.x); t.y += yfx_to_f(s0.y); t.z += yfx_to_f(s1.x); t.w += yfx_to_f(s1.y);
+    } else if constexpr (IN == 4) {
 #pragma unroll
       for (int c = 0; c < YCOPIES; ++c) { t.x += r.y[c][j].x; t.y += r.y[c][j].y; t.z += r.y[c][j].z; t.w += r.y[c][j].w; }
     }
@@ -299,7 +329,7 @@ __device__ __forceinline__ void xrow_sum(const XRow<IN>& r, float4 (&v)[3]) {
 
 template <int K, int IN>
 __device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, float* aux, const float4 (&gam)[3], int g0, int bg,
-                                                 const XRow<IN == 4 ? 4 : 0>& xpre, int4 ripre, bool prefetched) {
+                                                 const XRow<IN == 4 ? 4 : 0, true>& xpre, int4 ripre, bool prefetched) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   if (IN == 0 || IN == 3 || IN == 4 || IN == 5) {
     for (int bb = wave; bb < bg; bb += 4) {  // one wave per row
@@ -310,7 +340,7 @@ __device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, f
         if (pre) {
           xrow_sum(xpre, v);
         } else {
-          XRow<IN == 4 ? 4 : 0> xr;
+          XRow<IN == 4 ? 4 : 0, true> xr;
           xrow_issue(a, b, lane, xr);
           xrow_sum(xr, v);
         }
@@ -431,7 +461,7 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
   const int row0 = (blockIdx.x * WROWS + rg) * RPW;
   // inputs of the first batch group first (vmcnt retires in issue order): the LayerNorm /
   // embedding math then overlaps the weight stream instead of waiting behind it
-  XRow<IN == 4 ? 4 : 0> xpre;
+  XRow<IN == 4 ? 4 : 0, true> xpre;
   int4 ripre = make_int4(-1, 0, 0, 0);
   const bool prefetched = wave < min(BG, a.B);
   // control record of this lane's epilogue row in the first batch group (bb = lane % BG): the
@@ -441,14 +471,15 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
   // residual epilogue (OUT 1): this lane's (row, batch row) of the first group is (row0 + lane / BG,
   // lane % BG); its x element (and, for c_proj after a fused MLP, the pending accumulators) is
   // loaded now instead of behind the dot products
-  float xep = 0.f, yep[YCOPIES];
+  float xep = 0.f;
+  unsigned long long yep[YCOPIES];
   if constexpr (OUT == 1) {
     const int n = row0 + lane / BG, b = lane % BG;
     if (lane < RPW * BG && n < a.N && b < a.B) {
       xep = a.st.x[(size_t)b * D + n];
-      if (IN == 2 && a.yacc)
+      if (IN == 2 && a.yfx)
 #pragma unroll
-        for (int c = 0; c < YCOPIES; ++c) yep[c] = a.yacc[((size_t)b * YCOPIES + c) * D + n];
+        for (int c = 0; c < YCOPIES; ++c) yep[c] = a.yfx[((size_t)b * YCOPIES + c) * D + n];
     }
   }
   if ((IN == 0 || IN == 3 || IN == 4) && prefetched) {
@@ -592,13 +623,15 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
         } else if (OUT == 1) {
           float* xp = a.st.x + (size_t)b * D + n;
           float t = g0 == 0 ? xep : *xp;
-          if (IN == 2 && a.yacc) {  // c_proj: fold the fused MLP's accumulators into x and clear them
+          if (IN == 2 && a.yfx) {  // c_proj: fold the fused MLP's accumulators into x and clear them
+            unsigned long long ys = 0;
 #pragma unroll
             for (int c = 0; c < YCOPIES; ++c) {
-              float* yp = a.yacc + ((size_t)b * YCOPIES + c) * D + n;
-              if (a.add_y) t += g0 == 0 ? yep[c] : *yp;
-              *yp = 0.f;
+              unsigned long long* yp = a.yfx + ((size_t)b * YCOPIES + c) * D + n;
+              ys += g0 == 0 ? yep[c] : *yp;
+              *yp = 0ull;
             }
+            if (a.add_y) t += yfx_to_f(ys);
           }
           *xp = t + v;
         } else if (OUT == 2) {
@@ -704,12 +737,13 @@ __global__ __launch_bounds__(256) void ar_cproj_b1_kernel(GemvArgs a) {
   }
   const int row0 = (blockIdx.x * 4 + wave) * RPW;
   // residual epilogue operands of lane r < RPW (row row0 + r): x and the fused MLP's accumulators
-  float xep = 0.f, yep[YCOPIES];
+  float xep = 0.f;
+  unsigned long long yep[YCOPIES];
   if (lane < RPW && row0 + lane < a.N) {
     xep = a.st.x[row0 + lane];
-    if (a.yacc)
+    if (a.yfx)
 #pragma unroll
-      for (int c = 0; c < YCOPIES; ++c) yep[c] = a.yacc[(size_t)c * D + row0 + lane];
+      for (int c = 0; c < YCOPIES; ++c) yep[c] = a.yfx[(size_t)c * D + row0 + lane];
   }
   const TW* __restrict__ W = reinterpret_cast<const TW*>(a.W);
   typename WReg<TW>::T wr[RPW][3];
@@ -757,12 +791,14 @@ __global__ __launch_bounds__(256) void ar_cproj_b1_kernel(GemvArgs a) {
     const float v = wave_sum(acc[r]);
     if (lane == r && row0 + r < a.N) {
       float t = xep;
-      if (a.yacc) {
+      if (a.yfx) {
+        unsigned long long ys = 0;
 #pragma unroll
         for (int c = 0; c < YCOPIES; ++c) {
-          if (a.add_y) t += yep[c];
-          a.yacc[(size_t)c * D + row0 + r] = 0.f;
+          ys += yep[c];
+          a.yfx[(size_t)c * D + row0 + r] = 0ull;
         }
+        if (a.add_y) t += yfx_to_f(ys);
       }
       a.st.x[row0 + r] = t + v;
     }
@@ -837,7 +873,7 @@ __global__ __launch_bounds__(256) void ar_mlp_fused_kernel(GemvArgs a, const bf1
     }
   __syncthreads();
   // thread tid: outputs e = tid + 256 jj; pack g element jj * 16 + j = W[e][n0 + 16 g + j]
-  float* y = a.yacc + (size_t)(blockIdx.x % YCOPIES) * D;  // row bb's copies: y + bb * YCOPIES * D
+  unsigned long long* y = a.yfx + (size_t)(blockIdx.x % YCOPIES) * D;  // row bb's copies: y + bb * YCOPIES * D
 #pragma unroll
   for (int bb = 0; bb < BG; ++bb) {
 #pragma unroll
@@ -851,7 +887,7 @@ __global__ __launch_bounds__(256) void ar_mlp_fused_kernel(GemvArgs a, const bf1
         t = fmaf(__uint_as_float(u.y << 16), hs[bb][4 * g + 2], t);
         t = fmaf(__uint_as_float(u.y & 0xffff0000u), hs[bb][4 * g + 3], t);
       }
-      atomicAdd(y + (size_t)bb * YCOPIES * D + tid + 256 * jj, t);
+      atomicAdd(y + (size_t)bb * YCOPIES * D + tid + 256 * jj, yfx_of(t));  // no-return int64 add
     }
   }
 }
@@ -1044,7 +1080,8 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
   // block for long splits (batched steps)
   constexpr int TK = NW * 16;
   constexpr bool SLOT = sizeof(TKV) < 4;  // per-key-slot online softmax (bf16 / fp8 KV)
-  static_assert(!QKV || (sizeof(TKV) == 2 && NW == 4 && 3 * HD <= 2 * NW * 64), "the K-split c_attn path: bf16 keys, 256 threads");
+  static_assert(!QKV || (sizeof(TKV) == 2 && (NW == 4 || NW == 8)), "the K-split c_attn path: bf16 keys, 4 or 8 waves");
+  constexpr int QH = QKV ? (3 * HD + NW * 64 - 1) / (NW * 64) : 1;  // q / k / v elements per thread (2 at 4 waves, 1 at 8)
   __shared__ float wm_s[NW], wl_s[NW];
   __shared__ float wo_s[NW][4][HD];  // [wave][16-lane row][part * 24 + i]
   __shared__ float qs_s[QKV ? HD : 1];
@@ -1061,11 +1098,11 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
   // QKV: thread tid owns elements e = tid and tid + 256 (tid < 32) of this head's (q, k, v) (element
   // e % 96 of q / k / v for e / 96 = 0 / 1 / 2); their four K-slice partials are issued with the
   // control record (clamped element: no load under a branch)
-  float pq[QKV ? 2 : 1][QKV ? 4 : 1];
+  float pq[QH][QKV ? 4 : 1];
   if constexpr (QKV) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int e = min(tid + 256 * h, 3 * HD - 1);
+    for (int h = 0; h < QH; ++h) {
+      const int e = min(tid + NW * 64 * h, 3 * HD - 1);
       const float* pp = st.qkvp + (size_t)b * (3 * D) + (e / HD) * D + head * HD + e % HD;
 #pragma unroll
       for (int k = 0; k < 4; ++k) pq[h][k] = pp[(size_t)k * st.max_streams * (3 * D)];
@@ -1124,7 +1161,9 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
   const int klast = ((k1 - 1) / ATK) * ATK;  // SLOT: start of the last tile (a tile past it is clamped to it)
   auto issue = [&](int kb, KvPiece<TKV>(&kp)[3], KvPiece<TKV>(&vp)[3]) {
     if constexpr (SLOT) {  // keys past k1 in the last chunk: allocated rows, masked by `valid`
-      const size_t off = (size_t)(min(kb, klast) / KV_CHUNK) * cstride + (size_t)kq * HD + part * 24;
+      // (a tile of NW * 16 keys spans NW / 4 chunks; chunks past the last one are clamped to it)
+      const size_t off = (size_t)min((kb / KV_CHUNK) + (kq / KV_CHUNK), klast / KV_CHUNK) * cstride +
+                         (size_t)(kq % KV_CHUNK) * HD + part * 24;
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         kp[i].load(Kg + off + i * 8);
@@ -1208,8 +1247,8 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
     // the partials were issued before the tiles (vmcnt retires in issue order: this waits for them
     // alone); raw barrier after the LDS writes, the tiles stay in flight
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int e = tid + 256 * h;
+    for (int h = 0; h < QH; ++h) {
+      const int e = tid + NW * 64 * h;
       float v = 0.f;
 #pragma unroll
       for (int k = 0; k < 4; ++k) v += pq[h][k];
@@ -2264,6 +2303,8 @@ static void launch_bt(const GemvArgs& a, hipStream_t s) {
 // blocks (B = 32 at t = 256-511: 1024 blocks 164, 512 169, 256 = one split that writes xn
 // itself 155.5; B = 16: 138 / 136 / 131; B = 8: 144 / 133 / 130).
 constexpr int ATTN_BLOCKS = 256;
+// (round 3, measured no faster: 8-wave blocks for the one-split bf16 attention at B = 32, 132.1 vs 130.3
+// us/step at t = 0..1,023: the tile loop streams the KV history at ~7 TB/s either way)
 static int attn_ns_max(int B) {  // enough splits to fill the chip, no more (early-exit blocks cost)
   int ns = NSPLIT;
   while (ns > 1 && ns * N_HEAD * B > ATTN_BLOCKS) ns >>= 1;
@@ -2403,7 +2444,8 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
   // fragment-packed operand rows on the v2 steps with the rows kernel (9 <= B <= 32; exp bit 4: row-major)
   a.xpk = (mf && B > MFMA_LN_MAX && B <= 32 && !(g_opt_exp & 4)) ? 1 : 0;
   a.layer = l;
-  a.yacc = (fm || mf) ? a.st.yacc : nullptr;
+  a.yacc = mf ? a.st.yacc : nullptr;
+  a.yfx = fm ? a.st.yfx : nullptr;
   a.add_y = l > 0;
   switch (op) {
     case 0:

@@ -495,8 +495,9 @@ int lvx_finalize(lvx_ctx* c) {
       (r = c->dalloc(&st.lmbest, (size_t)LM_MAX_BLOCKS * 4 * 2)) ||
       (r = c->dalloc(&st.yacc, (size_t)YCOPIES * S * D)) || (r = c->dalloc(&st.qkvp, (size_t)4 * S * 3 * D)) ||
       (r = c->dalloc(&st.xa, (size_t)S16 * D)) || (r = c->dalloc(&st.pctr, persist_ctr_words())) ||
-      (r = c->dalloc(&st.pdone, 4)) || (r = c->dalloc(&st.ptmo, 4)))
+      (r = c->dalloc(&st.pdone, 4)) || (r = c->dalloc(&st.ptmo, 4)) || (r = c->dalloc(&st.yfx, (size_t)YCOPIES * S * D)))
     return r;
+  HIP_TRY(hipMemset(st.yfx, 0, (size_t)YCOPIES * S * D * 8));
   HIP_TRY(hipMemset(st.pctr, 0, persist_ctr_words() * 4));
   HIP_TRY(hipMemset(st.pdone, 0, 16));
   HIP_TRY(hipMemset(st.ptmo, 0, 16));
@@ -615,6 +616,7 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   else if (n == "exp") g_opt_exp = value;
   else if (n == "f32b") g_opt_f32b = value != 0;
   else if (n == "persist") g_opt_persist = value != 0;
+  else if (n == "pexp") g_opt_pexp = value;
   else return fail(LVX_E_NAME, "unknown option " + n);
   g_opt_epoch.fetch_add(1);  // every context's captured kernels change (checked in cached_graph)
   return LVX_OK;

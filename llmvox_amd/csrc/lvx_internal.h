@@ -25,7 +25,7 @@ __host__ __device__ inline size_t kv_at(size_t layer, size_t chunks, size_t stre
 constexpr int YCOPIES = LVX_YCOPIES;  // accumulator copies of the fused MLP (spreads atomic contention)
 constexpr int LM_MAX_BLOCKS = 1024;  // lm_head blocks of the fused argmax tail (4096 rows / 8 per block = 512)
 extern int g_opt_defer_select, g_opt_fuse_mlp, g_opt_bt, g_opt_codec_g2, g_opt_codec_skinny, g_opt_codec_g3, g_opt_exp,
-    g_opt_f32b, g_opt_persist;
+    g_opt_f32b, g_opt_persist, g_opt_pexp;
 size_t persist_ctr_words();  // words of ArState::pctr  // cross-check switches (lvx_set_option)
 
 // Device-resident AR weights. Matrices are [out][in] row-major (torch Linear layout),
@@ -84,7 +84,9 @@ struct ArState {
   float* logits = nullptr;      // [B][4096]
   float* qkvp = nullptr;        // [4][max_streams][2304] c_attn K-slice partials (batched B > 16: summed by the attention)
   uint64_t* lmbest = nullptr;   // [LM_MAX_BLOCKS][4][2] per-block top1/top2 granules of lm_head (deferred select, B <= 2)
-  float* yacc = nullptr;        // [max_streams][YCOPIES][768] fused-MLP output accumulators (fp32 atomics);
+  unsigned long long* yfx = nullptr;  // [max_streams][YCOPIES][768] B <= 2 fused-MLP output, 2^-32 fixed point
+                                     // (int64 atomics), a row's copies adjacent
+  float* yacc = nullptr;        // [max_streams][YCOPIES][768] batched mlp c_proj K-slice partials (fp32);
                                 // a row's copies adjacent: spaced by max_streams rows they shared
                                 // L2 channels (B = 1: 82.6 vs 69.6 us/step at max_streams 32)
   bf16_t* xa = nullptr;         // [max_streams rounded to 16][768] attention outputs of the persistent step (xfrag)

@@ -51,8 +51,9 @@ def _run(e, order, texts, prefix_rows, n_prefix, n_main):
 def eng():
     from llmvox_amd.engine import build_engine
     e = build_engine(0, "bf16", "bf16", max_streams=40, max_positions=1024, max_codec_frames=256)
-    yield e
     e.set_option("persist", 1)
+    yield e
+    e.set_option("persist", 0)
     e.close()
 
 
