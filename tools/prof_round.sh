@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round measurement refresh (round 2+): PMC passes over the driver's default bench command
+# Round measurement refresh (round 2+; TAG defaults to the current round): PMC passes over the driver's default bench command
 # (configs[2], --steps 20: the roofline probe at KV position 2,560), kernel-trace stats of it, and
 # the bench line itself. Outputs under gpurun_out/$TAG; copy the summaries to profiles/.
 #   FETCH_SIZE and WRITE_SIZE passes  -> tools/pmc_traffic.py  -> pmc_traffic.json
@@ -7,7 +7,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 export PYTHONPATH=.
-TAG=${TAG:-r02}
+TAG=${TAG:-r03}
 O=gpurun_out/$TAG; mkdir -p $O
 ARGS=${ARGS:-"--steps 20 --warmup 0 --no-cpu-baseline --no-parity-line"}
 KEY=${KEY:-bf16/kvbf16/B32/P512}
