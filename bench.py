@@ -658,13 +658,14 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
             run_chunk(c)
             c += 1
             now = time.perf_counter()
-            if now - wt >= window_s or now - t0 >= seconds:
+            done = now - t0 >= seconds and (not reset_every or c % reset_every == 0)  # whole utterances
+            if now - wt >= window_s or done:
                 torch.cuda.synchronize()
                 now = time.perf_counter()
                 run_chunks.windows.append({"chunks": c - wc, "seconds": round(now - wt, 3),
                                            "tokens_per_s": round((c - wc) * S * chunk / (now - wt), 1)})
                 wc, wt = c, now
-                if now - t0 >= seconds and (not reset_every or c % reset_every == 0):
+                if done:
                     break
         K = c
     else:
