@@ -10,6 +10,11 @@ attention), a ``TextIteratorStreamer`` fed by ``generate`` on a worker thread, s
 ``config["llm_max_tokens"]`` new tokens, special tokens kept so the end-of-turn token reaches the
 router. Checkpoints are read from a local path (no network). The LLM is not part of the TTS hot
 path; it is the text source the reference's /tts endpoint streams into it.
+
+This module is a behavioural restatement of the reference's Hugging Face glue, not an algorithm:
+the chat-template / streamer / generation calls and their arguments are the ones the reference
+makes, because the routed words (and so the TTS byte stream) must be the reference's for the same
+checkpoint and seed.
 """
 from __future__ import annotations
 
