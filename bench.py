@@ -92,17 +92,20 @@ def attn_splits(B, wbytes):
     return ns
 
 
+KSPLIT = False  # library option "ksplit" (bench.py --opt ksplit=1)
+
+
 def kernel_bytes(which, B, t, wbytes, kvbytes):
     """Algorithmic HBM bytes of one launch of op `which` (weights streamed once + KV + the
-    activations it must read and write), as the batched path at this B moves them. At
-    9 <= B <= 32 with bf16 weights and KV, c_attn hands its output to the attention as four K-slice
-    partials (ar_qkv_ksplit_kernel: 4 x 2,304 fp32 per row written, read back by the attention,
-    which also appends the new key). Split-KV partials (8 heads x ns x (96 + 2) fp32 per row) are
+    activations it must read and write), as the batched path at this B moves them. With option
+    ksplit = 1 (off by default since round 3), at 9 <= B <= 32 with bf16 weights, c_attn hands its
+    output to the attention as four K-slice partials (ar_qkv_ksplit_kernel: 4 x 2,304 fp32 per row
+    written, read back by the attention, which also appends the new key). Split-KV partials (8 heads x ns x (96 + 2) fp32 per row) are
     charged only when the attention runs more than one split (attn_splits)."""
     D, F, V = 768, 3072, 4096
     act = 4 * B
     mfma = wbytes == 2 and 3 <= B <= 64
-    ksplit = mfma and kvbytes == 2 and 9 <= B <= 32
+    ksplit = KSPLIT and mfma and kvbytes <= 2 and 9 <= B <= 32
     ns = attn_splits(B, wbytes)
     parts = act * 8 * ns * 98 if ns > 1 else 0           # split-KV partials written / read once
     rows_bf16 = 2 * D * B                                  # one bf16 operand row set
@@ -719,8 +722,9 @@ def main():
                     help="KV position of the roofline probe (default: the run's mean position, steps * chunk / 2)")
     ap.add_argument("--codec-overlap", action="store_true",
                     help="run the codec on a second HIP stream beside the next chunk's AR (measured slower)")
-    ap.add_argument("--graph-stream", action="store_true",
-                    help="run on a non-default stream so the decode steps replay as HIP graphs")
+    ap.add_argument("--graph-stream", action="store_true", help="(default) kept for old command lines")
+    ap.add_argument("--null-stream", action="store_true",
+                    help="run on torch's default (null) stream: the decode steps are launched kernel by kernel")
     ap.add_argument("--no-graphs", action="store_true",
                     help="never replay graphs (steps and kernel probes launched kernel by kernel)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -784,16 +788,21 @@ def main():
                        codec_dtype=args.codec_dtype)
     dev = eng.device
     torch.cuda.set_device(dev)
+    global KSPLIT
     for kv in filter(None, args.opt.split(",")):
         k, v = kv.split("=")
         eng.set_option(k, int(v))
+        if k == "ksplit":
+            KSPLIT = int(v) != 0
     if args.no_graphs:
         eng.set_graphs(False)
-    if args.graph_stream:
+    if not args.null_stream:
         # decode steps replayed as HIP graphs need a non-default stream (the legacy null stream,
         # torch's default, cannot be captured; the library launches its steps one by one there).
-        # Measured no faster than the default in round 1 (configs[1] 13.04-13.06k vs 12.95-13.35k
-        # tok/s, configs[2] 210.9-211.9k vs 213.4k)
+        # Round 3, alternating A/B on one box (tools/gpu_graph_ab.sh): graphs equal or faster and
+        # steadier (configs[2] 224.6 / 224.7k vs 218.7 / 223.7k; configs[1] 12.8 / 13.0k vs 12.2 /
+        # 12.9k), and launched steps swing with host load (B = 8: 107-180 vs 99-104 us/step,
+        # tools/step_sweep.py): the host no longer paces the step.
         torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     if args.config == 3:
         return run_config3(args, eng, world, rank, local, dist)

@@ -147,15 +147,14 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
  *   "defer_select" 1: the greedy select is committed by the next step's first kernel (B <= 2: c_attn
  *                     layer 0 reduces lm_head's granules; B >= 4: ar_embed_select); 0: ar_argmax_kernel
  *                     after every lm_head (bit-identical results: tests/test_gpu_select.py);
- *   "fuse_mlp"     1: bf16, B <= 2: c_fc + gelu + mlp c_proj in one kernel (fp32 atomics in arrival
- *                     order); 0: the two deterministic GEMV kernels;
+ *   "fuse_mlp"     1: bf16, B <= 2: c_fc + gelu + mlp c_proj in one kernel (2^-32 fixed-point int64
+ *                     atomics: exact sums, reproducible run to run); 0: the two GEMV kernels;
  *   "bt"           1: batched path v3 for 32 < B <= 64; 2: v3 for every batched B; 0: never;
  *   "codec_g2"     1: large-M bf16 codec GEMMs on the 128 x 128 MFMA tile kernel; 0: the general one;
  *   "codec_skinny" 1: bf16 codec weight GEMMs with M <= 384 frames on the K-split-over-waves kernel
  *                     (no split-K combine); 0: the tile kernels;
- *   "exp"          development bits, 0 = production kernels; bit 1: at 9 <= B <= 32 (bf16) c_attn
- *                     as one launch with the KV append in its epilogue instead of K-slice partials
- *                     summed by the attention (bit-identical: tests/test_gpu_batched.py); bit 2: the
+ *   "exp"          development bits, 0 = production kernels; bit 1: the one-launch c_attn even with
+ *                     option ksplit = 1 (bit-identical: tests/test_gpu_batched.py); bit 2: the
  *                     batched MFMA GEMMs read the row-major weights instead of the fragment-packed
  *                     copy (bit-identical); bit 4: at 9 <= B <= 32 the bf16 operand rows (xn, xb,
  *                     hb) row-major instead of fragment-packed (bit-identical);
@@ -164,7 +163,12 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
  *   "persist"      1: bf16 weights + bf16 KV, 17 <= B <= 32: each decode step is ONE persistent dataflow
  *                     launch (ar_persist_kernel); 0 (default, measured faster): the 26 launches of the
  *                     batched path (bit-identical: tests/test_gpu_persist.py);
- *   "pexp"         persistent-step development bits (1: no KV-history prefetch). */
+ *   "pexp"         persistent-step development bits (1: no KV-history prefetch).
+ *   "ksplit"       (default 0) c_attn as four K-slice partials summed by the attention (9 <= B <= 32):
+ *                  bit-identical to the one-launch c_attn; faster only when steps are launched one
+ *                  by one (the null stream), slower under graph replay.
+ *   "ln_max"       (2..8, default 8) largest B whose batched GEMMs normalise in their own prologue;
+ *                  larger B run the rows kernel + K-split c_attn structure. */
 int lvx_set_option(lvx_ctx* ctx, const char* name, int value);
 /* Enable/disable HIP-graph replay of lvx_ar_step for a given B (default on). */
 int lvx_set_graphs(lvx_ctx* ctx, int enable);

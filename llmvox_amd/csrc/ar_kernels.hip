@@ -1080,12 +1080,12 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
   // block for long splits (batched steps)
   constexpr int TK = NW * 16;
   constexpr bool SLOT = sizeof(TKV) < 4;  // per-key-slot online softmax (bf16 / fp8 KV)
-  static_assert(!QKV || (sizeof(TKV) == 2 && (NW == 4 || NW == 8)), "the K-split c_attn path: bf16 keys, 4 or 8 waves");
+  static_assert(!QKV || (sizeof(TKV) <= 2 && (NW == 4 || NW == 8)), "the K-split c_attn path: bf16 / fp8 keys, 4 or 8 waves");
   constexpr int QH = QKV ? (3 * HD + NW * 64 - 1) / (NW * 64) : 1;  // q / k / v elements per thread (2 at 4 waves, 1 at 8)
   __shared__ float wm_s[NW], wl_s[NW];
   __shared__ float wo_s[NW][4][HD];  // [wave][16-lane row][part * 24 + i]
   __shared__ float qs_s[QKV ? HD : 1];
-  __shared__ __attribute__((aligned(16))) bf16_t kvh_s[QKV ? 2 : 1][HD];  // QKV: the new key's K, V
+  __shared__ __attribute__((aligned(16))) TKV kvh_s[QKV ? 2 : 1][sizeof(TKV) < 4 ? HD : 1];  // QKV: the new key's K, V
   const int sp = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   TS_DECL;
@@ -1211,10 +1211,11 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
 #pragma unroll
       for (int i = 0; i < 3; ++i) { kx[i] = kp[i]; vx[i] = vp[i]; }
       if (kb + TK >= k1 && min(kb + kq, k1 - 1) == t - 1) {
+        typedef decltype(kx[0].u) PieceT;  // uint4 (8 bf16) / uint2 (8 fp8)
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-          kx[i].u = reinterpret_cast<const uint4*>(kvh_s[0])[part * 3 + i];
-          vx[i].u = reinterpret_cast<const uint4*>(kvh_s[1])[part * 3 + i];
+          kx[i].u = reinterpret_cast<const PieceT*>(kvh_s[0])[part * 3 + i];
+          vx[i].u = reinterpret_cast<const PieceT*>(kvh_s[1])[part * 3 + i];
         }
       }
 #pragma unroll
@@ -1256,9 +1257,11 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
         qs_s[e] = v;
       } else if (e < 3 * HD && k1 == t) {  // K / V of the new key (the last split): appended, kept in LDS
         const int which = e / HD - 1, d = e % HD;
-        const bf16_t hv = f32_to_bf16(v);
+        TKV hv;  // the value the one-launch c_attn stores (store_kv)
+        if constexpr (sizeof(TKV) == 2) hv = f32_to_bf16(v);
+        else hv = f32_to_fp8(v);
         kvh_s[which][d] = hv;
-        reinterpret_cast<bf16_t*>(which ? st.vc : st.kc)[base + krow(ri.y) + d] = hv;
+        reinterpret_cast<TKV*>(which ? st.vc : st.kc)[base + krow(ri.y) + d] = hv;
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1409,7 +1412,9 @@ __device__ __forceinline__ uint2 pack4_bf16(float4 v) {
 constexpr int MFMA_BATCH_MIN = 3;  // smallest B on the batched MFMA path (measured B = 3: 117 vs 154 us, B = 2: 119 vs 114)
 // batched path: LayerNorm / embedding fused into the MFMA GEMM prologue for B <= this value
 // (measured: B = 8 147 vs 156 us/step; B = 32 slower, every block re-normalising 32 rows)
-constexpr int MFMA_LN_MAX = 8;
+// (runtime value: option "ln_max", for A/B of the two batched structures at small B)
+int g_mfma_ln_max = 8;
+#define MFMA_LN_MAX g_mfma_ln_max
 
 // ---------------------------------------------------------------------------------
 // Batched path v2 (bf16 weights, 4 < B <= 32): every per-row prologue runs ONCE per row into a
@@ -2314,7 +2319,9 @@ static int attn_ns_max(int B) {  // enough splits to fill the chip, no more (ear
 static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_t s, int ns_max = NSPLIT,
                         int direct = 0, int selcopy = 0, bool qkv = false) {
   dim3 grid(ns_max, N_HEAD, B);
-  if (qkv)  // c_attn left K-slice partials (qkv_ksplit): bf16 KV
+  if (qkv && kvdtype == LVX_DTYPE_FP8)  // c_attn left K-slice partials (qkv_ksplit)
+    hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t, 2, 4, true>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
+  else if (qkv)
     hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2, 4, true>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
   else if (kvdtype == LVX_DTYPE_BF16)
     hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2, 4>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
@@ -2388,11 +2395,18 @@ static bool fused_mlp(int B) {
 }
 
 // c_attn as K-slice partials summed by the attention: batched bf16 steps on the v2 kernels with the
-// rows kernel before c_attn (9 <= B <= 32), bf16 KV
+// rows kernel before c_attn (9 <= B <= 32), bf16 or fp8 KV. Option "ksplit", off by default since
+// round 3: with the steps replayed as HIP graphs (bench.py's default stream since round 3) the
+// one-launch c_attn is faster at every B and position measured (tools/step_sweep.py, graph replay,
+// us/step: B = 32 t = 0 / 384 / 768: 101.5 / 127.3 / 155.5 vs 103.8 / 130.5 / 160.6; B = 24 115.8 vs
+// 119.1; B = 16 110.8 vs 112.2; fp8 KV B = 12 / 16 / 32 103.6 / 105.4 / 110.1 vs 105.3 / 107.3 / 111.8);
+// launched one by one on the null stream it had measured faster (B = 16 123.4 vs 126.3, B = 32
+// 149.6 vs 154.3): the K split pays only against launch gaps. Bit-identical either way.
+int g_opt_ksplit = 0;
 template <typename TW>
 static bool qkv_ksplit(int B, int kvdtype) {
-  return use_mfma<TW>(B) && !use_bt<TW>(B) && B > MFMA_LN_MAX && B <= 32 && kvdtype == LVX_DTYPE_BF16 &&
-         !(g_opt_exp & 1);
+  return g_opt_ksplit && use_mfma<TW>(B) && !use_bt<TW>(B) && B > MFMA_LN_MAX && B <= 32 &&
+         (kvdtype == LVX_DTYPE_BF16 || kvdtype == LVX_DTYPE_FP8) && !(g_opt_exp & 1);
 }
 static void launch_qkv_ksplit(const GemvArgs& a, hipStream_t s) {
   if (a.B <= 16) hipLaunchKernelGGL(ar_qkv_ksplit_kernel<1>, dim3(36, 4), dim3(256), 0, s, a);

@@ -617,6 +617,8 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   else if (n == "f32b") g_opt_f32b = value != 0;
   else if (n == "persist") g_opt_persist = value != 0;
   else if (n == "pexp") g_opt_pexp = value;
+  else if (n == "ksplit") g_opt_ksplit = value != 0;
+  else if (n == "ln_max") g_mfma_ln_max = std::min(std::max(value, 2), 8);
   else return fail(LVX_E_NAME, "unknown option " + n);
   g_opt_epoch.fetch_add(1);  // every context's captured kernels change (checked in cached_graph)
   return LVX_OK;

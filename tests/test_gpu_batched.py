@@ -132,25 +132,47 @@ def test_v3_path_agrees_with_v2(eng, B):
     assert np.abs(got - ref).max() < 0.02 * np.abs(ref).max()
 
 
-@pytest.mark.parametrize("B", [9, 16, 17, 32])
-def test_qkv_ksplit_matches_one_launch_cattn(B):
-    """9 <= B <= 32 (bf16): c_attn runs as K-slice partials summed by the attention, which also
-    appends the new key (ar_qkv_ksplit_kernel); option exp bit 1 restores the one-launch c_attn with
-    the KV append in its epilogue. Same K-slice order: tokens, margins and logits bit for bit, with
-    permuted slots and ragged positions."""
+@pytest.mark.parametrize("B,kv", [(9, "bf16"), (16, "bf16"), (17, "bf16"), (32, "bf16"), (12, "fp8"), (32, "fp8")])
+def test_qkv_ksplit_matches_one_launch_cattn(B, kv):
+    """9 <= B <= 32 (bf16 or fp8 KV): c_attn runs as K-slice partials summed by the attention, which
+    also appends the new key in the cache's dtype (ar_qkv_ksplit_kernel, option ksplit = 1) against
+    the one-launch c_attn with the KV append in its epilogue (the default). Same K-slice order and the
+    same conversion: tokens, margins and logits bit for bit, with permuted slots and ragged positions."""
     from llmvox_amd.engine import build_engine
-    e = build_engine(0, "bf16", "bf16", max_streams=64, max_positions=512, max_codec_frames=256)
+    e = build_engine(0, "bf16", kv, max_streams=64, max_positions=512, max_codec_frames=256)
     try:
         texts = _texts(B, 96, seed=11)
         order = list(np.random.default_rng(B).permutation(B))
         prefix = set(range(0, B, 3))
         res = []
-        for exp in (0, 1):
-            e.set_option("exp", exp)
+        for ks in (1, 0):
+            e.set_option("ksplit", ks)
             res.append(_run(e, order, texts, prefix, 40, 56))
-        e.set_option("exp", 0)
         np.testing.assert_array_equal(res[0][0], res[1][0])
         np.testing.assert_array_equal(res[0][1], res[1][1])
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("B,kv", [(8, "bf16"), (8, "fp8"), (6, "bf16")])
+def test_rows_structure_at_small_b(B, kv):
+    """Option ln_max below B runs a small batch on the rows-kernel structure (rows kernel + K-split
+    c_attn + 16-row-tile GEMMs) instead of the GEMMs that normalise in their own prologue: another
+    summation order, so the logits agree to bf16 rounding and the tokens where the margin allows."""
+    from llmvox_amd.engine import build_engine
+    e = build_engine(0, "bf16", kv, max_streams=64, max_positions=512, max_codec_frames=256)
+    try:
+        e.set_option("fuse_mlp", 0)
+        texts = _texts(B, 64, seed=21)
+        order = list(np.random.default_rng(B + 7).permutation(B))
+        res = []
+        for lm in (8, 4):
+            e.set_option("ln_max", lm)
+            res.append(_run(e, order, texts, set(range(0, B, 3)), 16, 1))
+        e.set_option("ln_max", 8)
+        e.set_option("fuse_mlp", 1)
+        ref, got = res[0][1], res[1][1]
+        assert np.abs(got - ref).max() < 0.02 * np.abs(ref).max()
     finally:
         e.close()
 
