@@ -153,6 +153,9 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
  *   "codec_g2"     1: large-M bf16 codec GEMMs on the 128 x 128 MFMA tile kernel; 0: the general one;
  *   "codec_skinny" 1: bf16 codec weight GEMMs with M <= 384 frames on the K-split-over-waves kernel
  *                     (no split-K combine); 0: the tile kernels;
+ *   "codec_exp"    codec development bits, 0 = production kernels; bit 0: the general GroupNorm
+ *                     kernel at every L (same bits); bits 1-2: dwconv+AdaLN frames per block at
+ *                     >= 2,048 frames (0: 16, 1: 8, 2: 32, 3: 4; same bits);
  *   "exp"          development bits, 0 = production kernels; bit 1: the one-launch c_attn even with
  *                     option ksplit = 1 (bit-identical: tests/test_gpu_batched.py); bit 2: the
  *                     batched MFMA GEMMs read the row-major weights instead of the fragment-packed

@@ -622,7 +622,7 @@ __global__ __launch_bounds__(256, BMt == 128 ? 2 : 1) void gemm_bf16_kernel(Gemm
         const float v = acc[i][j][r] + bias;
         float o;
         if constexpr (EPI == E_BIAS) o = v;
-        else if constexpr (EPI == E_BIAS_GELU) o = gelu_erf(v);
+        else if constexpr (EPI == E_BIAS_GELU) o = sizeof(TC) == 2 ? gelu_erf_bf16out(v) : gelu_erf(v);
         else if constexpr (EPI == E_BIAS_GAMMA_RES) o = rv[r] + gam * v;
         else if constexpr (EPI == E_BIAS_RES) o = rv[r] + v;
         else o = acc[i][j][r] * g.alpha;
@@ -793,47 +793,99 @@ __global__ __launch_bounds__(512, NS == 2 ? 2 : 1) void gemm_glds_kernel(GemmArg
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 3; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[kk][j], acc[i][j], 0, 0, 0);
+          // weights as the MFMA's A operand: the accumulator is the transposed tile, so each lane
+          // holds 4 consecutive output columns of one row (same products, same k order: same bits)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[kk][j], fa[kk][i], acc[i][j], 0, 0, 0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail DMAs
-  // epilogue: acc[i][j][e] = C[m0 + wm*64 + i*16 + 4*(lane >> 4) + e][n0 + wn*48 + j*16 + (lane & 15)];
-  // every operand in flight at once (one round trip; rows / columns clamped, no branch)
+  // epilogue: acc[i][j][e] = C[m0 + wm*64 + i*16 + (lane & 15)][n0 + wn*48 + j*16 + 4*(lane >> 4) + e]:
+  // bias / gamma / residual as 16-B loads and the outputs as one 16-B (fp32) or 8-B (bf16) store per
+  // (i, j), 4x fewer memory instructions than one element per lane; every operand in flight at once
+  // (one round trip; rows / columns clamped, no branch). N % 4 != 0 (the head's 1,282 columns) takes
+  // the per-element form.
   TC* C = reinterpret_cast<TC*>(g.C);
-  float bias[3], gam[3], rv[3][4][4];
+  constexpr bool RES = EPI == E_BIAS_GAMMA_RES || EPI == E_BIAS_RES;
+  const int cq = 4 * (lane >> 4);
+  if ((g.N & 3) == 0 && (g.ldc & 3) == 0 && (!RES || (g.ldr & 3) == 0)) {
+    f32x4v bias[3], gam[3], rv[3][4];
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int colc = min(n0 + wn * 48 + j * 16 + (lane & 15), g.N - 1);
-    bias[j] = g.bias ? g.bias[colc] : 0.f;
-    gam[j] = (EPI == E_BIAS_GAMMA_RES) ? g.gamma[colc] : 0.f;
-    if constexpr (EPI == E_BIAS_GAMMA_RES || EPI == E_BIAS_RES) {
+    for (int j = 0; j < 3; ++j) {
+      const int c4 = min(n0 + wn * 48 + j * 16 + cq, g.N - 4);
+      bias[j] = g.bias ? *reinterpret_cast<const f32x4v*>(g.bias + c4) : f32x4v{0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI == E_BIAS_GAMMA_RES) gam[j] = *reinterpret_cast<const f32x4v*>(g.gamma + c4);
+      if constexpr (RES) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          rv[j][i][e] = g.res[(size_t)min(m0 + wm * 64 + i * 16 + 4 * (lane >> 4) + e, g.M - 1) * g.ldr + colc];
+        for (int i = 0; i < 4; ++i)
+          rv[j][i] = *reinterpret_cast<const f32x4v*>(g.res + (size_t)min(m0 + wm * 64 + i * 16 + frow, g.M - 1) * g.ldr + c4);
+      }
     }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int col = n0 + wn * 48 + j * 16 + cq;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = acc[i][j][e] + bias[j][e];
+          float o;
+          if constexpr (EPI == E_BIAS) o = v;
+          else if constexpr (EPI == E_BIAS_GELU) o = sizeof(TC) == 2 ? gelu_erf_bf16out(v) : gelu_erf(v);
+          else if constexpr (EPI == E_BIAS_GAMMA_RES) o = rv[j][i][e] + gam[j][e] * v;
+          else o = rv[j][i][e] + v;
+          acc[i][j][e] = o;
+        }
+        asm volatile("" : "+v"(acc[i][j]));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wm * 64 + i * 16 + frow;
+        if (col < g.N && row < g.M) {
+          TC* p = C + (size_t)row * g.ldc + col;
+          if constexpr (sizeof(TC) == 2) {
+            *reinterpret_cast<uint2*>(p) =
+                make_uint2((uint32_t)f32_to_bf16(acc[i][j][0]) | ((uint32_t)f32_to_bf16(acc[i][j][1]) << 16),
+                           (uint32_t)f32_to_bf16(acc[i][j][2]) | ((uint32_t)f32_to_bf16(acc[i][j][3]) << 16));
+          } else {
+            *reinterpret_cast<f32x4v*>(p) = acc[i][j];
+          }
+        }
+      }
+    }
+    return;
   }
+  float bias[3][4], gam[3][4], rv[3][4][4];
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int colc = min(n0 + wn * 48 + j * 16 + cq + e, g.N - 1);
+      bias[j][e] = g.bias ? g.bias[colc] : 0.f;
+      gam[j][e] = (EPI == E_BIAS_GAMMA_RES) ? g.gamma[colc] : 0.f;
+      if constexpr (RES) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rv[j][i][e] = g.res[(size_t)min(m0 + wm * 64 + i * 16 + frow, g.M - 1) * g.ldr + colc];
+      }
+    }
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    const int col = n0 + wn * 48 + j * 16 + (lane & 15);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int row0 = m0 + wm * 64 + i * 16 + 4 * (lane >> 4);
+      const int row = m0 + wm * 64 + i * 16 + frow;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float v = acc[i][j][e] + bias[j];
+        const float v = acc[i][j][e] + bias[j][e];
         float o;
         if constexpr (EPI == E_BIAS) o = v;
-        else if constexpr (EPI == E_BIAS_GELU) o = gelu_erf(v);
-        else if constexpr (EPI == E_BIAS_GAMMA_RES) o = rv[j][i][e] + gam[j] * v;
+        else if constexpr (EPI == E_BIAS_GELU) o = sizeof(TC) == 2 ? gelu_erf_bf16out(v) : gelu_erf(v);
+        else if constexpr (EPI == E_BIAS_GAMMA_RES) o = rv[j][i][e] + gam[j][e] * v;
         else o = rv[j][i][e] + v;
         acc[i][j][e] = o;
-        asm volatile("" : "+v"(acc[i][j][e]));
       }
-      if (col < g.N) {
+      asm volatile("" : "+v"(acc[i][j]));
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (row0 + e < g.M) store_out<TC>(C + (size_t)(row0 + e) * g.ldc + col, acc[i][j][e]);
+      for (int e = 0; e < 4; ++e) {
+        const int col = n0 + wn * 48 + j * 16 + cq + e;
+        if (col < g.N && row < g.M) store_out<TC>(C + (size_t)row * g.ldc + col, acc[i][j][e]);
       }
     }
   }
@@ -1106,6 +1158,55 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const float* __restrict__
   }
 }
 
+// gn_apply for L * 6 <= 2,048 (L <= 341: every chunk decode): the group in one round of 8 loads per
+// thread, issued before the affine operands (gn_apply_kernel waited for those at its loop head: one
+// more round trip ahead of the data), values kept in registers (no LDS copy: 4 blocks per CU). Same
+// sums in the same order as gn_apply_kernel: same bits.
+template <bool SWISH, typename TO>
+__global__ __launch_bounds__(256) void gn_apply1_kernel(const float* __restrict__ x, int L, const float* __restrict__ gw,
+                                                        const float* __restrict__ gb, TO* __restrict__ y) {
+  __shared__ float red[4];
+  const int gi = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  constexpr int CG = CD / GN_G;
+  const size_t off = (size_t)b * L * CD + gi * CG;
+  const int q0 = tid % 6, q1 = (q0 + 4) % 6, q2 = (q0 + 2) % 6;
+  const float4* gw4 = reinterpret_cast<const float4*>(gw + gi * CG);
+  const float4* gb4 = reinterpret_cast<const float4*>(gb + gi * CG);
+  const int n4 = L * 6;
+  float4 v[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) v[u] = gn_ld(x + off, min(tid + u * 256, n4 - 1));
+  const float4 wq0 = gw4[q0], wq1 = gw4[q1], wq2 = gw4[q2], bq0 = gb4[q0], bq1 = gb4[q1], bq2 = gb4[q2];
+  __builtin_amdgcn_sched_barrier(0);
+  float s = 0.f;
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (tid + u * 256 < n4) s += sum4(v[u]);
+  const float mean = block_sum<256>(s, red) / (float)(L * 24);
+  float q = 0.f;
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (tid + u * 256 < n4) q += sqd4(v[u], mean);
+  const float rstd = 1.0f / sqrtf(block_sum<256>(q, red) / (float)(L * 24) + 1e-6f);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = tid + u * 256;
+    if (e >= n4) break;
+    const int t = e / 6, qq = e - t * 6, ph = u % 3;  // chunk (tid + 4 u) mod 6
+    const float4 w = ph == 0 ? wq0 : ph == 1 ? wq1 : wq2, bb = ph == 0 ? bq0 : ph == 1 ? bq1 : bq2;
+    float4 o = make_float4((v[u].x - mean) * rstd * w.x + bb.x, (v[u].y - mean) * rstd * w.y + bb.y,
+                           (v[u].z - mean) * rstd * w.z + bb.z, (v[u].w - mean) * rstd * w.w + bb.w);
+    if (SWISH) o = make_float4(swishf(o.x), swishf(o.y), swishf(o.z), swishf(o.w));
+    store4(y + off + (size_t)t * CD + qq * 4, o);
+  }
+}
+int g_opt_codec_exp = 0;  // codec A/B bits (development): 1 the general gn_apply at every L; 6: dwconv FT (0: 16, 2: 8, 4: 32, 6: 4)
+template <bool SWISH, typename TO>
+static void gn_apply_launch(const float* x, int B, int L, const float* gw, const float* gb, TO* y, hipStream_t s) {
+  if (L * 6 <= 8 * 256 && !(g_opt_codec_exp & 1)) hipLaunchKernelGGL((gn_apply1_kernel<SWISH, TO>), dim3(GN_G, B), dim3(256), 0, s, x, L, gw, gb, y);
+  else hipLaunchKernelGGL((gn_apply_kernel<SWISH, TO>), dim3(GN_G, B), dim3(256), 0, s, x, L, gw, gb, y);
+}
+
 // ---------------------------------------------------------------------------------
 // GroupNorm statistics (decoder/models.py:15-16: 32 groups, eps 1e-6): per (stream, group)
 // mean and 1/sqrt(var + eps) over L frames x 24 channels, two-pass fp32.
@@ -1178,27 +1279,38 @@ __global__ __launch_bounds__(256) void dwconv_adaln_tile_kernel(const float* __r
   __shared__ float red[2][4][FT];
   const int b = blockIdx.y, t0 = blockIdx.x * FT, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   float v[3][FT], sc[3], sh[3];
+  // every load of the block issued before the first use, the small operands first (the compiler had
+  // interleaved the three channel passes: three dependent round trips ahead of the main 66 loads);
+  // the sched_barrier keeps the FMAs behind them
+  float w[3][7], xs[3][FT + 6], bb[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int c = tid + 256 * j;
-    float w[7], xs[FT + 6];
 #pragma unroll
-    for (int k = 0; k < 7; ++k) w[k] = dwt[k * CD + c];
-#pragma unroll
-    for (int i = 0; i < FT + 6; ++i) xs[i] = x[((size_t)b * L + min(max(t0 + i - 3, 0), L - 1)) * CD + c];
-    const float bb = dwb[c];
+    for (int k = 0; k < 7; ++k) w[j][k] = dwt[k * CD + c];
+    bb[j] = dwb[c];
     sc[j] = scale[c];
     sh[j] = shift[c];
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int c = tid + 256 * j;
+#pragma unroll
+    for (int i = 0; i < FT + 6; ++i) xs[j][i] = x[((size_t)b * L + min(max(t0 + i - 3, 0), L - 1)) * CD + c];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
 #pragma unroll
     for (int f = 0; f < FT; ++f) {
       float a = 0.f;
 #pragma unroll
       for (int k = 0; k < 7; ++k) {
         const int tt = t0 + f + k - 3;
-        const float na = a + w[k] * xs[f + k];
+        const float na = a + w[j][k] * xs[j][f + k];
         a = (tt >= 0 && tt < L) ? na : a;
       }
-      v[j][f] = a + bb;
+      v[j][f] = a + bb[j];
     }
   }
   // AdaLayerNorm (modules.py:81-86) per frame: block_sum's order (wave DPP sum, then waves 0..3)
@@ -1351,19 +1463,37 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 
-template <int R>
+// One radix-R Stockham pass over the 640-point transform in LDS. The twiddles a thread needs
+// (e^{+2 pi i k r / (Ns R)} = tw[2 (640 / (Ns R)) k r], for its j = tid + 256 it) are loaded into
+// registers by stockham_tw at the top of the kernel, with the spectrum: the passes then run on LDS
+// alone (a twiddle load inside each pass had been one L2 round trip per pass).
+template <int R, int NJ>
+struct StockTw {
+  float2 t[NJ][R - 1];
+};
+template <int R, int NJ>
+__device__ __forceinline__ void stockham_tw(int Ns, const float2* __restrict__ tw, StockTw<R, NJ>& w) {
+  const int step = FM / (Ns * R);
+#pragma unroll
+  for (int it = 0; it < NJ; ++it) {
+    const int j = min((int)threadIdx.x + 256 * it, FM / R - 1), k = j % Ns;
+#pragma unroll
+    for (int r = 1; r < R; ++r) w.t[it][r - 1] = tw[(2 * step * k * r) % (2 * FM)];
+  }
+}
+template <int R, int NJ>
 __device__ __forceinline__ void stockham_pass(const float2* __restrict__ src, float2* __restrict__ dst, int Ns,
-                                              const float2* __restrict__ tw) {
-  // twiddle for e^{+2 pi i k r / (Ns R)} over the 640-point transform = tw[2 * (640/(Ns R)) * k * r]
-  for (int j = threadIdx.x; j < FM / R; j += blockDim.x) {
+                                              const StockTw<R, NJ>& w, const float2 (&c5)[5]) {
+#pragma unroll
+  for (int it = 0; it < NJ; ++it) {
+    const int j = threadIdx.x + 256 * it;
+    if (j >= FM / R) break;
     const int k = j % Ns;
-    const int step = FM / (Ns * R);
     float2 v[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const float2 x = src[j + r * (FM / R)];
-      const int ti = (2 * step * k * r) % (2 * FM);
-      v[r] = (r == 0) ? x : cmul(x, tw[ti]);
+      v[r] = (r == 0) ? x : cmul(x, w.t[it][r - 1]);
     }
     float2 y[R];
     if constexpr (R == 2) {
@@ -1379,13 +1509,13 @@ __device__ __forceinline__ void stockham_pass(const float2* __restrict__ src, fl
       y[2] = make_float2(a0.x - a2.x, a0.y - a2.y);
       y[1] = make_float2(a1.x + a3.x, a1.y + a3.y);
       y[3] = make_float2(a1.x - a3.x, a1.y - a3.y);
-    } else {  // R == 5: direct 5-point DFT with e^{+2 pi i rq/5} = tw[256 * ((r q) mod 5)]
+    } else {  // R == 5: direct 5-point DFT with e^{+2 pi i rq/5} = tw[256 * ((r q) mod 5)] = c5[(r q) mod 5]
 #pragma unroll
       for (int q = 0; q < R; ++q) {
         float2 accv = v[0];
 #pragma unroll
         for (int r = 1; r < R; ++r) {
-          const float2 c = cmul(v[r], tw[256 * ((r * q) % 5)]);
+          const float2 c = cmul(v[r], c5[(r * q) % 5]);
           accv.x += c.x;
           accv.y += c.y;
         }
@@ -1405,34 +1535,71 @@ __global__ __launch_bounds__(256) void istft_frames_kernel(const float* __restri
   __shared__ float2 X[NB];
   const int f = blockIdx.x, tid = threadIdx.x;
   const float* row = spec + (size_t)f * (2 * NB);
-  for (int k = tid; k < NB; k += 256) {
-    const float mag = fminf(expf(row[k]), 100.0f);
-    const float ph = row[NB + k];
-    float2 x = make_float2(mag * cosf(ph), mag * sinf(ph));
-    if (k == 0 || k == NB - 1) x.y = 0.f;  // C2R ignores imag of DC and Nyquist
-    X[k] = x;
+  // every global load of the block first (clamped indices, no load under a branch): the frame's
+  // magnitudes / phases, the twiddles of the Z step and of each pass, the window
+  float lm[3], lp[3];
+  float2 tz[3], wv[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int k = min(tid + 256 * u, NB - 1);
+    lm[u] = row[k];
+    lp[u] = row[NB + k];
+  }
+#pragma unroll
+  for (int u = 0; u < 3; ++u) tz[u] = tw[min(tid + 256 * u, FM - 1)];
+  StockTw<4, 1> w1, w2, w3;
+  StockTw<2, 2> w4;
+  StockTw<5, 1> w5;
+  stockham_tw(1, tw, w1);
+  stockham_tw(4, tw, w2);
+  stockham_tw(16, tw, w3);
+  stockham_tw(64, tw, w4);
+  stockham_tw(128, tw, w5);
+  float2 c5[5];
+#pragma unroll
+  for (int m = 0; m < 5; ++m) c5[m] = tw[256 * m];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) wv[u] = reinterpret_cast<const float2*>(window)[min(tid + 256 * u, FM - 1)];
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int k = tid + 256 * u;
+    if (k < NB) {
+      const float mag = fminf(expf(lm[u]), 100.0f);
+      const float ph = lp[u];
+      float2 x = make_float2(mag * cosf(ph), mag * sinf(ph));
+      if (k == 0 || k == NB - 1) x.y = 0.f;  // C2R ignores imag of DC and Nyquist
+      X[k] = x;
+    }
   }
   __syncthreads();
   // Z[k] = Xe[k] + i Xo[k];  Xe = (X[k] + conj X[M-k]) / 2,  Xo = (X[k] - conj X[M-k]) e^{+2 pi i k/N} / 2
-  for (int k = tid; k < FM; k += 256) {
-    const float2 a = X[k];
-    const float2 bc = make_float2(X[FM - k].x, -X[FM - k].y);
-    const float2 xe = make_float2(0.5f * (a.x + bc.x), 0.5f * (a.y + bc.y));
-    const float2 xo = cmul(make_float2(0.5f * (a.x - bc.x), 0.5f * (a.y - bc.y)), tw[k]);
-    bufA[k] = make_float2(xe.x - xo.y, xe.y + xo.x);
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int k = tid + 256 * u;
+    if (k < FM) {
+      const float2 a = X[k];
+      const float2 bc = make_float2(X[FM - k].x, -X[FM - k].y);
+      const float2 xe = make_float2(0.5f * (a.x + bc.x), 0.5f * (a.y + bc.y));
+      const float2 xo = cmul(make_float2(0.5f * (a.x - bc.x), 0.5f * (a.y - bc.y)), tz[u]);
+      bufA[k] = make_float2(xe.x - xo.y, xe.y + xo.x);
+    }
   }
   __syncthreads();
-  stockham_pass<4>(bufA, bufB, 1, tw);
-  stockham_pass<4>(bufB, bufA, 4, tw);
-  stockham_pass<4>(bufA, bufB, 16, tw);
-  stockham_pass<2>(bufB, bufA, 64, tw);
-  stockham_pass<5>(bufA, bufB, 128, tw);
+  stockham_pass(bufA, bufB, 1, w1, c5);
+  stockham_pass(bufB, bufA, 4, w2, c5);
+  stockham_pass(bufA, bufB, 16, w3, c5);
+  stockham_pass(bufB, bufA, 64, w4, c5);
+  stockham_pass(bufA, bufB, 128, w5, c5);
   float* out = frames + (size_t)f * NFFT;
   const float sc = 1.0f / FM;
-  for (int m = tid; m < FM; m += 256) {
-    const float2 zz = bufB[m];
-    out[2 * m] = zz.x * sc * window[2 * m];
-    out[2 * m + 1] = zz.y * sc * window[2 * m + 1];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int m = tid + 256 * u;
+    if (m < FM) {
+      const float2 zz = bufB[m];
+      reinterpret_cast<float2*>(out)[m] = make_float2(zz.x * sc * wv[u].x, zz.y * sc * wv[u].y);
+    }
   }
 }
 
@@ -1496,21 +1663,21 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
   gemm_w<TW, TAct, A_CONV, E_BIAS>(g, s);
 
   auto resnet = [&](int i) {  // models.py:58-78
-    hipLaunchKernelGGL((gn_apply_kernel<true, TAct>), dim3(GN_G, B), dim3(256), 0, s, x, L, w.rn_n1w[i], w.rn_n1b[i], gn);
+    gn_apply_launch<true, TAct>(x, B, L, w.rn_n1w[i], w.rn_n1b[i], gn, s);
     GemmArgs c{};
     c.ws = sc.ws;
     c.L = L; c.M = M; c.cin = CD; c.taps = 3; c.K = 3 * CD; c.N = CD; c.ldw = 3 * CD;
     c.A = gn; c.lda = CD;
     c.W = w.rn_c1w[i]; c.wscale = w.rn_c1s[i]; c.bias = w.rn_c1b[i]; c.C = t1; c.ldc = CD;
     gemm_w<TW, TAct, A_CONV, E_BIAS>(c, s);
-    hipLaunchKernelGGL((gn_apply_kernel<true, TAct>), dim3(GN_G, B), dim3(256), 0, s, t1, L, w.rn_n2w[i], w.rn_n2b[i], gn);
+    gn_apply_launch<true, TAct>(t1, B, L, w.rn_n2w[i], w.rn_n2b[i], gn, s);
     c.W = w.rn_c2w[i]; c.wscale = w.rn_c2s[i]; c.bias = w.rn_c2b[i]; c.C = x; c.res = x; c.ldr = CD;
     gemm_w<TW, TAct, A_CONV, E_BIAS_RES>(c, s);
   };
   resnet(0);
   resnet(1);
   {  // AttnBlock (models.py:107-127)
-    hipLaunchKernelGGL((gn_apply_kernel<false, TAct>), dim3(GN_G, B), dim3(256), 0, s, x, L, w.at_nw, w.at_nb, gn);
+    gn_apply_launch<false, TAct>(x, B, L, w.at_nw, w.at_nb, gn, s);
     GemmArgs c{};
     c.ws = sc.ws;
     c.L = L; c.M = M; c.K = CD; c.N = 3 * CD; c.ldw = CD;
@@ -1558,7 +1725,14 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
   hipLaunchKernelGGL(gn_adaln_kernel, dim3(M), dim3(256), 0, s, x, L, sc.stats, w.pn_w, w.pn_b,
                      w.ada_scale + (size_t)bw * CD, w.ada_shift + (size_t)bw * CD, x);
   for (int i = 0; i < 12; ++i) {  // ConvNeXt blocks (modules.py:43-60)
-    if (M >= 2048)
+    const int dwft = (g_opt_codec_exp >> 1) & 3;
+    if (M >= 2048 && dwft == 1)
+      hipLaunchKernelGGL((dwconv_adaln_tile_kernel<TAct, 8>), dim3((L + 7) / 8, B), dim3(256), 0, s, x, L, w.dw_w[i],
+                         w.dw_b[i], w.cn_scale[i] + (size_t)bw * CD, w.cn_shift[i] + (size_t)bw * CD, t2a);
+    else if (M >= 2048 && dwft == 2)
+      hipLaunchKernelGGL((dwconv_adaln_tile_kernel<TAct, 32>), dim3((L + 31) / 32, B), dim3(256), 0, s, x, L, w.dw_w[i],
+                         w.dw_b[i], w.cn_scale[i] + (size_t)bw * CD, w.cn_shift[i] + (size_t)bw * CD, t2a);
+    else if (M >= 2048 && dwft == 0)
       hipLaunchKernelGGL((dwconv_adaln_tile_kernel<TAct, 16>), dim3((L + 15) / 16, B), dim3(256), 0, s, x, L, w.dw_w[i],
                          w.dw_b[i], w.cn_scale[i] + (size_t)bw * CD, w.cn_shift[i] + (size_t)bw * CD, t2a);
     else

@@ -120,6 +120,20 @@ __device__ __forceinline__ float gelu_tanh(float x) {  // src/model.py:21-26
 __device__ __forceinline__ float gelu_erf(float x) {  // nn.GELU() default
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
 }
+// GELU (erf form) for outputs stored in bf16 (2^-9 relative rounding): erfc from Abramowitz & Stegun
+// 7.1.26 (|error| <= 1.5e-7 absolute), branch-free on the native v_rcp_f32 / v_exp_f32, about a third
+// of erff's instructions. x >= 0: x (1 - erfc(z) / 2); x < 0: x erfc(z) / 2 (no cancellation in the
+// negative tail); z = |x| / sqrt(2).
+__device__ __forceinline__ float gelu_erf_bf16out(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float h = 0.5f * (p * t) * __builtin_amdgcn_exp2f(-(z * z) * 1.4426950408889634f);
+  return x * (x >= 0.f ? 1.0f - h : h);
+}
 __device__ __forceinline__ float swishf(float x) { return x / (1.0f + expf(-x)); }
 
 #define LVX_CHECK_LAUNCH() (void)0
