@@ -155,12 +155,13 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
  *                     (no split-K combine); 0: the tile kernels;
  *   "codec_exp"    codec development bits, 0 = production kernels; bit 0: the general GroupNorm
  *                     kernel at every L (same bits); bits 1-2: dwconv+AdaLN frames per block at
- *                     >= 2,048 frames (0: 16, 1: 8, 2: 32, 3: 4; same bits);
+ *                     >= 2,048 frames (0: 4, 1: 16, 2: 32, 3: 8; same bits);
  *   "exp"          development bits, 0 = production kernels; bit 1: the one-launch c_attn even with
  *                     option ksplit = 1 (bit-identical: tests/test_gpu_batched.py); bit 2: the
  *                     batched MFMA GEMMs read the row-major weights instead of the fragment-packed
  *                     copy (bit-identical); bit 4: at 9 <= B <= 32 the bf16 operand rows (xn, xb,
- *                     hb) row-major instead of fragment-packed (bit-identical);
+ *                     hb) row-major instead of fragment-packed (bit-identical); bit 8: fp32 batched
+ *                     c_proj / mlp c_proj in 32-row instead of 16-row batch tiles (bit-identical);
  *   "f32b"         1: fp32 weights, 3 <= B <= 64: batched steps on exact-fp32 MFMA (ar_f32b_kernel);
  *                     0: the fp32 GEMV family (same ids against the reference: tests/test_gpu_f32b.py);
  *   "persist"      1: bf16 weights + bf16 KV, 17 <= B <= 32: each decode step is ONE persistent dataflow

@@ -1121,6 +1121,8 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
   const int s = ri.x;
   if (s < 0) {
     copy_tail();
+    // an idle row's fp32 operand is 0, as the merge would give it
+    if (direct == 3 && sp == 0 && tid < HD) st.part_o[(size_t)(b * N_HEAD + head) * NSPLIT * HD + tid] = 0.f;
     return;
   }
   const int t = ri.y + 1;
@@ -1320,6 +1322,10 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
       const float f = (wm_s[w] == -INFINITY) ? 0.f : expf(wm_s[w] - M);
       ov += f * ((wo_s[w][0][tid] + wo_s[w][1][tid]) + (wo_s[w][2][tid] + wo_s[w][3][tid]));
       lv += f * wl_s[w];
+    }
+    if (direct == 3) {  // fp32 parity mode, one split: the normalised head output in split 0's slot
+      st.part_o[(size_t)(b * N_HEAD + head) * NSPLIT * HD + tid] = ov * (1.0f / lv);
+      return;
     }
     if (direct) {
       st.xn[direct == 2 ? xfrag(b, head * HD + tid, D) : (size_t)b * D + head * HD + tid] = f32_to_bf16(ov * (1.0f / lv));
@@ -2131,6 +2137,7 @@ template <int K, int NT, int IN, int OUT>
 __global__ __launch_bounds__(K / 192 * 64) void ar_f32b_kernel(GemvArgs a) {
   constexpr int NW = K / 192, R = NT * 16, NTH = NW * 64;
   constexpr bool STAGE = IN != 1;  // K == 768: the operand tile in LDS
+  // IN 4 (c_proj after a one-split attention, direct == 3): the normalised rows are split 0 of part_o
   static_assert(!STAGE || K == 768, "the LDS operand tile holds K = 768 rows");
   constexpr int LDX = D + 4;  // fp32 row stride: 16 rows x 4 banks apart, conflict-free 16-B reads
   __shared__ __attribute__((aligned(16))) float xs[STAGE ? R * LDX : 4];
@@ -2143,7 +2150,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_f32b_kernel(GemvArgs a) {
   // first row inputs for the LayerNorm modes (their statistics then overlap the weight stream)
   const float4* wsrc = reinterpret_cast<const float4*>(a.Wf) + ((size_t)(n0 >> 4) * (K / 16) + wave * 12) * 64 + lane;
   float4 wf[12];
-  if constexpr (IN == 1 || IN == 2) {
+  if constexpr (IN == 1 || IN == 2 || IN == 4) {
 #pragma unroll
     for (int j = 0; j < 12; ++j) wf[j] = wsrc[j * 64];
     // all 12 in flight before anything else (left to itself the scheduler interleaved each load with
@@ -2192,14 +2199,16 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_f32b_kernel(GemvArgs a) {
     }
   } else if constexpr (IN == 2) {
     // split-KV merge (as gemv_stage_input IN 2): coefficients per (row, head, split), then every
-    // element sums all NSPLIT partials (part_o is zeroed at allocation: unused splits are finite)
+    // element sums the partials of the nsm splits the attention ran at this B (attn_ns_max). The
+    // splits past nsm have coefficient 0 (part_o is zeroed at allocation, finite): leaving them out
+    // of the sum changes no bit, and at B = 32 (one split) it cuts the block's partial reads 16-fold
+    int nsm = NSPLIT;
+    while (nsm > 1 && nsm * N_HEAD * B > 256) nsm >>= 1;
     for (int q = tid; q < R * N_HEAD; q += NTH) {
       const int bb = q / N_HEAD, head = q - bb * N_HEAD, b = min(r0 + bb, B - 1);
       const int4 ri = a.st.rowinfo[b];
       float* cf = cf_s + q * NSPLIT;
       const int t = ri.y + 1;
-      int nsm = NSPLIT;  // the attention's split count at this B (attn_ns_max)
-      while (nsm > 1 && nsm * N_HEAD * B > 256) nsm >>= 1;
       const int ns = (ri.x < 0 || r0 + bb >= B) ? 0 : min(nsm, (t + 63) / 64);
       const float* ml = a.st.part_ml + ((size_t)(b * N_HEAD + head) * NSPLIT) * 2;
       float m[NSPLIT], l[NSPLIT];
@@ -2220,19 +2229,36 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_f32b_kernel(GemvArgs a) {
       for (int i = 0; i < NSPLIT; ++i) cf[i] = m[i] * inv;
     }
     __syncthreads();
+    auto merge = [&](auto nsc) {
+      constexpr int NS = decltype(nsc)::value;
+      for (int e = tid; e < R * D; e += NTH) {
+        const int bb = e / D, c = e - bb * D;
+        const int b = min(r0 + bb, B - 1);
+        const int head = c / HD, d = c - head * HD;
+        const float* cf = cf_s + (bb * N_HEAD + head) * NSPLIT;
+        const float* po = a.st.part_o + ((size_t)(b * N_HEAD + head) * NSPLIT) * HD + d;
+        float pv[NS];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) pv[i] = po[(size_t)i * HD];
+        float y = 0.f;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) y += cf[i] * pv[i];
+        xs[bb * LDX + c] = y;
+      }
+    };
+    if (nsm == 1) merge(std::integral_constant<int, 1>{});
+    else if (nsm == 2) merge(std::integral_constant<int, 2>{});
+    else if (nsm == 4) merge(std::integral_constant<int, 4>{});
+    else if (nsm == 8) merge(std::integral_constant<int, 8>{});
+    else merge(std::integral_constant<int, NSPLIT>{});
+  } else if constexpr (IN == 4) {
+    // one round trip: the rows as the attention normalised them (the merge of one split: the same
+    // product o * (1 / l), the same bits)
     for (int e = tid; e < R * D; e += NTH) {
       const int bb = e / D, c = e - bb * D;
       const int b = min(r0 + bb, B - 1);
       const int head = c / HD, d = c - head * HD;
-      const float* cf = cf_s + (bb * N_HEAD + head) * NSPLIT;
-      const float* po = a.st.part_o + ((size_t)(b * N_HEAD + head) * NSPLIT) * HD + d;
-      float pv[NSPLIT];
-#pragma unroll
-      for (int i = 0; i < NSPLIT; ++i) pv[i] = po[(size_t)i * HD];
-      float y = 0.f;
-#pragma unroll
-      for (int i = 0; i < NSPLIT; ++i) y += cf[i] * pv[i];
-      xs[bb * LDX + c] = y;
+      xs[bb * LDX + c] = a.st.part_o[(size_t)(b * N_HEAD + head) * NSPLIT * HD + d];
     }
   }
   if constexpr (STAGE) __syncthreads();
@@ -2280,10 +2306,14 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_f32b_kernel(GemvArgs a) {
 
 int g_opt_f32b = 1;  // 1: batched fp32 parity steps (3 <= B <= 64) on exact-fp32 MFMA; 0: the GEMV family
 
+// 32-row batch tiles (NT = 2) where N gives the grid enough blocks; the N = 768 ops (c_proj, mlp
+// c_proj: 48 blocks of 32 rows, each loading all 32 operand rows) run 16-row tiles (96 blocks): a
+// block's time is the bytes it loads. Same bits either way (a column's dot product is its own).
 template <int K, int IN, int OUT>
 static void launch_f32b(const GemvArgs& a, hipStream_t s) {
-  dim3 grid((a.N + 15) / 16, a.B <= 16 ? 1 : (a.B + 31) / 32), block(K / 192 * 64);
-  if (a.B <= 16) hipLaunchKernelGGL((ar_f32b_kernel<K, 1, IN, OUT>), grid, block, 0, s, a);
+  const bool nt1 = a.B <= 16 || (a.N <= D && !(g_opt_exp & 8));
+  dim3 grid((a.N + 15) / 16, nt1 ? (a.B + 15) / 16 : (a.B + 31) / 32), block(K / 192 * 64);
+  if (nt1) hipLaunchKernelGGL((ar_f32b_kernel<K, 1, IN, OUT>), grid, block, 0, s, a);
   else hipLaunchKernelGGL((ar_f32b_kernel<K, 2, IN, OUT>), grid, block, 0, s, a);
 }
 
@@ -2432,8 +2462,12 @@ static void launch_op_f32b(int op, GemvArgs& a, const ArWeights& w, int l, int k
       if (l == 0) launch_f32b<768, 3, 0>(a, s);
       else launch_f32b<768, 0, 0>(a, s);
       break;
-    case 1: launch_attn(a.st, kvdtype, B, l, s, attn_ns_max(B)); break;
-    case 2: a.W = w.w_aproj[l]; a.Wf = w.f_aproj[l]; a.N = D; launch_f32b<768, 2, 1>(a, s); break;
+    case 1: launch_attn(a.st, kvdtype, B, l, s, attn_ns_max(B), attn_ns_max(B) == 1 ? 3 : 0); break;
+    case 2:
+      a.W = w.w_aproj[l]; a.Wf = w.f_aproj[l]; a.N = D;
+      if (attn_ns_max(B) == 1) launch_f32b<768, 4, 1>(a, s);  // the attention wrote the rows (direct 3)
+      else launch_f32b<768, 2, 1>(a, s);
+      break;
     case 3: a.W = w.w_fc[l]; a.Wf = w.f_fc[l]; a.N = DFF; a.ln_w = w.ln2[l]; launch_f32b<768, 0, 2>(a, s); break;
     case 4: a.W = w.w_mproj[l]; a.Wf = w.f_mproj[l]; a.N = D; launch_f32b<3072, 1, 1>(a, s); break;
     case 5: a.W = w.w_lm; a.Wf = w.f_lm; a.N = VOCAB; a.ln_w = w.lnf; launch_f32b<768, 0, 3>(a, s); break;

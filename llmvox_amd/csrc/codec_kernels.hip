@@ -1200,7 +1200,7 @@ __global__ __launch_bounds__(256) void gn_apply1_kernel(const float* __restrict_
     store4(y + off + (size_t)t * CD + qq * 4, o);
   }
 }
-int g_opt_codec_exp = 0;  // codec A/B bits (development): 1 the general gn_apply at every L; 6: dwconv FT (0: 16, 2: 8, 4: 32, 6: 4)
+int g_opt_codec_exp = 0;  // codec A/B bits (development): 1 the general gn_apply at every L; 6: dwconv FT at >= 2,048 frames (0: 4, 2: 16, 4: 32, 6: 8)
 template <bool SWISH, typename TO>
 static void gn_apply_launch(const float* x, int B, int L, const float* gw, const float* gb, TO* y, hipStream_t s) {
   if (L * 6 <= 8 * 256 && !(g_opt_codec_exp & 1)) hipLaunchKernelGGL((gn_apply1_kernel<SWISH, TO>), dim3(GN_G, B), dim3(256), 0, s, x, L, gw, gb, y);
@@ -1726,13 +1726,13 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
                      w.ada_scale + (size_t)bw * CD, w.ada_shift + (size_t)bw * CD, x);
   for (int i = 0; i < 12; ++i) {  // ConvNeXt blocks (modules.py:43-60)
     const int dwft = (g_opt_codec_exp >> 1) & 3;
-    if (M >= 2048 && dwft == 1)
+    if (M >= 2048 && dwft == 3)
       hipLaunchKernelGGL((dwconv_adaln_tile_kernel<TAct, 8>), dim3((L + 7) / 8, B), dim3(256), 0, s, x, L, w.dw_w[i],
                          w.dw_b[i], w.cn_scale[i] + (size_t)bw * CD, w.cn_shift[i] + (size_t)bw * CD, t2a);
     else if (M >= 2048 && dwft == 2)
       hipLaunchKernelGGL((dwconv_adaln_tile_kernel<TAct, 32>), dim3((L + 31) / 32, B), dim3(256), 0, s, x, L, w.dw_w[i],
                          w.dw_b[i], w.cn_scale[i] + (size_t)bw * CD, w.cn_shift[i] + (size_t)bw * CD, t2a);
-    else if (M >= 2048 && dwft == 0)
+    else if (M >= 2048 && dwft == 1)
       hipLaunchKernelGGL((dwconv_adaln_tile_kernel<TAct, 16>), dim3((L + 15) / 16, B), dim3(256), 0, s, x, L, w.dw_w[i],
                          w.dw_b[i], w.cn_scale[i] + (size_t)bw * CD, w.cn_shift[i] + (size_t)bw * CD, t2a);
     else
