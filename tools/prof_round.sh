@@ -9,7 +9,11 @@ cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 export PYTHONPATH=.
 TAG=${TAG:-r03}
 O=gpurun_out/$TAG; mkdir -p $O
+# PMC passes launch the steps one by one on the null stream (--null-stream): with the default
+# side-stream HIP-graph replay, rocprofv3 --pmc segfaults in its own thread (profiles/r03/pmc_segv_graph_replay.log);
+# per-dispatch counters do not depend on how the dispatch was submitted
 ARGS=${ARGS:-"--steps 20 --warmup 0 --no-cpu-baseline --no-parity-line"}
+PARGS=${PARGS:-"$ARGS --null-stream"}
 KEY=${KEY:-bf16/kvbf16/B32/P512}
 CKEY=${CKEY:-bf16/F8192/L256}
 run() { # tag, timeout, rocprof args..., -- cmd
@@ -17,12 +21,12 @@ run() { # tag, timeout, rocprof args..., -- cmd
   timeout -s KILL $t rocprofv3 "$@" > $O/$tag.log 2>&1 || { echo "FAIL $tag"; tail -30 $O/$tag.log; exit 1; }
 }
 csv() { find $O/$1 -name "*counter_collection.csv" | head -1; }
-run f 300 --pmc FETCH_SIZE -d $O/f -o run --output-format csv -- python3 bench.py $ARGS
-run w 300 --pmc WRITE_SIZE -d $O/w -o run --output-format csv -- python3 bench.py $ARGS
+run f 300 --pmc FETCH_SIZE -d $O/f -o run --output-format csv -- python3 bench.py $PARGS
+run w 300 --pmc WRITE_SIZE -d $O/w -o run --output-format csv -- python3 bench.py $PARGS
 python3 tools/pmc_traffic.py $(csv f) $(csv w) $KEY $O/pmc_traffic.json > $O/pmc_traffic.txt || exit 1
 cat $O/pmc_traffic.txt
 rm -rf $O/f $O/w  # raw per-dispatch CSVs: too large to merge back (gpurun_out <= 64 MiB)
-run m 300 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d $O/m -o run --output-format csv -- python3 bench.py $ARGS
+run m 300 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d $O/m -o run --output-format csv -- python3 bench.py $PARGS
 python3 tools/pmc_codec.py $(csv m) $CKEY $O/pmc_codec.json || exit 1
 rm -rf $O/m
 run kt 300 --kernel-trace --stats -d $O/kt -o run --output-format csv -- python3 bench.py $ARGS
