@@ -109,10 +109,15 @@ def kernel_bytes(which, B, t, wbytes, kvbytes):
     ns = attn_splits(B, wbytes)
     parts = act * 8 * ns * 98 if ns > 1 else 0           # split-KV partials written / read once
     rows_bf16 = 2 * D * B                                  # one bf16 operand row set
+    # the batched path's LayerNorm ahead of c_attn (layers >= 1) and lm_head folds the previous mlp
+    # c_proj's four K-slice partials into x: x and the four partial rows read, x written back and the
+    # bf16 operand rows written (ar_rows_kernel<4>, part of those probes); at B <= 8 the GEMM
+    # prologue reads x and the partials itself (nothing written)
+    fold = (6 * act * D + rows_bf16 if B > 8 else 5 * act * D) if mfma else 0
     if which == 0:
         if ksplit:  # operand rows in, 4 K-slice partials out (the KV append happens in the attention)
-            return 3 * D * D * wbytes + rows_bf16 + act * 4 * 3 * D
-        return 3 * D * D * wbytes + (rows_bf16 if mfma else act * D) + act * D + 2 * D * kvbytes * B
+            return 3 * D * D * wbytes + rows_bf16 + act * 4 * 3 * D + fold
+        return 3 * D * D * wbytes + (rows_bf16 if mfma else act * D) + act * D + 2 * D * kvbytes * B + fold
     if which == 1:
         kv = 2 * t * D * kvbytes * B
         if ksplit:  # partials in, new key appended, head outputs (bf16 rows or split partials) out
@@ -127,7 +132,7 @@ def kernel_bytes(which, B, t, wbytes, kvbytes):
     if which == 4:  # mfma: four K-slice partials (fp32) out
         return D * F * wbytes + ((2 * F * B + 4 * act * D) if mfma else act * (F + 2 * D))
     if which == 5:
-        return V * D * wbytes + ((rows_bf16 if mfma else act * D) + act * V)
+        return V * D * wbytes + ((rows_bf16 if mfma else act * D) + act * V) + fold
     raise ValueError(which)
 
 

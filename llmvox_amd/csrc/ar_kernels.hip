@@ -100,6 +100,8 @@ struct GemvArgs {
   int defer_sel;         // deferred greedy select (option "defer_select"). 1: B <= 2 GEMV step, lm_head
                          // publishes per-block granules, the next step's c_attn layer 0 reduces them;
                          // 2: batched step, the next step's embedding rows kernel reduces the logits
+  int xmap;              // ar_mfma2_kernel launched as a 1-D grid with the XCD-aligned tile order:
+                         // 1 = mlp c_proj (K slice = XCD mod 4), 2 = c_proj batch tiles (tile = XCD mod 2)
 };
 
 // ---------------------------------------------------------------------------------
@@ -1634,15 +1636,29 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   __shared__ float xo[OUT == 7 ? 16 * NT * 16 : 1];
   __shared__ float2 rs[XM == 1 ? NT * 16 : 1];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int n0 = blockIdx.x * 16;
-  const int r0 = blockIdx.z * (NT * 16);  // first batch row of this block's tile (grid.z batch tiles)
+  // XCD-aligned tile order (a.xmap, 1-D grid): workgroups are dealt to the 8 XCDs round robin, so
+  // with this order XCD x runs only the tiles of K slice x mod 4 (mlp c_proj) or of batch tile x mod 2
+  // (c_proj) and its L2 fetches only that part of the shared operand rows (the default order put
+  // every slice / batch tile on every XCD: 8 copies of all rows through the Infinity Fabric)
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (a.xmap == 1) {
+    const int x = bx & 7;
+    by = x & 3;
+    bx = (bx >> 3) * 2 + (x >> 2);
+  } else if (a.xmap == 2) {
+    const int x = bx & 7;
+    bz = x & 1;
+    bx = (bx >> 3) * 4 + (x >> 1);
+  }
+  const int n0 = bx * 16;
+  const int r0 = bz * (NT * 16);  // first batch row of this block's tile (grid.z batch tiles)
   const int B = a.B;
   TS_DECL;
   TS_MARK(0);
   const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(a.W);
   const bf16_t* __restrict__ X = XM == 1 ? a.st.xb : ((KTOT == 768) ? a.st.xn : a.st.hb);
   const int wrow = min(n0 + (lane & 15), a.N - 1);
-  const int k0 = blockIdx.y * K + wave * 192 + 8 * (lane >> 4);
+  const int k0 = by * K + wave * 192 + 8 * (lane >> 4);
   // epilogue operands first (a load in the epilogue is one more dependent round trip): thread tid
   // stores elements e = tid + k * NW * 64, all of batch row tid % (NT * 16) (NW * 64 is a multiple
   // of NT * 16): its control record (OUT 0, KV append) or its x values (OUT 7, residual)
@@ -1675,7 +1691,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   uint4 wf[6], xf[NT][6];
   // fragment-packed weights (a.Wf): the wave's 6 loads are 6 contiguous KB
   const bf16_t* wsrc = a.Wf ? reinterpret_cast<const bf16_t*>(a.Wf) +
-                                  (((size_t)(n0 >> 4) * (KTOT / 32) + (blockIdx.y * K + wave * 192) / 32) * 64 + lane) * 8
+                                  (((size_t)(n0 >> 4) * (KTOT / 32) + (by * K + wave * 192) / 32) * 64 + lane) * 8
                             : W + (size_t)wrow * KTOT + k0;
   const int wstep = a.Wf ? 512 : 32;
 #pragma unroll
@@ -1685,7 +1701,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
     const int b = min(r0 + t * 16 + (lane & 15), B - 1);  // padded columns recompute row B-1, never stored
     // fragment-packed rows (a.xpk): the tile's 6 fragments are 6 contiguous KB (padded rows: whatever
     // the tile holds there, never stored)
-    const bf16_t* xsrc = a.xpk ? X + ((((size_t)(r0 >> 4) + t) * (KTOT / 32) + (blockIdx.y * K + wave * 192) / 32) * 64 + lane) * 8
+    const bf16_t* xsrc = a.xpk ? X + ((((size_t)(r0 >> 4) + t) * (KTOT / 32) + (by * K + wave * 192) / 32) * 64 + lane) * 8
                                : X + (size_t)b * KTOT + k0;
     const int xstep = a.xpk ? 512 : 32;
 #pragma unroll
@@ -1760,6 +1776,8 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
       a.st.x[(size_t)b * D + n] = xn;
       a.st.xb[a.xpk ? xfrag(b, n, D) : (size_t)b * D + n] = f32_to_bf16(xn * gpre[k]);
       xo[e] = xn;
+    } else if (OUT == 6) {  // split-K partial of mlp c_proj (K slice by) -> pending copy
+      a.yacc[((size_t)b * YCOPIES + by) * D + n] = v;
     } else {
       gemv_store<OUT>(a, n, b, v);
     }
@@ -1777,7 +1795,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
         const float d = xo[r * (NT * 16) + tid] - mean;
         m2 += d * d;
       }
-      reinterpret_cast<float2*>(a.st.xstat)[(size_t)(r0 + tid) * (D / 16) + blockIdx.x] = make_float2(mean, m2);
+      reinterpret_cast<float2*>(a.st.xstat)[(size_t)(r0 + tid) * (D / 16) + bx] = make_float2(mean, m2);
     }
   }
   TS_SAVE(OUT == 0 ? 1 : OUT == 7 ? 3 : OUT == 5 ? 4 : OUT == 6 ? 5 : 6, a.layer, blockIdx.x + gridDim.x * blockIdx.y);
@@ -1793,6 +1811,12 @@ static void launch_mfma2(const GemvArgs& a, hipStream_t s, bool btile = false) {
   dim3 grid((a.N + 15) / 16), block((K / 192) * 64);
   if (btile && a.B > 16) {  // 16-row batch tiles in grid.z: half the operand bytes per block
     grid.z = (a.B + 15) / 16;
+    if (grid.z == 2 && grid.x % 4 == 0 && !(g_opt_exp & 16)) {  // XCD-aligned order (xmap 2)
+      GemvArgs b = a;
+      b.xmap = 2;
+      hipLaunchKernelGGL((ar_mfma2_kernel<K, 1, OUT, K, XM>), dim3(grid.x * 2), block, 0, s, b);
+      return;
+    }
     hipLaunchKernelGGL((ar_mfma2_kernel<K, 1, OUT, K, XM>), grid, block, 0, s, a);
   } else if (a.B <= 16) hipLaunchKernelGGL((ar_mfma2_kernel<K, 1, OUT, K, XM>), grid, block, 0, s, a);
   else if (a.B <= 32) hipLaunchKernelGGL((ar_mfma2_kernel<K, 2, OUT, K, XM>), grid, block, 0, s, a);
@@ -1886,9 +1910,14 @@ template <int OUT>
 static void launch_mproj_split(const GemvArgs& a, hipStream_t s) {
   static_assert(DFF == YCOPIES * 768, "one pending copy per K slice");
   dim3 grid((a.N + 15) / 16, YCOPIES), block(256);
-  if (a.B <= 16) hipLaunchKernelGGL((ar_mfma2_kernel<768, 1, OUT, DFF>), grid, block, 0, s, a);
-  else if (a.B <= 32) hipLaunchKernelGGL((ar_mfma2_kernel<768, 2, OUT, DFF>), grid, block, 0, s, a);
-  else hipLaunchKernelGGL((ar_mfma2_kernel<768, 4, OUT, DFF>), grid, block, 0, s, a);
+  GemvArgs b = a;
+  if (YCOPIES == 4 && grid.x % 2 == 0 && !(g_opt_exp & 16)) {  // XCD-aligned order (xmap 1): 1-D grid
+    b.xmap = 1;
+    grid = dim3(grid.x * 4);
+  }
+  if (a.B <= 16) hipLaunchKernelGGL((ar_mfma2_kernel<768, 1, OUT, DFF>), grid, block, 0, s, b);
+  else if (a.B <= 32) hipLaunchKernelGGL((ar_mfma2_kernel<768, 2, OUT, DFF>), grid, block, 0, s, b);
+  else hipLaunchKernelGGL((ar_mfma2_kernel<768, 4, OUT, DFF>), grid, block, 0, s, b);
 }
 
 // Batched GEMM with the per-row prologue fused (K = 768; small B): every block builds the
