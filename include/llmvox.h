@@ -162,6 +162,8 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
  *                     copy (bit-identical); bit 4: at 9 <= B <= 32 the bf16 operand rows (xn, xb,
  *                     hb) row-major instead of fragment-packed (bit-identical); bit 8: fp32 batched
  *                     c_proj / mlp c_proj in 32-row instead of 16-row batch tiles (bit-identical);
+ *                     bit 16: batched bf16 c_proj / mlp c_proj in the 2-D grid order instead of the
+ *                     XCD-aligned 1-D order (bit-identical);
  *   "f32b"         1: fp32 weights, 3 <= B <= 64: batched steps on exact-fp32 MFMA (ar_f32b_kernel);
  *                     0: the fp32 GEMV family (same ids against the reference: tests/test_gpu_f32b.py);
  *   "persist"      1: bf16 weights + bf16 KV, 17 <= B <= 32: each decode step is ONE persistent dataflow

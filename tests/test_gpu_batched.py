@@ -221,3 +221,27 @@ def test_fragment_packed_rows_with_odd_engine_size(S):
         np.testing.assert_array_equal(res[0][1], res[1][1])
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("B", [4, 17, 32])
+def test_xcd_aligned_tile_order_matches_grid_order(B):
+    """Round 3: c_proj (16-row batch tiles, B > 16) and mlp c_proj (four K slices) launch as 1-D grids
+    ordered so that each XCD runs one batch tile / K slice (its L2 fetches only that part of the
+    operand rows); option exp bit 16 restores the 2-D grid order. Same tiles, same arithmetic: bit for
+    bit, ragged batch, permuted slots."""
+    from llmvox_amd.engine import build_engine
+    e = build_engine(0, "bf16", "bf16", max_streams=64, max_positions=512, max_codec_frames=256)
+    try:
+        e.set_option("fuse_mlp", 0)
+        texts = _texts(B, 64, seed=11)
+        order = list(np.random.default_rng(B + 3).permutation(B))
+        res = []
+        for exp in (0, 16):
+            e.set_option("exp", exp)
+            res.append(_run(e, order, texts, set(range(0, B, 4)), 24, 40))
+        e.set_option("exp", 0)
+        e.set_option("fuse_mlp", 1)
+        np.testing.assert_array_equal(res[0][0], res[1][0])
+        np.testing.assert_array_equal(res[0][1], res[1][1])
+    finally:
+        e.close()

@@ -110,3 +110,34 @@ def test_f32b_rows_independent_of_batch_position(eng):
         out.append((tok.cpu().numpy()[inv], eng.last_logits(B).cpu().numpy()[inv]))
     np.testing.assert_array_equal(out[0][0], out[1][0])
     np.testing.assert_array_equal(out[0][1], out[1][1])
+
+
+@pytest.mark.parametrize("B", [17, 32])
+def test_f32b_tile_and_direct_rows_bit_identical(eng, B):
+    """Round 3: the N = 768 fp32 GEMMs (c_proj, mlp c_proj) run 16-row batch tiles (option exp bit 8:
+    32-row tiles): the same arithmetic either way, bit for bit (ragged batch). (At these B the
+    attention runs one split and writes the normalised rows c_proj stages, IN 4: held to the
+    reference's ids by the golden tests above.)"""
+    rng = np.random.default_rng(B)
+    n = 24
+    texts = rng.integers(3, 384, size=(B, n)).astype(np.int32)
+    dev = eng.device
+    res = []
+    for exp in (0, 8):
+        eng.set_option("exp", exp)
+        try:
+            for s in range(B):
+                eng.reset_slot(s)
+            pre = torch.from_numpy(texts[::3].copy()).to(dev)  # every third row runs 10 steps alone
+            Bp = pre.shape[0]
+            eng.ar_steps(10, torch.arange(0, B, 3, dtype=torch.int32, device=dev), pre,
+                         torch.zeros(Bp, dtype=torch.int32, device=dev), torch.zeros(Bp, n, dtype=torch.int32, device=dev))
+            rowstep = torch.tensor([10 if b % 3 == 0 else 0 for b in range(B)], dtype=torch.int32, device=dev)
+            tok = torch.zeros(B, n, dtype=torch.int32, device=dev)
+            eng.ar_steps(12, torch.arange(B, dtype=torch.int32, device=dev), torch.from_numpy(texts).to(dev), rowstep, tok)
+            eng.check_errors()
+            res.append((tok.cpu().numpy(), eng.last_logits(B).cpu().numpy()))
+        finally:
+            eng.set_option("exp", 0)
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    np.testing.assert_array_equal(res[0][1], res[1][1])
