@@ -2516,7 +2516,14 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
   }
   const bool mf = use_mfma<TW>(B);
   const bool fm = fused_mlp<TW>(B);
-  const int nsm = mf ? attn_ns_max(B) : NSPLIT;
+  // batched steps at B >= 9: one attention split per (row, head), the head output written straight
+  // into the bf16 operand row (no merge kernel). Round 3, tools/step_sweep.py (graph replay, us per
+  // step at t = 128 / 640): bf16 KV B = 12 104.3 / 113.0 -> 95.4 / 107.7, B = 16 107.1 / 126.7 ->
+  // 97.4 / 119.0; fp8 KV B = 12 103.2 / 110.3 -> 95.4 / 108.4, B = 16 104.2 / 111.5 -> 96.1 / 109.2.
+  // At B = 8 (64 blocks) one split loses at long histories (fp8 KV 102.4 -> 105.7 at t = 640 while
+  // 98.1 -> 92.5 at t = 128): B <= 8 keeps the split-KV attention + merge. Option exp bit 32 restores
+  // the two splits at 9 <= B <= 16 (A/B).
+  const int nsm = mf ? ((B > 8 && !(g_opt_exp & 32)) ? 1 : attn_ns_max(B)) : NSPLIT;
   const bool pk = mf && !(g_opt_exp & 2);  // fragment-packed weights for the MFMA GEMMs (exp bit 2: row-major)
   // fragment-packed operand rows on the v2 steps with the rows kernel (9 <= B <= 32; exp bit 4: row-major)
   a.xpk = (mf && B > MFMA_LN_MAX && B <= 32 && !(g_opt_exp & 4)) ? 1 : 0;

@@ -1200,7 +1200,9 @@ __global__ __launch_bounds__(256) void gn_apply1_kernel(const float* __restrict_
     store4(y + off + (size_t)t * CD + qq * 4, o);
   }
 }
-int g_opt_codec_exp = 0;  // codec A/B bits (development): 1 the general gn_apply at every L; 6: dwconv FT at >= 2,048 frames (0: 4, 2: 16, 4: 32, 6: 8)
+// codec A/B bits (development): 1 the general gn_apply at every L; 6: dwconv FT at >= 2,048 frames
+// (0: 4, 2: 16, 4: 32, 6: 8); 8: library exp / sin / cos in the bf16 iSTFT
+int g_opt_codec_exp = 0;
 template <bool SWISH, typename TO>
 static void gn_apply_launch(const float* x, int B, int L, const float* gw, const float* gb, TO* y, hipStream_t s) {
   if (L * 6 <= 8 * 256 && !(g_opt_codec_exp & 1)) hipLaunchKernelGGL((gn_apply1_kernel<SWISH, TO>), dim3(GN_G, B), dim3(256), 0, s, x, L, gw, gb, y);
@@ -1529,6 +1531,10 @@ __device__ __forceinline__ void stockham_pass(const float2* __restrict__ src, fl
   __syncthreads();
 }
 
+// FAST (bf16 codec modes, whose PCM is held to 2 % relative RMS of fp32): exp / sin / cos of the head's
+// magnitudes and phases on the native v_exp / v_sin / v_cos (~1e-6 relative for |phase| of order 10)
+// instead of the range-reduced library forms; the fp32 parity mode keeps expf / cosf / sinf.
+template <bool FAST>
 __global__ __launch_bounds__(256) void istft_frames_kernel(const float* __restrict__ spec, const float2* __restrict__ tw,
                                                            const float* __restrict__ window, float* __restrict__ frames) {
   __shared__ float2 bufA[FM], bufB[FM];
@@ -1565,9 +1571,9 @@ __global__ __launch_bounds__(256) void istft_frames_kernel(const float* __restri
   for (int u = 0; u < 3; ++u) {
     const int k = tid + 256 * u;
     if (k < NB) {
-      const float mag = fminf(expf(lm[u]), 100.0f);
+      const float mag = fminf(FAST ? __expf(lm[u]) : expf(lm[u]), 100.0f);
       const float ph = lp[u];
-      float2 x = make_float2(mag * cosf(ph), mag * sinf(ph));
+      float2 x = FAST ? make_float2(mag * __cosf(ph), mag * __sinf(ph)) : make_float2(mag * cosf(ph), mag * sinf(ph));
       if (k == 0 || k == NB - 1) x.y = 0.f;  // C2R ignores imag of DC and Nyquist
       X[k] = x;
     }
@@ -1758,7 +1764,11 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
     h.A = t2a; h.lda = CD; h.W = w.head_w; h.wscale = w.head_s; h.bias = w.head_b; h.C = sc.spec; h.ldc = 2 * NB;
     gemm_w<TW, TAct, A_PLAIN, E_BIAS>(h, s);
   }
-  hipLaunchKernelGGL(istft_frames_kernel, dim3(M), dim3(256), 0, s, sc.spec,
+  if (sizeof(TAct) == 2 && !(g_opt_codec_exp & 8))
+    hipLaunchKernelGGL(istft_frames_kernel<true>, dim3(M), dim3(256), 0, s, sc.spec,
+                       reinterpret_cast<const float2*>(w.twiddle), w.window, sc.frames);
+  else
+    hipLaunchKernelGGL(istft_frames_kernel<false>, dim3(M), dim3(256), 0, s, sc.spec,
                      reinterpret_cast<const float2*>(w.twiddle), w.window, sc.frames);
   hipLaunchKernelGGL(istft_ola_kernel, dim3((HOPL * L + 255) / 256, B), dim3(256), 0, s, sc.frames, w.window, L, pcm, sc.err);
 }
