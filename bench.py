@@ -81,13 +81,13 @@ def plan_for(ids, start, n, pad=384):
 # ---------------------------------------------------------------------------------------
 def attn_splits(B, wbytes):
     """KV splits per (row, head) of the decode attention at this B (ar_kernels.hip launch_op /
-    attn_ns_max): 16 on the B <= 2 GEMV path; bf16 weights at B >= 9: one (round 3); otherwise
-    (bf16 at 3 <= B <= 8, the fp32 batched path at 3 <= B <= 64) halved until splits x 8 heads x B
+    attn_ns_max): 16 on the B <= 2 GEMV path; bf16 weights at B >= 5: one (round 3); otherwise
+    (bf16 at 3 <= B <= 4, the fp32 batched path at 3 <= B <= 64) halved until splits x 8 heads x B
     <= 256 blocks. One split: the attention writes the normalised operand rows itself and no split
     partials exist."""
     if B < 3 or B > 64:
         return 16
-    if wbytes == 2 and B > 8:
+    if wbytes == 2 and B >= 5:  # (5 <= B <= 8: one split of 8-wave blocks)
         return 1
     ns = 16
     while ns > 1 and ns * 8 * B > 256:

@@ -2376,9 +2376,13 @@ static int attn_ns_max(int B) {  // enough splits to fill the chip, no more (ear
 }
 
 static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_t s, int ns_max = NSPLIT,
-                        int direct = 0, int selcopy = 0, bool qkv = false) {
+                        int direct = 0, int selcopy = 0, bool qkv = false, bool nw8 = false) {
   dim3 grid(ns_max, N_HEAD, B);
-  if (qkv && kvdtype == LVX_DTYPE_FP8)  // c_attn left K-slice partials (qkv_ksplit)
+  if (nw8 && !qkv && kvdtype == LVX_DTYPE_BF16)  // 8 waves, 128-key tiles: twice the KV bytes in flight per block
+    hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2, 8>), grid, dim3(512), 0, s, st, l, ns_max, direct, selcopy);
+  else if (nw8 && !qkv && kvdtype == LVX_DTYPE_FP8)
+    hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t, 2, 8>), grid, dim3(512), 0, s, st, l, ns_max, direct, selcopy);
+  else if (qkv && kvdtype == LVX_DTYPE_FP8)  // c_attn left K-slice partials (qkv_ksplit)
     hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t, 2, 4, true>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
   else if (qkv)
     hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2, 4, true>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
@@ -2523,7 +2527,13 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
   // At B = 8 (64 blocks) one split loses at long histories (fp8 KV 102.4 -> 105.7 at t = 640 while
   // 98.1 -> 92.5 at t = 128): B <= 8 keeps the split-KV attention + merge. Option exp bit 32 restores
   // the two splits at 9 <= B <= 16 (A/B).
-  const int nsm = mf ? ((B > 8 && !(g_opt_exp & 32)) ? 1 : attn_ns_max(B)) : NSPLIT;
+  // 5 <= B <= 8: one split too, in 8-wave blocks (128-key tiles: twice the KV bytes in flight per
+  // block, 40-64 blocks); tools/step_sweep.py, fp8 KV, B = 8, t = 128 / 640 / 896: 98.0 / 102.3 / 104.2
+  // -> 92.6 / 102.8 / 106.5 us (bf16 KV 98.7 / 105.9 / 108.5 -> 95.1 / 105.3 / 108.8): ~1 % over a
+  // 1,024-token utterance; at B = 4 it loses (91.9 / 94.5 / 95.5 -> 87.6 / 96.3 / 100.8). Option exp
+  // bit 64 restores the split-KV attention + merge kernel at 5 <= B <= 8.
+  const bool a8 = mf && B >= 5 && B <= 8 && !(g_opt_exp & 64);
+  const int nsm = mf ? (((B > 8 && !(g_opt_exp & 32)) || a8) ? 1 : attn_ns_max(B)) : NSPLIT;
   const bool pk = mf && !(g_opt_exp & 2);  // fragment-packed weights for the MFMA GEMMs (exp bit 2: row-major)
   // fragment-packed operand rows on the v2 steps with the rows kernel (9 <= B <= 32; exp bit 4: row-major)
   a.xpk = (mf && B > MFMA_LN_MAX && B <= 32 && !(g_opt_exp & 4)) ? 1 : 0;
@@ -2558,7 +2568,7 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       break;
     case 1:
       launch_attn(a.st, kvdtype, B, l, s, nsm, (mf && nsm == 1) ? 1 + a.xpk : 0, a.defer_sel == 1 && l == 0,
-                  qkv_ksplit<TW>(B, kvdtype));
+                  qkv_ksplit<TW>(B, kvdtype), a8);
       break;
     case 2:
       a.W = w.w_aproj[l]; a.Wf = pk ? w.f_aproj[l] : nullptr; a.N = D;
