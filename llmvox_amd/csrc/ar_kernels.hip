@@ -2531,8 +2531,11 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
   // block, 40-64 blocks); tools/step_sweep.py, fp8 KV, B = 8, t = 128 / 640 / 896: 98.0 / 102.3 / 104.2
   // -> 92.6 / 102.8 / 106.5 us (bf16 KV 98.7 / 105.9 / 108.5 -> 95.1 / 105.3 / 108.8): ~1 % over a
   // 1,024-token utterance; at B = 4 it loses (91.9 / 94.5 / 95.5 -> 87.6 / 96.3 / 100.8). Option exp
-  // bit 64 restores the split-KV attention + merge kernel at 5 <= B <= 8.
-  const bool a8 = mf && B >= 5 && B <= 8 && !(g_opt_exp & 64);
+  // bit 64 restores the split-KV attention + merge kernel at 5 <= B <= 8. fp8 KV (half the bytes per
+  // key) keeps the 8-wave blocks up to B = 16: B = 12 / 16, t = 128 / 640 / 896: 95.8 / 108.3 / 114.8 ->
+  // 97.0 / 105.5 / 109.6 and 95.8 / 109.6 / 115.5 -> 97.0 / 106.8 / 110.2 us; bf16 KV there loses
+  // (B = 16: 97.0 / 109.9 / 128.1 -> 100.8 / 112.5 / 130.5).
+  const bool a8 = mf && B >= 5 && (B <= 8 || (kvdtype == LVX_DTYPE_FP8 && (B <= 16 || ((g_opt_exp & 128) && B <= 32)))) && !(g_opt_exp & 64);
   const int nsm = mf ? (((B > 8 && !(g_opt_exp & 32)) || a8) ? 1 : attn_ns_max(B)) : NSPLIT;
   const bool pk = mf && !(g_opt_exp & 2);  // fragment-packed weights for the MFMA GEMMs (exp bit 2: row-major)
   // fragment-packed operand rows on the v2 steps with the rows kernel (9 <= B <= 32; exp bit 4: row-major)
