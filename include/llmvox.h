@@ -153,6 +153,8 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
  *   "codec_g2"     1: large-M bf16 codec GEMMs on the 128 x 128 MFMA tile kernel; 0: the general one;
  *   "codec_skinny" 1: bf16 codec weight GEMMs with M <= 384 frames on the K-split-over-waves kernel
  *                     (no split-K combine); 0: the tile kernels;
+ *   "codec_g3f"    1: fp32 (parity mode) codec GEMMs with >= 192 tiles of 128 x 192 on the LDS-DMA
+ *                     kernel (exact-fp32 v_mfma_f32_16x16x4_f32); 0: the 64 x 64 register-staged one;
  *   "codec_exp"    codec development bits, 0 = production kernels; bit 0: the general GroupNorm
  *                     kernel at every L (same bits); bits 1-2: dwconv+AdaLN frames per block at
  *                     >= 2,048 frames (0: 4, 1: 16, 2: 32, 3: 8; same bits);

@@ -12,6 +12,7 @@
 // The iSTFT is a per-frame LDS Stockham FFT (640-point complex, radices 4,4,4,2,5) wrapped as a
 // 1280-point C2R, followed by a gather-form overlap-add with the window-envelope divide.
 #include <algorithm>
+#include <type_traits>
 
 #include "lvx_internal.h"
 
@@ -703,8 +704,14 @@ __device__ __forceinline__ void glds16(const void* src, unsigned char* lds) {
                                    (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
 }
 
-template <int AMODE, int EPI, typename TC, int NS>
+template <int AMODE, int EPI, typename TC, int NS, typename TA = bf16_t>
 __global__ __launch_bounds__(512, NS == 2 ? 2 : 1) void gemm_glds_kernel(GemmArgs g) {
+  // TA = bf16: 64-deep k-tiles, v_mfma_f32_16x16x32_bf16. TA = float (the fp32 parity mode): the same
+  // 128-B LDS rows hold 32 k of fp32, and each 16-B fragment (4 consecutive k of one row) feeds four
+  // exact-fp32 v_mfma_f32_16x16x4_f32, MFMA e taking element e from every lane group (A and B
+  // permuted alike: the k order inside a 16-k block is 4 g + e)
+  constexpr int EPS = 16 / (int)sizeof(TA);  // elements per 16-B segment
+  constexpr int BKE = 8 * EPS;               // elements per k-tile (64 bf16 / 32 fp32)
   __shared__ __attribute__((aligned(1024))) unsigned char smem[NS * G3_STAGE];  // the only LDS object
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 2, wn = wave & 3;
@@ -715,37 +722,37 @@ __global__ __launch_bounds__(512, NS == 2 ? 2 : 1) void gemm_glds_kernel(GemmArg
   const int gsz = 8 * ntn, grp = q / gsz, within = q - grp * gsz;
   const int gm = min(8, ntm - grp * 8);
   const int m0 = (grp * 8 + within % gm) * G3_BM, n0 = (within / gm) * G3_BN;
-  const bf16_t* __restrict__ A = reinterpret_cast<const bf16_t*>(g.A);
-  const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(g.W);
-  const int nkt = g.K / G3_BK;  // K % 64 == 0 (checked by the launcher)
+  const TA* __restrict__ A = reinterpret_cast<const TA*>(g.A);
+  const TA* __restrict__ W = reinterpret_cast<const TA*>(g.W);
+  const int nkt = g.K / BKE;  // K % BKE == 0 (checked by the launcher)
   // DMA geometry: lane -> row lane / 8 of a 1-KB piece, LDS slot lane % 8 <- global segment gseg
   const int lrow = lane >> 3, gseg = (lane & 7) ^ lrow;
-  const bf16_t* bsrc[G3_BP];
+  const TA* bsrc[G3_BP];
 #pragma unroll
   for (int i = 0; i < G3_BP; ++i) {
     const int n = min(n0 + (wave * G3_BP + i) * 8 + lrow, g.N - 1);  // rows past N: never stored
-    bsrc[i] = W + (size_t)n * g.ldw + gseg * 8;
+    bsrc[i] = W + (size_t)n * g.ldw + gseg * EPS;
   }
-  const bf16_t* asrc[G3_AP];
+  const TA* asrc[G3_AP];
   int cb[G3_AP], ct[G3_AP];
 #pragma unroll
   for (int i = 0; i < G3_AP; ++i) {
     const int m = min(m0 + (wave * G3_AP + i) * 8 + lrow, g.M - 1);  // rows past M: never stored
-    asrc[i] = A + (size_t)m * g.lda + gseg * 8;
+    asrc[i] = A + (size_t)m * g.lda + gseg * EPS;
     cb[i] = AMODE == A_CONV ? m / g.L : 0;
     ct[i] = m - cb[i] * g.L;
   }
   auto issue = [&](int kt, int st) {
     unsigned char* sa = smem + st * G3_STAGE;
     unsigned char* sb = sa + G3_ABYTES;
-    const int kb = kt * G3_BK;
+    const int kb = kt * BKE;
 #pragma unroll
     for (int i = 0; i < G3_AP; ++i) {
       const void* src;
       if (AMODE == A_PLAIN) {
         src = asrc[i] + kb;
       } else {  // implicit conv: a 64-wide k-tile lies in one tap; padding rows from the zero granule
-        const int tap = kb / g.cin, c = kb - tap * g.cin + gseg * 8;
+        const int tap = kb / g.cin, c = kb - tap * g.cin + gseg * EPS;
         const int tt = ct[i] + tap - (g.taps - 1) / 2;
         src = (tt >= 0 && tt < g.L) ? (const void*)(A + ((size_t)cb[i] * g.L + tt) * g.cin + c) : (const void*)g3_zero;
       }
@@ -776,26 +783,34 @@ __global__ __launch_bounds__(512, NS == 2 ? 2 : 1) void gemm_glds_kernel(GemmArg
     const unsigned char* sa = smem + (kt % NS) * G3_STAGE;
     const unsigned char* sb = sa + G3_ABYTES;
     // both k32 sub-steps' fragments issued before the first MFMA
-    bf16x8 fa[2][4], fb[2][3];
+    typedef typename std::conditional<sizeof(TA) == 2, bf16x8, f32x4v>::type Frag;
+    Frag fa[2][4], fb[2][3];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int slot = ((kk * 4 + fseg) ^ fsw) * 16;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        fa[kk][i] = *reinterpret_cast<const bf16x8*>(sa + (wm * 64 + i * 16 + frow) * 128 + slot);
+        fa[kk][i] = *reinterpret_cast<const Frag*>(sa + (wm * 64 + i * 16 + frow) * 128 + slot);
 #pragma unroll
       for (int j = 0; j < 3; ++j)
-        fb[kk][j] = *reinterpret_cast<const bf16x8*>(sb + (wn * 48 + j * 16 + frow) * 128 + slot);
+        fb[kk][j] = *reinterpret_cast<const Frag*>(sb + (wn * 48 + j * 16 + frow) * 128 + slot);
     }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
+        for (int j = 0; j < 3; ++j) {
           // weights as the MFMA's A operand: the accumulator is the transposed tile, so each lane
           // holds 4 consecutive output columns of one row (same products, same k order: same bits)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[kk][j], fa[kk][i], acc[i][j], 0, 0, 0);
+          if constexpr (sizeof(TA) == 2) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[kk][j], fa[kk][i], acc[i][j], 0, 0, 0);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fb[kk][j][e], fa[kk][i][e], acc[i][j], 0, 0, 0);
+          }
+        }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail DMAs
   // epilogue: acc[i][j][e] = C[m0 + wm*64 + i*16 + (lane & 15)][n0 + wn*48 + j*16 + 4*(lane >> 4) + e]:
@@ -892,19 +907,21 @@ __global__ __launch_bounds__(512, NS == 2 ? 2 : 1) void gemm_glds_kernel(GemmArg
 }
 
 int g_opt_codec_g3 = 1;  // 1: large-M bf16 GEMMs on gemm_glds_kernel; 0: off (cross-check)
+int g_opt_codec_g3f = 0;  // 1: large-M fp32 (parity mode) GEMMs on gemm_glds_kernel<float>; 0: gemm_mfma
 // the LDS-DMA kernel needs enough 128 x 192 tiles to fill the chip
+template <typename TA = bf16_t>
 static bool g3_ok(const GemmArgs& g) {
-  return g_opt_codec_g3 && g.K % G3_BK == 0 && ((g.M + G3_BM - 1) / G3_BM) * ((g.N + G3_BN - 1) / G3_BN) >= 192;
+  return g_opt_codec_g3 && g.K % (128 / (int)sizeof(TA)) == 0 && ((g.M + G3_BM - 1) / G3_BM) * ((g.N + G3_BN - 1) / G3_BN) >= 192;
 }
-template <int AMODE, int EPI, typename TC>
+template <int AMODE, int EPI, typename TC, typename TA = bf16_t>
 static void g3_launch(GemmArgs g, hipStream_t s) {
   static_assert(EPI != E_SCALE, "weight GEMMs only");
   dim3 grid((g.N + G3_BN - 1) / G3_BN, (g.M + G3_BM - 1) / G3_BM);
   // more tiles than CUs: two blocks per CU (2 stages, 80 KB each), else one (3 stages, 120 KB).
   // Kernel traces of the 32 x 256-frame decode: N = 2,304 (768 tiles) 52.5 vs 61 us, N = 768 (256
   // tiles) 40.4 vs 47 us; 16 x 256 frames (N = 2,304: 384 tiles) 1.57 vs 1.70 ms per decode
-  if (grid.x * grid.y > 256) hipLaunchKernelGGL((gemm_glds_kernel<AMODE, EPI, TC, 2>), grid, dim3(512), 0, s, g);
-  else hipLaunchKernelGGL((gemm_glds_kernel<AMODE, EPI, TC, 3>), grid, dim3(512), 0, s, g);
+  if (grid.x * grid.y > 256) hipLaunchKernelGGL((gemm_glds_kernel<AMODE, EPI, TC, 2, TA>), grid, dim3(512), 0, s, g);
+  else hipLaunchKernelGGL((gemm_glds_kernel<AMODE, EPI, TC, 3, TA>), grid, dim3(512), 0, s, g);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1057,7 +1074,8 @@ static void gemm_w(const GemmArgs& g, hipStream_t s) {
     else gemm_launch<true, TA, bf16_t, AMODE, EPI, TC>(g, 1, s);
   } else {
     static_assert(sizeof(TA) == 4 && sizeof(TC) == 4, "parity mode keeps fp32 activations");
-    gemm_launch<false, float, float, AMODE, EPI, float>(g, 1, s);
+    if (EPI != E_SCALE && g_opt_codec_g3f && g3_ok<float>(g)) g3_launch<AMODE, (EPI == E_SCALE ? E_BIAS : EPI), float, float>(g, s);
+    else gemm_launch<false, float, float, AMODE, EPI, float>(g, 1, s);
   }
 }
 // activation x activation GEMMs (AttnBlock scores / P.V): operands are fp32 in memory

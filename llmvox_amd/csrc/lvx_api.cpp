@@ -613,6 +613,7 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   else if (n == "codec_g2") g_opt_codec_g2 = value != 0;
   else if (n == "codec_skinny") g_opt_codec_skinny = value != 0;
   else if (n == "codec_g3") g_opt_codec_g3 = value != 0;
+  else if (n == "codec_g3f") g_opt_codec_g3f = value != 0;
   else if (n == "codec_exp") g_opt_codec_exp = value;
   else if (n == "exp") g_opt_exp = value;
   else if (n == "f32b") g_opt_f32b = value != 0;

@@ -24,7 +24,7 @@ __host__ __device__ inline size_t kv_at(size_t layer, size_t chunks, size_t stre
 #endif
 constexpr int YCOPIES = LVX_YCOPIES;  // accumulator copies of the fused MLP (spreads atomic contention)
 constexpr int LM_MAX_BLOCKS = 1024;  // lm_head blocks of the fused argmax tail (4096 rows / 8 per block = 512)
-extern int g_opt_defer_select, g_opt_fuse_mlp, g_opt_bt, g_opt_codec_g2, g_opt_codec_skinny, g_opt_codec_g3, g_opt_codec_exp, g_opt_exp,
+extern int g_opt_defer_select, g_opt_fuse_mlp, g_opt_bt, g_opt_codec_g2, g_opt_codec_skinny, g_opt_codec_g3, g_opt_codec_g3f, g_opt_codec_exp, g_opt_exp,
     g_opt_f32b, g_opt_persist, g_opt_pexp, g_mfma_ln_max, g_opt_ksplit;
 size_t persist_ctr_words();  // words of ArState::pctr  // cross-check switches (lvx_set_option)
 
