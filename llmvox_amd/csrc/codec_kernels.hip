@@ -907,7 +907,7 @@ __global__ __launch_bounds__(512, NS == 2 ? 2 : 1) void gemm_glds_kernel(GemmArg
 }
 
 int g_opt_codec_g3 = 1;  // 1: large-M bf16 GEMMs on gemm_glds_kernel; 0: off (cross-check)
-int g_opt_codec_g3f = 0;  // 1: large-M fp32 (parity mode) GEMMs on gemm_glds_kernel<float>; 0: gemm_mfma
+int g_opt_codec_g3f = 1;  // 1: large-M fp32 (parity mode) GEMMs on gemm_glds_kernel<float>; 0: gemm_mfma
 // the LDS-DMA kernel needs enough 128 x 192 tiles to fill the chip
 template <typename TA = bf16_t>
 static bool g3_ok(const GemmArgs& g) {

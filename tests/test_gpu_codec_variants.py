@@ -8,7 +8,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 SHAPES = ((32, 256), (1, 256), (2, 160), (1, 10), (3, 7))
-DEFAULT_G3F = 0  # the library's default of option codec_g3f
+DEFAULT_G3F = 1  # the library's default of option codec_g3f
 
 
 @pytest.fixture(scope="module", params=["bf16", "fp32"])
