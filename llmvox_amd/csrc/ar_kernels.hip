@@ -1082,12 +1082,12 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
   // block for long splits (batched steps)
   constexpr int TK = NW * 16;
   constexpr bool SLOT = sizeof(TKV) < 4;  // per-key-slot online softmax (bf16 / fp8 KV)
-  static_assert(!QKV || (sizeof(TKV) <= 2 && (NW == 4 || NW == 8)), "the K-split c_attn path: bf16 / fp8 keys, 4 or 8 waves");
+  static_assert(!QKV || NW == 4 || NW == 8, "the K-split c_attn path: 4 or 8 waves");
   constexpr int QH = QKV ? (3 * HD + NW * 64 - 1) / (NW * 64) : 1;  // q / k / v elements per thread (2 at 4 waves, 1 at 8)
   __shared__ float wm_s[NW], wl_s[NW];
   __shared__ float wo_s[NW][4][HD];  // [wave][16-lane row][part * 24 + i]
   __shared__ float qs_s[QKV ? HD : 1];
-  __shared__ __attribute__((aligned(16))) TKV kvh_s[QKV ? 2 : 1][sizeof(TKV) < 4 ? HD : 1];  // QKV: the new key's K, V
+  __shared__ __attribute__((aligned(16))) TKV kvh_s[QKV ? 2 : 1][QKV ? HD : 1];  // QKV: the new key's K, V
   const int sp = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   TS_DECL;
@@ -1215,11 +1215,10 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
 #pragma unroll
       for (int i = 0; i < 3; ++i) { kx[i] = kp[i]; vx[i] = vp[i]; }
       if (kb + TK >= k1 && min(kb + kq, k1 - 1) == t - 1) {
-        typedef decltype(kx[0].u) PieceT;  // uint4 (8 bf16) / uint2 (8 fp8)
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          kx[i].u = reinterpret_cast<const PieceT*>(kvh_s[0])[part * 3 + i];
-          vx[i].u = reinterpret_cast<const PieceT*>(kvh_s[1])[part * 3 + i];
+        for (int i = 0; i < 3; ++i) {  // 8 keys' worth of bytes from the LDS copy (fp8: uint2, bf16: uint4, fp32: 2 x float4)
+          kx[i].load(kvh_s[0] + part * 24 + i * 8);
+          vx[i].load(kvh_s[1] + part * 24 + i * 8);
         }
       }
 #pragma unroll
@@ -1262,7 +1261,8 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
       } else if (e < 3 * HD && k1 == t) {  // K / V of the new key (the last split): appended, kept in LDS
         const int which = e / HD - 1, d = e % HD;
         TKV hv;  // the value the one-launch c_attn stores (store_kv)
-        if constexpr (sizeof(TKV) == 2) hv = f32_to_bf16(v);
+        if constexpr (sizeof(TKV) == 4) hv = v;
+        else if constexpr (sizeof(TKV) == 2) hv = f32_to_bf16(v);
         else hv = f32_to_fp8(v);
         kvh_s[which][d] = hv;
         reinterpret_cast<TKV*>(which ? st.vc : st.kc)[base + krow(ri.y) + d] = hv;
@@ -1465,6 +1465,9 @@ __device__ __forceinline__ void embed_row(const GemvArgs& a, int4 ri, int lane, 
 }
 
 // 0: LayerNorm(x)  4: LayerNorm(x + pending copies)  3: embedding (+ stores x) then LayerNorm
+// 5: as 4 with fp32 output rows in st.h ([B][768]; the batched fp32 parity mode's c_attn / lm_head
+// operand, ar_qkv_ksplit_f32_kernel / ar_f32b_kernel IN 6: h is free between mlp c_proj and the next
+// c_fc)  6: as 3 with the fp32 output rows of 5
 template <int MODE>
 __global__ __launch_bounds__(256) void ar_rows_kernel(GemvArgs a) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1475,13 +1478,13 @@ __global__ __launch_bounds__(256) void ar_rows_kernel(GemvArgs a) {
   float4 g[3], v[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) g[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
-  if (MODE == 0 || MODE == 4) {
-    XRow<MODE> r;
+  if (MODE == 0 || MODE == 4 || MODE == 5) {
+    XRow<MODE == 5 ? 4 : MODE> r;
     xrow_issue(a, b, lane, r);
     __builtin_amdgcn_sched_barrier(0);  // gamma and the rows issued up front (the scheduler sank a
                                         // gamma load behind the variance: one more round trip)
     xrow_sum(r, v);
-    if (MODE == 4)  // fold the pending copies into x here (one wave owns the row): the next c_proj
+    if (MODE == 4 || MODE == 5)  // fold the pending copies into x here (one wave owns the row): the next c_proj
 #pragma unroll      // then adds its output to a final x instead of re-reading the copies
       for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = v[j];
   } else {
@@ -1492,6 +1495,11 @@ __global__ __launch_bounds__(256) void ar_rows_kernel(GemvArgs a) {
   }
   TS_MARK(1);
   wave_ln_regs(v, g);
+  if constexpr (MODE == 5 || MODE == 6) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.h + (size_t)b * D + j * 256 + lane * 4) = v[j];
+    return;
+  }
   uint2* dst = reinterpret_cast<uint2*>(a.st.xn + (size_t)b * D);
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
@@ -2162,24 +2170,30 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_bt_kernel(GemvArgs a) {
 // are summed through LDS in wave order: deterministic, and a row's result never depends on its batch
 // position (an MFMA column's dot product uses only that column's data).
 // ---------------------------------------------------------------------------------
-template <int K, int NT, int IN, int OUT>
+// KTOT > K (mlp c_proj, OUT 6): the K = 3072 reduction split over blockIdx.z into KTOT / K slices of
+// 768, each slice's partial stored to its pending copy (st.yacc), folded into x by the rows kernel
+// (ar_rows_kernel<5>) that normalises c_attn's / lm_head's operand rows (IN 6): 4x the blocks, a
+// quarter of the bytes per block.
+template <int K, int NT, int IN, int OUT, int KTOT = K>
 __global__ __launch_bounds__(K / 192 * 64) void ar_f32b_kernel(GemvArgs a) {
   constexpr int NW = K / 192, R = NT * 16, NTH = NW * 64;
   constexpr bool STAGE = IN != 1;  // K == 768: the operand tile in LDS
+  static_assert(KTOT == K || (IN == 1 && OUT == 6 && KTOT == YCOPIES * K), "split K: mlp c_proj into the pending copies");
   // IN 4 (c_proj after a one-split attention, direct == 3): the normalised rows are split 0 of part_o
+  // IN 6 (c_attn / lm_head after ar_rows_kernel<5>): the LayerNorm'd fp32 rows in st.h
   static_assert(!STAGE || K == 768, "the LDS operand tile holds K = 768 rows");
   constexpr int LDX = D + 4;  // fp32 row stride: 16 rows x 4 banks apart, conflict-free 16-B reads
   __shared__ __attribute__((aligned(16))) float xs[STAGE ? R * LDX : 4];
   __shared__ float red[NW][16 * R];
   __shared__ float cf_s[IN == 2 ? R * N_HEAD * NSPLIT : 1];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int n0 = blockIdx.x * 16, r0 = blockIdx.y * R;
+  const int n0 = blockIdx.x * 16, r0 = blockIdx.y * R, ks = KTOT > K ? blockIdx.z : 0;
   const int B = a.B;
   // weights (fragment-packed, the wave's 12 contiguous KB), issued first for IN 1 / IN 2; behind the
   // first row inputs for the LayerNorm modes (their statistics then overlap the weight stream)
-  const float4* wsrc = reinterpret_cast<const float4*>(a.Wf) + ((size_t)(n0 >> 4) * (K / 16) + wave * 12) * 64 + lane;
+  const float4* wsrc = reinterpret_cast<const float4*>(a.Wf) + ((size_t)(n0 >> 4) * (KTOT / 16) + ks * (K / 16) + wave * 12) * 64 + lane;
   float4 wf[12];
-  if constexpr (IN == 1 || IN == 2 || IN == 4) {
+  if constexpr (IN == 1 || IN == 2 || IN == 4 || IN == 6) {
 #pragma unroll
     for (int j = 0; j < 12; ++j) wf[j] = wsrc[j * 64];
     // all 12 in flight before anything else (left to itself the scheduler interleaved each load with
@@ -2289,6 +2303,22 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_f32b_kernel(GemvArgs a) {
       const int head = c / HD, d = c - head * HD;
       xs[bb * LDX + c] = a.st.part_o[(size_t)(b * N_HEAD + head) * NSPLIT * HD + d];
     }
+  } else if constexpr (IN == 6) {
+    // the rows kernel's LayerNorm'd rows, 16 B per thread and load, all in flight (padded rows:
+    // row B-1, never stored)
+    constexpr int NL = R * D / 4 / NTH;
+    static_assert(R * D / 4 % NTH == 0, "whole float4 loads per thread");
+    float4 rv[NL];
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int e = (tid + i * NTH) * 4, bb = e / D, c = e - bb * D;
+      rv[i] = *reinterpret_cast<const float4*>(a.st.h + (size_t)min(r0 + bb, B - 1) * D + c);
+    }
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int e = (tid + i * NTH) * 4, bb = e / D, c = e - bb * D;
+      *reinterpret_cast<float4*>(xs + bb * LDX + c) = rv[i];
+    }
   }
   if constexpr (STAGE) __syncthreads();
   f32x4_t acc[NT];
@@ -2304,7 +2334,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_f32b_kernel(GemvArgs a) {
       for (int j = 0; j < 12; ++j) xf[j] = *reinterpret_cast<const float4*>(xr + 16 * j);
     } else {
       const int b = min(r0 + t * 16 + (lane & 15), B - 1);  // padded columns recompute row B-1, never stored
-      const float* xr = a.st.h + (size_t)b * K + wave * 192 + kq;
+      const float* xr = a.st.h + (size_t)b * KTOT + ks * K + wave * 192 + kq;
 #pragma unroll
       for (int j = 0; j < 12; ++j) xf[j] = *reinterpret_cast<const float4*>(xr + 16 * j);
     }
@@ -2329,7 +2359,65 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_f32b_kernel(GemvArgs a) {
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) v += red[w][e];
-    gemv_store<OUT>(a, n, b, v);
+    if constexpr (OUT == 6) a.yacc[((size_t)b * YCOPIES + ks) * D + n] = v;  // K slice ks -> its pending copy
+    else gemv_store<OUT>(a, n, b, v);
+  }
+}
+
+// c_attn of the batched fp32 parity mode (B <= 32), the K = 768 reduction split over the grid as in
+// ar_qkv_ksplit_kernel: a block is 4 waves x 16 output rows of one 192-wide K slice (48 KB of
+// fragment-packed fp32 weights) and stages the slice of the rows kernel's LayerNorm'd fp32 rows (st.h,
+// NT * 16 x 192) once in LDS for its 4 waves; each wave stores its 16 x (NT * 16) partial to
+// st.qkvp[slice]; the attention (ar_attn_v2_kernel<float, ..., QKV>) sums the four slices in slice
+// order and appends the new key. 144 blocks of 48 + 24 KB instead of 144 of 48 + 96 KB.
+template <int NT>
+__global__ __launch_bounds__(256) void ar_qkv_ksplit_f32_kernel(GemvArgs a) {
+  constexpr int XR = NT * 16, XS = 196;  // rows, fp32 row stride (784 B: 16 rows 4 banks apart)
+  __shared__ __attribute__((aligned(16))) float xs[XR * XS];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int n0 = (blockIdx.x * 4 + wave) * 16, ks = blockIdx.y;
+  const int B = a.B;
+  constexpr int XC = XR * 48 / 256;  // 16-B chunks per thread (3 / 6)
+  static_assert(XR * 48 % 256 == 0, "whole chunks per thread");
+  float4 xv[XC];
+#pragma unroll
+  for (int j = 0; j < XC; ++j) {  // the operand slice first (rows past B: row B-1, never stored)
+    const int c = tid + 256 * j, r = c / 48, q = c - r * 48;
+    xv[j] = *reinterpret_cast<const float4*>(a.st.h + (size_t)min(r, B - 1) * D + ks * 192 + q * 4);
+  }
+  const float4* wsrc = reinterpret_cast<const float4*>(a.Wf) + ((size_t)(n0 >> 4) * (D / 16) + ks * 12) * 64 + lane;
+  float4 wf[12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) wf[j] = wsrc[j * 64];
+#pragma unroll
+  for (int j = 0; j < XC; ++j) {
+    const int c = tid + 256 * j, r = c / 48, q = c - r * 48;
+    *reinterpret_cast<float4*>(xs + r * XS + q * 4) = xv[j];
+  }
+  __syncthreads();
+  const int kq = 4 * (lane >> 4);
+  f32x4_t acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    float4 xf[12];
+    const float* xr = xs + (t * 16 + (lane & 15)) * XS + kq;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) xf[j] = *reinterpret_cast<const float4*>(xr + 16 * j);
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[j].x, xf[j].x, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[j].y, xf[j].y, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[j].z, xf[j].z, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[j].w, xf[j].w, acc[t], 0, 0, 0);
+    }
+  }
+  // lane: C[n0 + 4 (lane >> 4) + i][t * 16 + (lane & 15)], i = 0..3
+  float* dst = a.st.qkvp + (size_t)ks * a.st.max_streams * (3 * D) + n0 + 4 * (lane >> 4);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int b = t * 16 + (lane & 15);
+    if (b < B) *reinterpret_cast<float4*>(dst + (size_t)b * (3 * D)) = make_float4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
   }
 }
 
@@ -2338,12 +2426,12 @@ int g_opt_f32b = 1;  // 1: batched fp32 parity steps (3 <= B <= 64) on exact-fp3
 // 32-row batch tiles (NT = 2) where N gives the grid enough blocks; the N = 768 ops (c_proj, mlp
 // c_proj: 48 blocks of 32 rows, each loading all 32 operand rows) run 16-row tiles (96 blocks): a
 // block's time is the bytes it loads. Same bits either way (a column's dot product is its own).
-template <int K, int IN, int OUT>
+template <int K, int IN, int OUT, int KTOT = K>
 static void launch_f32b(const GemvArgs& a, hipStream_t s) {
   const bool nt1 = a.B <= 16 || (a.N <= D && !(g_opt_exp & 8));
-  dim3 grid((a.N + 15) / 16, nt1 ? (a.B + 15) / 16 : (a.B + 31) / 32), block(K / 192 * 64);
-  if (nt1) hipLaunchKernelGGL((ar_f32b_kernel<K, 1, IN, OUT>), grid, block, 0, s, a);
-  else hipLaunchKernelGGL((ar_f32b_kernel<K, 2, IN, OUT>), grid, block, 0, s, a);
+  dim3 grid((a.N + 15) / 16, nt1 ? (a.B + 15) / 16 : (a.B + 31) / 32, KTOT / K), block(K / 192 * 64);
+  if (nt1) hipLaunchKernelGGL((ar_f32b_kernel<K, 1, IN, OUT, KTOT>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((ar_f32b_kernel<K, 2, IN, OUT, KTOT>), grid, block, 0, s, a);
 }
 
 // Measured (round-1 sweep, us per step at positions 256-511): v3 saves kernels but every block
@@ -2382,6 +2470,8 @@ static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_
     hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2, 8>), grid, dim3(512), 0, s, st, l, ns_max, direct, selcopy);
   else if (nw8 && !qkv && kvdtype == LVX_DTYPE_FP8)
     hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t, 2, 8>), grid, dim3(512), 0, s, st, l, ns_max, direct, selcopy);
+  else if (qkv && kvdtype == LVX_DTYPE_F32)  // fp32 parity mode: ar_qkv_ksplit_f32_kernel's partials
+    hipLaunchKernelGGL((ar_attn_v2_kernel<float, 2, 4, true>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
   else if (qkv && kvdtype == LVX_DTYPE_FP8)  // c_attn left K-slice partials (qkv_ksplit)
     hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t, 2, 4, true>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
   else if (qkv)
@@ -2481,29 +2571,58 @@ static bool use_f32b(int B) {
   return sizeof(TW) == 4 && g_opt_f32b && B >= MFMA_BATCH_MIN && B <= 64;
 }
 
-// batched fp32 parity steps: five exact-fp32 MFMA kernels + the attention per layer, x final at
-// every boundary; the split-KV partials are merged in c_proj's prologue; the select is the argmax
-// kernel after lm_head
+// batched fp32 parity steps: five exact-fp32 MFMA kernels + the attention per layer; the split-KV
+// partials are merged in c_proj's prologue; the select is the argmax kernel after lm_head.
+// mlp c_proj runs as 4 K slices into the pending copies (384 blocks of 4 waves instead of 96 of 16:
+// the 16-wave blocks each loaded 392 KB on 96 CUs); the rows kernel before c_attn (layers >= 1) and
+// lm_head folds them into x and leaves the LayerNorm'd fp32 rows the GEMM stages (IN 6). Option exp
+// bit 512: the unsplit mlp c_proj with x final at every boundary and the LayerNorm in the GEMM prologue.
 static void launch_op_f32b(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtype, int B, hipStream_t s) {
+  const bool ksp = !(g_opt_exp & 512);
   a.layer = l;
-  a.yacc = nullptr;
+  a.yacc = ksp ? a.st.yacc : nullptr;
   a.add_y = 0;
   a.xpk = 0;
+  // c_attn split over K too (B <= 32), its partials summed by the attention; option exp bit 1024: one launch
+  const bool qsp = ksp && B <= 32 && !(g_opt_exp & 1024);
   switch (op) {
     case 0:
       a.W = w.w_attn[l]; a.Wf = w.f_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
-      if (l == 0) launch_f32b<768, 3, 0>(a, s);
-      else launch_f32b<768, 0, 0>(a, s);
+      if (qsp) {  // rows kernel (layer 0: embedding; else x + the MLP copies) -> fp32 rows, then the K slices
+        if (l == 0) hipLaunchKernelGGL((ar_rows_kernel<6>), dim3(B), dim3(64), 0, s, a);
+        else hipLaunchKernelGGL((ar_rows_kernel<5>), dim3(B), dim3(64), 0, s, a);
+        if (B <= 16) hipLaunchKernelGGL((ar_qkv_ksplit_f32_kernel<1>), dim3(3 * D / 64, 4), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((ar_qkv_ksplit_f32_kernel<2>), dim3(3 * D / 64, 4), dim3(256), 0, s, a);
+      } else if (l == 0) {
+        launch_f32b<768, 3, 0>(a, s);
+      } else if (ksp) {
+        hipLaunchKernelGGL((ar_rows_kernel<5>), dim3(B), dim3(64), 0, s, a);
+        launch_f32b<768, 6, 0>(a, s);
+      } else {
+        launch_f32b<768, 0, 0>(a, s);
+      }
       break;
-    case 1: launch_attn(a.st, kvdtype, B, l, s, attn_ns_max(B), attn_ns_max(B) == 1 ? 3 : 0); break;
+    case 1: launch_attn(a.st, kvdtype, B, l, s, attn_ns_max(B), attn_ns_max(B) == 1 ? 3 : 0, 0, qsp); break;
     case 2:
       a.W = w.w_aproj[l]; a.Wf = w.f_aproj[l]; a.N = D;
       if (attn_ns_max(B) == 1) launch_f32b<768, 4, 1>(a, s);  // the attention wrote the rows (direct 3)
       else launch_f32b<768, 2, 1>(a, s);
       break;
     case 3: a.W = w.w_fc[l]; a.Wf = w.f_fc[l]; a.N = DFF; a.ln_w = w.ln2[l]; launch_f32b<768, 0, 2>(a, s); break;
-    case 4: a.W = w.w_mproj[l]; a.Wf = w.f_mproj[l]; a.N = D; launch_f32b<3072, 1, 1>(a, s); break;
-    case 5: a.W = w.w_lm; a.Wf = w.f_lm; a.N = VOCAB; a.ln_w = w.lnf; launch_f32b<768, 0, 3>(a, s); break;
+    case 4:
+      a.W = w.w_mproj[l]; a.Wf = w.f_mproj[l]; a.N = D;
+      if (ksp) launch_f32b<768, 1, 6, DFF>(a, s);
+      else launch_f32b<3072, 1, 1>(a, s);
+      break;
+    case 5:
+      a.W = w.w_lm; a.Wf = w.f_lm; a.N = VOCAB; a.ln_w = w.lnf;
+      if (ksp) {
+        hipLaunchKernelGGL((ar_rows_kernel<5>), dim3(B), dim3(64), 0, s, a);
+        launch_f32b<768, 6, 3>(a, s);
+      } else {
+        launch_f32b<768, 0, 3>(a, s);
+      }
+      break;
   }
 }
 

@@ -141,3 +141,37 @@ def test_f32b_tile_and_direct_rows_bit_identical(eng, B):
             eng.set_option("exp", 0)
     np.testing.assert_array_equal(res[0][0], res[1][0])
     np.testing.assert_array_equal(res[0][1], res[1][1])
+
+
+@pytest.mark.parametrize("B", [3, 20, 32])
+def test_f32b_ksplit_matches_unsplit(eng, B):
+    """Round 3: fp32 c_attn and mlp c_proj split over K (partials summed by the attention / folded by the
+    rows kernel; default) against the one-launch forms (option exp bit 1024: c_attn one launch; bit 512:
+    mlp c_proj unsplit too, LayerNorm in the GEMM prologue). Ragged batch: same ids, logits within fp32
+    summation-order noise (B = 3: the split-KV attention with the K-split c_attn partials)."""
+    rng = np.random.default_rng(100 + B)
+    n = 24
+    texts = rng.integers(3, 384, size=(B, n)).astype(np.int32)
+    dev = eng.device
+    res = []
+    for exp in (0, 1024, 1536):
+        eng.set_option("exp", exp)
+        try:
+            for s in range(B):
+                eng.reset_slot(s)
+            pre = torch.from_numpy(texts[::2].copy()).to(dev)  # even rows first run 8 steps alone
+            Bp = pre.shape[0]
+            eng.ar_steps(8, torch.arange(0, B, 2, dtype=torch.int32, device=dev), pre,
+                         torch.zeros(Bp, dtype=torch.int32, device=dev), torch.zeros(Bp, n, dtype=torch.int32, device=dev))
+            rowstep = torch.tensor([8 if b % 2 == 0 else 0 for b in range(B)], dtype=torch.int32, device=dev)
+            tok = torch.zeros(B, n, dtype=torch.int32, device=dev)
+            eng.ar_steps(14, torch.arange(B, dtype=torch.int32, device=dev), torch.from_numpy(texts).to(dev), rowstep, tok)
+            eng.check_errors()
+            res.append((tok.cpu().numpy(), eng.last_logits(B).cpu().numpy()))
+        finally:
+            eng.set_option("exp", 0)
+    for r in res[1:]:
+        np.testing.assert_array_equal(res[0][0], r[0])
+        d = float(np.abs(res[0][1] - r[1]).max())
+        print(f"\n[f32b K-split vs one launch, B={B}] max |dlogit| {d:.3g}")
+        assert d < 1e-5

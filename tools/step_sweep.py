@@ -2,13 +2,15 @@
 option sets; each config measured 3 times (median).
 usage: python tools/step_sweep.py B P0 'opt=v,...' ['opt=v' ...]
 LVX_SWEEP_STREAM=1: run on a torch side stream (the library then replays 16-step HIP graphs; on the
-default (null) stream it launches every kernel). LVX_SWEEP_KV=fp8: fp8 KV cache (configs[4])."""
+default (null) stream it launches every kernel). LVX_SWEEP_KV=fp8: fp8 KV cache (configs[4]).
+LVX_SWEEP_W=fp32: the fp32 parity mode (fp32 weights and KV)."""
 import os, statistics, sys, time
 import torch
 from llmvox_amd.engine import build_engine
 
 B, P0 = int(sys.argv[1]), int(sys.argv[2])
-e = build_engine(0, "bf16", os.environ.get("LVX_SWEEP_KV", "bf16"), max_streams=B, max_positions=P0 + 512, max_codec_frames=256)
+WD = os.environ.get("LVX_SWEEP_W", "bf16")
+e = build_engine(0, WD, "fp32" if WD == "fp32" else os.environ.get("LVX_SWEEP_KV", "bf16"), max_streams=B, max_positions=P0 + 512, max_codec_frames=256)
 dev = e.device
 plan = torch.full((B, P0 + 256), 100, dtype=torch.int32, device=dev)
 slots = torch.arange(B, dtype=torch.int32, device=dev)
