@@ -2423,12 +2423,13 @@ __global__ __launch_bounds__(256) void ar_qkv_ksplit_f32_kernel(GemvArgs a) {
 
 int g_opt_f32b = 1;  // 1: batched fp32 parity steps (3 <= B <= 64) on exact-fp32 MFMA; 0: the GEMV family
 
-// 32-row batch tiles (NT = 2) where N gives the grid enough blocks; the N = 768 ops (c_proj, mlp
-// c_proj: 48 blocks of 32 rows, each loading all 32 operand rows) run 16-row tiles (96 blocks): a
-// block's time is the bytes it loads. Same bits either way (a column's dot product is its own).
+// 16-row batch tiles (NT = 1) for every op: a block's time is the bytes it loads (the N = 768 ops:
+// 96 blocks of 16 rows instead of 48 of 32; round 3, c_fc and lm_head too: B = 32 248.3 -> 246.0
+// us/step at t = 384-639). Option exp bit 8: 32-row tiles (NT = 2) at B > 16, the cross-check. Same
+// bits either way (a column's dot product is its own).
 template <int K, int IN, int OUT, int KTOT = K>
 static void launch_f32b(const GemvArgs& a, hipStream_t s) {
-  const bool nt1 = a.B <= 16 || (a.N <= D && !(g_opt_exp & 8));
+  const bool nt1 = a.B <= 16 || !(g_opt_exp & 8);
   dim3 grid((a.N + 15) / 16, nt1 ? (a.B + 15) / 16 : (a.B + 31) / 32, KTOT / K), block(K / 192 * 64);
   if (nt1) hipLaunchKernelGGL((ar_f32b_kernel<K, 1, IN, OUT, KTOT>), grid, block, 0, s, a);
   else hipLaunchKernelGGL((ar_f32b_kernel<K, 2, IN, OUT, KTOT>), grid, block, 0, s, a);

@@ -114,8 +114,8 @@ def test_f32b_rows_independent_of_batch_position(eng):
 
 @pytest.mark.parametrize("B", [17, 32])
 def test_f32b_tile_and_direct_rows_bit_identical(eng, B):
-    """Round 3: the N = 768 fp32 GEMMs (c_proj, mlp c_proj) run 16-row batch tiles (option exp bit 8:
-    32-row tiles): the same arithmetic either way, bit for bit (ragged batch). (At these B the
+    """Round 3: the fp32 GEMMs run 16-row batch tiles (option exp bit 8: 32-row tiles at B > 16):
+    the same arithmetic either way, bit for bit (ragged batch). (At these B the
     attention runs one split and writes the normalised rows c_proj stages, IN 4: held to the
     reference's ids by the golden tests above.)"""
     rng = np.random.default_rng(B)
