@@ -1513,6 +1513,9 @@ __global__ __launch_bounds__(256) void ar_rows_kernel(GemvArgs a) {
 // ar_argmax_kernel commit, streaming_server.py:342-347) and then the embedding + LayerNorm of the
 // token it picked (ar_rows_kernel<3>). Four waves split the 4096 logits (one round trip with the
 // row's control records), wave 0 commits and builds the operand row.
+// F32OUT (the batched fp32 parity mode): the LayerNorm'd row in fp32 into st.h (ar_rows_kernel<6>'s
+// output, read by ar_qkv_ksplit_f32_kernel)
+template <bool F32OUT = false>
 __global__ __launch_bounds__(256) void ar_embed_select_kernel(GemvArgs a) {
   __shared__ float sv[4], sv2[4];
   __shared__ int si[4];
@@ -1570,11 +1573,16 @@ __global__ __launch_bounds__(256) void ar_embed_select_kernel(GemvArgs a) {
 #pragma unroll
   for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = v[j];
   wave_ln_regs(v, g);
-  uint2* dst = reinterpret_cast<uint2*>(a.st.xn + (size_t)b * D);
+  if constexpr (F32OUT) {
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    if (a.xpk) *reinterpret_cast<uint2*>(a.st.xn + xfrag(b, j * 256 + lane * 4, D)) = pack4_bf16(v[j]);
-    else dst[j * 64 + lane] = pack4_bf16(v[j]);
+    for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.h + (size_t)b * D + j * 256 + lane * 4) = v[j];
+  } else {
+    uint2* dst = reinterpret_cast<uint2*>(a.st.xn + (size_t)b * D);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (a.xpk) *reinterpret_cast<uint2*>(a.st.xn + xfrag(b, j * 256 + lane * 4, D)) = pack4_bf16(v[j]);
+      else dst[j * 64 + lane] = pack4_bf16(v[j]);
+    }
   }
   // the plan load for the next text id last: waiting for it earlier held the embedding loads
   if (take && lane == 0) a.st.rowx[b] = make_int2(rx.x + 1, plan_tok(a.st, b, rx.x + 2));
@@ -2296,12 +2304,21 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_f32b_kernel(GemvArgs a) {
     else merge(std::integral_constant<int, NSPLIT>{});
   } else if constexpr (IN == 4) {
     // one round trip: the rows as the attention normalised them (the merge of one split: the same
-    // product o * (1 / l), the same bits)
-    for (int e = tid; e < R * D; e += NTH) {
-      const int bb = e / D, c = e - bb * D;
-      const int b = min(r0 + bb, B - 1);
-      const int head = c / HD, d = c - head * HD;
-      xs[bb * LDX + c] = a.st.part_o[(size_t)(b * N_HEAD + head) * NSPLIT * HD + d];
+    // product o * (1 / l), the same bits), 16 B per load, all in flight (round 3: the 4-B loads of a
+    // strided loop were issued a few at a time: c_proj 12.4 us at B = 32)
+    constexpr int NL = R * D / 4 / NTH;
+    static_assert(R * D / 4 % NTH == 0, "whole float4 loads per thread");
+    float4 rv[NL];
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int e = (tid + i * NTH) * 4, bb = e / D, c = e - bb * D;
+      const int b = min(r0 + bb, B - 1), head = c / HD, d = c - head * HD;
+      rv[i] = *reinterpret_cast<const float4*>(a.st.part_o + (size_t)(b * N_HEAD + head) * NSPLIT * HD + d);
+    }
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int e = (tid + i * NTH) * 4, bb = e / D, c = e - bb * D;
+      *reinterpret_cast<float4*>(xs + bb * LDX + c) = rv[i];
     }
   } else if constexpr (IN == 6) {
     // the rows kernel's LayerNorm'd rows, 16 B per thread and load, all in flight (padded rows:
@@ -2506,7 +2523,7 @@ static void launch_op_bt(int op, GemvArgs& a, const ArWeights& w, int l, int kvd
     case 0:
       a.W = w.w_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
       if (l == 0 && a.defer_sel == 2) {  // embedding + the previous step's select, then c_attn
-        hipLaunchKernelGGL(ar_embed_select_kernel, dim3(B), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(ar_embed_select_kernel<>, dim3(B), dim3(256), 0, s, a);
         launch_bt<768, 1, 0>(a, s);
       } else if (l == 0) {
         launch_bt<768, 3, 0>(a, s);
@@ -2534,11 +2551,16 @@ static bool defer_select(int B) {
   return g_opt_defer_select && B <= 2 && !use_mfma<TW>(B);
 }
 template <typename TW>
+static bool use_f32b(int B);
+static bool f32b_qsplit(int B);
+template <typename TW>
 static bool defer_select_batched(int B) {
   // us/step (tools/step_sweep.py, t = 256+) argmax kernel / deferred: B = 3: 112.9 / 114.7 (B = 3
   // keeps the argmax kernel), B = 4: 106.0 / 104.9, 8: 120.7 / 118.3, 12: 123.0 / 120.5,
   // 16: 128.4 / 125.5, 32: 150.3 / 147.3, 64: 213.4 / 206.8
-  return g_opt_defer_select && ((use_mfma<TW>(B) && B >= 4) || use_bt<TW>(B));
+  // fp32 parity mode (round 3): with the K-split c_attn (its layer-0 rows kernel becomes
+  // ar_embed_select_kernel<true>); B = 32 t = 384-639: 213.9 -> 210.8 us/step
+  return g_opt_defer_select && ((use_mfma<TW>(B) && B >= 4) || use_bt<TW>(B) || (use_f32b<TW>(B) && B >= 4 && f32b_qsplit(B)));
 }
 
 // measured at B = 1 (round 1): 16 h rows per block (192 blocks) 76.7 us/step; 32 rows (96 blocks)
@@ -2578,6 +2600,7 @@ static bool use_f32b(int B) {
 // the 16-wave blocks each loaded 392 KB on 96 CUs); the rows kernel before c_attn (layers >= 1) and
 // lm_head folds them into x and leaves the LayerNorm'd fp32 rows the GEMM stages (IN 6). Option exp
 // bit 512: the unsplit mlp c_proj with x final at every boundary and the LayerNorm in the GEMM prologue.
+static bool f32b_qsplit(int B) { return !(g_opt_exp & 512) && B <= 32 && !(g_opt_exp & 1024); }
 static void launch_op_f32b(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtype, int B, hipStream_t s) {
   const bool ksp = !(g_opt_exp & 512);
   a.layer = l;
@@ -2585,12 +2608,13 @@ static void launch_op_f32b(int op, GemvArgs& a, const ArWeights& w, int l, int k
   a.add_y = 0;
   a.xpk = 0;
   // c_attn split over K too (B <= 32), its partials summed by the attention; option exp bit 1024: one launch
-  const bool qsp = ksp && B <= 32 && !(g_opt_exp & 1024);
+  const bool qsp = f32b_qsplit(B);
   switch (op) {
     case 0:
       a.W = w.w_attn[l]; a.Wf = w.f_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
       if (qsp) {  // rows kernel (layer 0: embedding; else x + the MLP copies) -> fp32 rows, then the K slices
-        if (l == 0) hipLaunchKernelGGL((ar_rows_kernel<6>), dim3(B), dim3(64), 0, s, a);
+        if (l == 0 && a.defer_sel == 2) hipLaunchKernelGGL(ar_embed_select_kernel<true>, dim3(B), dim3(256), 0, s, a);
+        else if (l == 0) hipLaunchKernelGGL((ar_rows_kernel<6>), dim3(B), dim3(64), 0, s, a);
         else hipLaunchKernelGGL((ar_rows_kernel<5>), dim3(B), dim3(64), 0, s, a);
         if (B <= 16) hipLaunchKernelGGL((ar_qkv_ksplit_f32_kernel<1>), dim3(3 * D / 64, 4), dim3(256), 0, s, a);
         else hipLaunchKernelGGL((ar_qkv_ksplit_f32_kernel<2>), dim3(3 * D / 64, 4), dim3(256), 0, s, a);
@@ -2668,7 +2692,7 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
     case 0:
       a.W = w.w_attn[l]; a.Wf = pk ? w.f_attn[l] : nullptr; a.N = 3 * D; a.ln_w = w.ln1[l];
       if (mf && l == 0 && a.defer_sel == 2) {  // embedding + the previous step's select, then c_attn
-        hipLaunchKernelGGL(ar_embed_select_kernel, dim3(B), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(ar_embed_select_kernel<>, dim3(B), dim3(256), 0, s, a);
         if (qkv_ksplit<TW>(B, kvdtype)) launch_qkv_ksplit(a, s);
         else launch_mfma2<768, 0>(a, s);
       } else if (mf && B <= MFMA_LN_MAX) {
@@ -2866,7 +2890,7 @@ int ar_select_probe(const ArWeights& w, const ArState& st, int B, int path, hipS
   } else {
     GemvArgs a = make_args<float>(w, st, LVX_DTYPE_F32, B, nullptr);
     a.ln_w = w.ln1[0];
-    hipLaunchKernelGGL(ar_embed_select_kernel, dim3(B), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(ar_embed_select_kernel<>, dim3(B), dim3(256), 0, s, a);
   }
   return 0;
 }
