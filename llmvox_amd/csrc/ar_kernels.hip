@@ -97,6 +97,7 @@ struct GemvArgs {
                             // accumulators in 2^-32 fixed point (int64 atomics: order-independent sums)
   const float* gsum;     // batched c_fc (ar_mfma2_kernel XM 1): ArWeights::fc_gsum of the layer
   int add_y;             // c_proj: fold the accumulators into x (layers >= 1; 0 at layer 0 = just clear)
+  int epi_late;          // ar_mfma2_kernel OUT 1: x and the copies loaded in the epilogue (option exp bit 4096, A/B)
   int defer_sel;         // deferred greedy select (option "defer_select"). 1: B <= 2 GEMV step, lm_head
                          // publishes per-block granules, the next step's c_attn layer 0 reduces them;
                          // 2: batched step, the next step's embedding rows kernel reduces the logits
@@ -1681,9 +1682,31 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   constexpr int EPT = (16 * NT * 16 + NW * 64 - 1) / (NW * 64);
   static_assert((NW * 64) % (NT * 16) == 0, "one batch row per thread in the epilogue");
   int4 ripre = make_int4(-1, 0, 0, 0);
-  float xpre[OUT == 7 ? EPT : 1];
+  float xpre[(OUT == 7 || OUT == 1) ? EPT : 1];
   float gpre[(OUT == 7 || XM == 1) ? EPT : 1];  // OUT 7: ln_2.weight[n]; XM 1: G[n]
   if constexpr (OUT == 0) ripre = a.st.rowinfo[min(r0 + tid % (NT * 16), B - 1)];
+  if constexpr (OUT == 1) {
+    // (B <= 8 c_proj) x and the MLP's pending copies up front, summed in gemv_store<1>'s order
+    // (x + c0 + c1 + c2 + c3, then + v): round 3, they were loaded in the epilogue, one more
+    // dependent round trip after the MFMAs. The copies are loaded whether or not they are folded
+    // (add_y: layers >= 1): no load under a branch.
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+      const int e = min(tid + k * NW * 64, 16 * NT * 16 - 1), r = e / (NT * 16), b = min(r0 + e - r * (NT * 16), B - 1);
+      const int n = min(n0 + r, a.N - 1);
+      float t = a.st.x[(size_t)b * D + n];
+      // (a.yacc is set on every MFMA step; a null one reads x itself, never folded)
+      const float* yp = a.yacc ? a.yacc + (size_t)b * YCOPIES * D + n : a.st.x + (size_t)b * D + n;
+      const int ys = a.yacc ? D : 0;
+      float yc[YCOPIES];
+#pragma unroll
+      for (int c = 0; c < YCOPIES; ++c) yc[c] = yp[c * ys];
+      if (a.yacc && a.add_y)
+#pragma unroll
+        for (int c = 0; c < YCOPIES; ++c) t += yc[c];
+      xpre[k] = t;
+    }
+  }
   if constexpr (OUT == 7 || XM == 1) {
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
@@ -1794,6 +1817,8 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
       xo[e] = xn;
     } else if (OUT == 6) {  // split-K partial of mlp c_proj (K slice by) -> pending copy
       a.yacc[((size_t)b * YCOPIES + by) * D + n] = v;
+    } else if (OUT == 1 && !a.epi_late) {  // x (+ the folded copies, prefetched) + v
+      a.st.x[(size_t)b * D + n] = xpre[k] + v;
     } else {
       gemv_store<OUT>(a, n, b, v);
     }
@@ -2685,6 +2710,7 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
   // fragment-packed operand rows on the v2 steps with the rows kernel (9 <= B <= 32; exp bit 4: row-major)
   a.xpk = (mf && B > MFMA_LN_MAX && B <= 32 && !(g_opt_exp & 4)) ? 1 : 0;
   a.layer = l;
+  a.epi_late = (g_opt_exp & 4096) ? 1 : 0;
   a.yacc = mf ? a.st.yacc : nullptr;
   a.yfx = fm ? a.st.yfx : nullptr;
   a.add_y = l > 0;
