@@ -330,6 +330,20 @@ __device__ __forceinline__ void xrow_sum(const XRow<IN, FX>& r, float4 (&v)[3]) 
   }
 }
 
+// Kernels whose grid fills a fraction of the chip (B rows, 144 K-split blocks): with the default
+// occupancy target the scheduler keeps few VGPRs live and issues part of the loads only after the
+// first ones have landed (rows kernel: 12 loads, a wait, then gamma and 3 row loads; the K-split
+// c_attn: weights two at a time), one more dependent round trip. Capping the target at 4 waves per
+// SIMD (128 VGPRs) leaves them all in flight at once (round 3, checked in the ISA). Measured
+// (tools/step_sweep.py, B = 32, t = 384-639, two A/B rounds on one box): bf16 129.2 / 133.0 vs
+// 130.5 / 129.9 us/step, fp32 210.8 / 211.3 vs 211.5 / 211.3: within the noise; the late loads (gamma,
+// lines already on their way to L2) return quickly.
+#ifdef LVX_NO_LOADS_FIRST  // A/B builds (tools/build_variant.sh)
+#define LVX_LOADS_FIRST
+#else
+#define LVX_LOADS_FIRST __attribute__((amdgpu_waves_per_eu(1, 4)))
+#endif
+
 template <int K, int IN>
 __device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, float* aux, const float4 (&gam)[3], int g0, int bg,
                                                  const XRow<IN == 4 ? 4 : 0, true>& xpre, int4 ripre, bool prefetched) {
@@ -1441,22 +1455,24 @@ __device__ __forceinline__ void embed_row(const GemvArgs& a, int4 ri, int lane, 
     return;
   }
   const int p = ri.y, prev = ri.w;
-  int tok = ri.z;
-  if (tok < 0) {
-    if (lane == 0) atomicOr(a.st.err, 2);
-    tok = 384;
-  }
+  const int tok = ri.z < 0 ? 384 : ri.z;
+  // every load issued before any branch or use (the error flag's atomic and the position-0 zeros
+  // came between them: one load went out a round trip late); prev is a valid codebook row
   float4 pe[3];
   const float* wr_ = a.wpe + (size_t)p * D;
 #pragma unroll
   for (int j = 0; j < 3; ++j) pe[j] = *reinterpret_cast<const float4*>(wr_ + j * 256 + lane * 4);
-  float ss = 0.f;
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int k = j * 256 + lane * 4;
-    if (j == 0) v[j] = *reinterpret_cast<const float4*>(a.text_table + (size_t)tok * TEXT_DIM + k);
-    else if (p == 0) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-    else v[j] = *reinterpret_cast<const float4*>(a.codebook + (size_t)prev * SPEECH_DIM + (k - TEXT_DIM));
+    v[j] = j == 0 ? *reinterpret_cast<const float4*>(a.text_table + (size_t)tok * TEXT_DIM + k)
+                  : *reinterpret_cast<const float4*>(a.codebook + (size_t)prev * SPEECH_DIM + (k - TEXT_DIM));
+  }
+  if (ri.z < 0 && lane == 0) atomicOr(a.st.err, 2);
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    if (j > 0 && p == 0) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
     ss += (v[j].x * v[j].x + v[j].y * v[j].y) + (v[j].z * v[j].z + v[j].w * v[j].w);
   }
   const float den = fmaxf(sqrtf(wave_sum(ss)), 1e-8f);
@@ -1465,12 +1481,13 @@ __device__ __forceinline__ void embed_row(const GemvArgs& a, int4 ri, int lane, 
     v[j] = make_float4(v[j].x / den + pe[j].x, v[j].y / den + pe[j].y, v[j].z / den + pe[j].z, v[j].w / den + pe[j].w);
 }
 
+
 // 0: LayerNorm(x)  4: LayerNorm(x + pending copies)  3: embedding (+ stores x) then LayerNorm
 // 5: as 4 with fp32 output rows in st.h ([B][768]; the batched fp32 parity mode's c_attn / lm_head
 // operand, ar_qkv_ksplit_f32_kernel / ar_f32b_kernel IN 6: h is free between mlp c_proj and the next
 // c_fc)  6: as 3 with the fp32 output rows of 5
 template <int MODE>
-__global__ __launch_bounds__(256) void ar_rows_kernel(GemvArgs a) {
+__global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_rows_kernel(GemvArgs a) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int b = blockIdx.x * (blockDim.x >> 6) + wave;
   if (b >= a.B) return;
@@ -1517,7 +1534,7 @@ __global__ __launch_bounds__(256) void ar_rows_kernel(GemvArgs a) {
 // F32OUT (the batched fp32 parity mode): the LayerNorm'd row in fp32 into st.h (ar_rows_kernel<6>'s
 // output, read by ar_qkv_ksplit_f32_kernel)
 template <bool F32OUT = false>
-__global__ __launch_bounds__(256) void ar_embed_select_kernel(GemvArgs a) {
+__global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_embed_select_kernel(GemvArgs a) {
   __shared__ float sv[4], sv2[4];
   __shared__ int si[4];
   const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1871,7 +1888,7 @@ static void launch_mfma2(const GemvArgs& a, hipStream_t s, bool btile = false) {
 // lane and batch tile) to st.qkvp[slice]; the attention sums the four slices in the order the
 // one-launch kernel summed its waves and appends the new key (bit-identical to ar_mfma2_kernel OUT 0).
 template <int NT>
-__global__ __launch_bounds__(256) void ar_qkv_ksplit_kernel(GemvArgs a) {
+__global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_qkv_ksplit_kernel(GemvArgs a) {
   // The batched GEMM launches are bound by the bytes each CU loads (~30 GB/s per CU from entry to
   // operands landed, tools/step_timeline.py: 72 KB per CU 2.8 us, 36 KB 1.5 us, nothing 0.5 us), so
   // the block's operand slice (NT * 16 rows x 192 columns), which all four waves multiply, is loaded
@@ -2413,7 +2430,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_f32b_kernel(GemvArgs a) {
 // st.qkvp[slice]; the attention (ar_attn_v2_kernel<float, ..., QKV>) sums the four slices in slice
 // order and appends the new key. 144 blocks of 48 + 24 KB instead of 144 of 48 + 96 KB.
 template <int NT>
-__global__ __launch_bounds__(256) void ar_qkv_ksplit_f32_kernel(GemvArgs a) {
+__global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_qkv_ksplit_f32_kernel(GemvArgs a) {
   constexpr int XR = NT * 16, XS = 196;  // rows, fp32 row stride (784 B: 16 rows 4 banks apart)
   __shared__ __attribute__((aligned(16))) float xs[XR * XS];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
