@@ -175,3 +175,29 @@ def test_f32b_ksplit_matches_unsplit(eng, B):
         d = float(np.abs(res[0][1] - r[1]).max())
         print(f"\n[f32b K-split vs one launch, B={B}] max |dlogit| {d:.3g}")
         assert d < 1e-5
+
+
+@pytest.mark.parametrize("B", [4, 32])
+def test_f32b_deferred_select_matches_argmax_kernel(eng, B):
+    """Round 3: the fp32 batched steps defer the greedy select into the next step's embedding kernel
+    (ar_embed_select_kernel<true>, fp32 rows out) instead of an argmax kernel after lm_head (option
+    defer_select = 0): the same select rule on the same logits, so ids, margins and logits are bit-equal."""
+    rng = np.random.default_rng(200 + B)
+    n = 20
+    texts = rng.integers(3, 384, size=(B, n)).astype(np.int32)
+    dev = eng.device
+    res = []
+    for d in (1, 0):
+        eng.set_option("defer_select", d)
+        try:
+            for s in range(B):
+                eng.reset_slot(s)
+            tok = torch.zeros(B, n, dtype=torch.int32, device=dev)
+            eng.ar_steps(n, torch.arange(B, dtype=torch.int32, device=dev), torch.from_numpy(texts).to(dev),
+                         torch.zeros(B, dtype=torch.int32, device=dev), tok)
+            eng.check_errors()
+            res.append((tok.cpu().numpy(), eng.last_logits(B).cpu().numpy()))
+        finally:
+            eng.set_option("defer_select", 1)
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    np.testing.assert_array_equal(res[0][1], res[1][1])
