@@ -344,7 +344,7 @@ __device__ __forceinline__ void xrow_sum(const XRow<IN, FX>& r, float4 (&v)[3]) 
 #define LVX_LOADS_FIRST __attribute__((amdgpu_waves_per_eu(1, 4)))
 #endif
 
-template <int K, int IN>
+template <int K, int IN, int BG = 0>
 __device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, float* aux, const float4 (&gam)[3], int g0, int bg,
                                                  const XRow<IN == 4 ? 4 : 0, true>& xpre, int4 ripre, bool prefetched) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -447,6 +447,33 @@ __device__ __forceinline__ void gemv_stage_input(const GemvArgs& a, float* xs, f
       for (int i = 0; i < NSPLIT; ++i) cf[i] = m[i] * inv;
     }
     __syncthreads();
+    if constexpr (BG == 2) {
+      // B = 2 (bg == 2: 6 elements per thread): all 6 x NSPLIT partial loads in flight before the
+      // first sum (the loop below waited for each element's 16 loads before issuing the next
+      // element's: 6 dependent round trips); the same sum per element. tools/step_sweep.py B = 2,
+      // t = 384-639: bf16 98.5-98.7 -> 96.3-96.5 us/step, fp32 110.9-112.3 -> 110.1-110.2
+      constexpr int IT = 2 * D / 256;
+      static_assert(2 * D % 256 == 0, "whole elements per thread");
+      float pv[IT][NSPLIT];
+#pragma unroll
+      for (int k = 0; k < IT; ++k) {
+        const int e = tid + 256 * k, bb = e / D, c = e - bb * D;
+        const int head = c / HD, d = c - head * HD;
+        const float* po = a.st.part_o + ((size_t)((g0 + bb) * N_HEAD + head) * NSPLIT) * HD + d;
+#pragma unroll
+        for (int i = 0; i < NSPLIT; ++i) pv[k][i] = po[(size_t)i * HD];
+      }
+#pragma unroll
+      for (int k = 0; k < IT; ++k) {
+        const int e = tid + 256 * k, bb = e / D, c = e - bb * D, head = c / HD;
+        const float* cf = aux + (bb * N_HEAD + head) * NSPLIT;
+        float y = 0.f;
+#pragma unroll
+        for (int i = 0; i < NSPLIT; ++i) y += cf[i] * pv[k][i];
+        xs[bb * K + c] = y;
+      }
+      return;
+    }
     for (int e = tid; e < bg * D; e += 256) {
       const int bb = e / D, c = e - bb * D;
       const int b = g0 + bb;
@@ -567,7 +594,7 @@ __global__ __launch_bounds__(256) void ar_gemv_kernel(GemvArgs a) {
   for (int g0 = 0; g0 < a.B; g0 += BG) {
     const int bg = min(BG, a.B - g0);
     if (g0) __syncthreads();
-    gemv_stage_input<K, IN>(a, xs, aux, gam, g0, bg, xpre, ripre, prefetched);
+    gemv_stage_input<K, IN, BG>(a, xs, aux, gam, g0, bg, xpre, ripre, prefetched);
     __syncthreads();
     float acc[RPW][BG];
 #pragma unroll
