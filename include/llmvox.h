@@ -120,7 +120,8 @@ int lvx_ar_logits(lvx_ctx* ctx, int B, float* dst_dev, void* stream);
  * the assertion of decoder/spectral_ops.py:72 -- the fixed periodic Hann envelope is >= 0.72 on the
  * trimmed span, so this is a self-check), a slot past max_positions (LVX_E_CAPACITY; reference:
  * the block_size AssertionError, src/model.py:205) or a row past the end of its plan
- * (LVX_E_CAPACITY). */
+ * (LVX_E_CAPACITY), or a non-finite / out-of-range (|v| >= 2^25) partial in the B <= 2 fused MLP's
+ * fixed-point accumulation (LVX_E_STATE; the reference would carry the value into its logits). */
 int lvx_check_errors(lvx_ctx* ctx, void* stream);
 /* Set a slot's position and previous token (rewind after a speculative run-ahead, or jump). */
 int lvx_stream_set(lvx_ctx* ctx, int slot, int pos, int prev_token, void* stream);
@@ -141,9 +142,10 @@ int lvx_select_probe(lvx_ctx* ctx, int path, int B, const int32_t* slots_dev, co
                      float* margin_plan_dev, void* stream);
 /* Host-side view of a slot's position (synchronises the stream). */
 int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
-/* Cross-check switches between two correct implementations of the same step (process-wide; every
- * context drops its captured graphs on its next call after a change). Defaults are the measured-
- * faster variants:
+/* Cross-check switches between two correct implementations of the same step, per context (round 4:
+ * an option set on one context never changes another context's kernels; each call binds a snapshot
+ * of its context's options, and the context drops its captured graphs on its next call after a
+ * change). Defaults are the measured-faster variants:
  *   "defer_select" 1: the greedy select is committed by the next step's first kernel (B <= 2: c_attn
  *                     layer 0 reduces lm_head's granules; B >= 4: ar_embed_select); 0: ar_argmax_kernel
  *                     after every lm_head (bit-identical results: tests/test_gpu_select.py);

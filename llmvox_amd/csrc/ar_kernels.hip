@@ -275,7 +275,16 @@ __device__ __forceinline__ void wave_ln_to_lds(float4 (&v)[3], const float4 (&ga
 // integer atomics (exact, so the sum does not depend on the order the 192 blocks arrive in: the
 // output is reproducible run to run), read back as (float)(sum of the copies) * 2^-32
 typedef unsigned long long u64x2n __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ unsigned long long yfx_of(float t) {
+// A partial outside +-2^25 (or NaN / inf) cannot be summed exactly by up to 48 adders per copy in
+// int64 (and __float2ll_rn is undefined past 2^63): it is clamped and reported (error bit 32,
+// lvx_check_errors -> LVX_E_STATE) instead of silently becoming an arbitrary finite value; the
+// reference would carry the non-finite value into its logits. Activations here are O(1)-O(100).
+constexpr float YFX_MAX = 33554432.0f;  // 2^25
+__device__ __forceinline__ unsigned long long yfx_of(float t, int32_t* err) {
+  if (!(fabsf(t) < YFX_MAX)) {
+    atomicOr(err, 32);
+    t = (t != t) ? 0.f : copysignf(YFX_MAX, t);
+  }
   return (unsigned long long)__float2ll_rn(t * 4294967296.0f);
 }
 __device__ __forceinline__ float yfx_to_f(unsigned long long s) {
@@ -853,14 +862,13 @@ __global__ __launch_bounds__(256) void ar_cproj_b1_kernel(GemvArgs a) {
 // Fused MLP for B <= 2 rows (bf16 weights; option "fuse_mlp"): block k owns h rows 16k..16k+15:
 //   h = gelu_tanh(c_fc(LayerNorm(x) * ln_2))      (its 16 rows of c_fc, 24.6 KB of weights)
 //   y += mlp.c_proj[:, 16k:16k+16] h               (its 16 columns of c_proj, thread-packed, 24.6 KB)
-// The 768-wide partial is added with no-return fp32 atomics (256 contiguous bytes per wave
-// instruction) into accumulator copy k % YCOPIES; the next c_attn / lm_head prologue reads
-// x + the copies, the next c_proj folds them into x and clears them. This removes the
-// c_fc -> c_proj kernel boundary (one of the per-layer seams, -6.7 us per step at B = 1).
-// The order in which the 48 blocks of a copy add is not fixed, so results vary run to run at
-// the 1e-7 level: option fuse_mlp = 0 selects the deterministic two-kernel path. (A 2^-32
-// fixed-point variant with 64-bit integer atomics is deterministic but gave back almost all of
-// the gain: measured 94.9 vs 95.6 us per step.)
+// The 768-wide partial is added into accumulator copy k % YCOPIES as 2^-32 fixed-point int64
+// (no-return 64-bit integer atomics, yfx_of): integer sums are exact, so the result does not depend
+// on the order the 192 blocks arrive in and a stream's tokens, margins and logits are reproducible
+// run to run (round 3; fp32 atomics had varied at the 1e-7 level). The next c_attn / lm_head
+// prologue reads x + the copies, the next c_proj folds them into x and clears them. This removes the
+// c_fc -> c_proj kernel boundary (one of the per-layer seams, -6.7 us per step at B = 1); option
+// fuse_mlp = 0 selects the two-kernel path (another summation order).
 // ---------------------------------------------------------------------------------
 template <int BG, int RB>
 __global__ __launch_bounds__(256) void ar_mlp_fused_kernel(GemvArgs a, const bf16_t* __restrict__ Wfc,
@@ -931,7 +939,7 @@ __global__ __launch_bounds__(256) void ar_mlp_fused_kernel(GemvArgs a, const bf1
         t = fmaf(__uint_as_float(u.y << 16), hs[bb][4 * g + 2], t);
         t = fmaf(__uint_as_float(u.y & 0xffff0000u), hs[bb][4 * g + 3], t);
       }
-      atomicAdd(y + (size_t)bb * YCOPIES * D + tid + 256 * jj, yfx_of(t));  // no-return int64 add
+      atomicAdd(y + (size_t)bb * YCOPIES * D + tid + 256 * jj, yfx_of(t, a.st.err));  // no-return int64 add
     }
   }
 }
@@ -1422,10 +1430,12 @@ __global__ __launch_bounds__(256) void ar_argmax_kernel(ArState st) {
 // ---------------------------------------------------------------------------------
 // Kernel-variant switches kept for cross-checks (lvx_set_option): each selects between two correct
 // implementations of the same step that tests/ compare (defaults are the measured-faster ones).
-int g_opt_defer_select = 1;  // 1: greedy select deferred into the next step's first kernel (B <= 2: c_attn
-                             // layer 0 reduces lm_head's granules; B >= 4: ar_embed_select); 0: ar_argmax_kernel
-int g_opt_fuse_mlp = 1;      // bf16, B <= 2: c_fc + gelu + mlp c_proj in one kernel (fp32 atomics, arrival
-                             // order); 0: two deterministic GEMV kernels
+// option defer_select (default 1, Opts in lvx_internal.h): 1: greedy select deferred into the next
+//   step's first kernel (B <= 2: c_attn layer 0 reduces lm_head's granules; B >= 4: ar_embed_select);
+//   0: ar_argmax_kernel
+// option fuse_mlp (default 1, Opts in lvx_internal.h): bf16, B <= 2: c_fc + gelu + mlp c_proj in one
+//   kernel, its 192 blocks' c_proj partials added as 2^-32 fixed-point int64 (exact integer sums in any
+//   arrival order: reproducible); 0: two GEMV kernels (another summation order)
 
 template <typename TW, int K, int KW, int RPW, int IN, int OUT>
 static void launch_gemv(const GemvArgs& a, hipStream_t s) {
@@ -1463,8 +1473,8 @@ constexpr int MFMA_BATCH_MIN = 3;  // smallest B on the batched MFMA path (measu
 // batched path: LayerNorm / embedding fused into the MFMA GEMM prologue for B <= this value
 // (measured: B = 8 147 vs 156 us/step; B = 32 slower, every block re-normalising 32 rows)
 // (runtime value: option "ln_max", for A/B of the two batched structures at small B)
-int g_mfma_ln_max = 8;
-#define MFMA_LN_MAX g_mfma_ln_max
+// option ln_max (default 8, Opts in lvx_internal.h):
+#define MFMA_LN_MAX (opts().ln_max)
 
 // ---------------------------------------------------------------------------------
 // Batched path v2 (bf16 weights, 4 < B <= 32): every per-row prologue runs ONCE per row into a
@@ -1698,18 +1708,23 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   __shared__ float2 rs[XM == 1 ? NT * 16 : 1];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   // XCD-aligned tile order (a.xmap, 1-D grid): workgroups are dealt to the 8 XCDs round robin, so
-  // with this order XCD x runs only the tiles of K slice x mod 4 (mlp c_proj) or of batch tile x mod 2
-  // (c_proj) and its L2 fetches only that part of the shared operand rows (the default order put
-  // every slice / batch tile on every XCD: 8 copies of all rows through the Infinity Fabric)
+  // with this order XCD x runs only the tiles of K slice x mod 4 (mlp c_proj: its L2 fetches only
+  // that part of the shared operand rows; the default order put every slice on every XCD: 8 copies
+  // of all rows through the Infinity Fabric) or both batch tiles of its weight slices (c_proj: each
+  // weight slice fetched once, the 49 KB of operand rows by every XCD)
   int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   if (a.xmap == 1) {
     const int x = bx & 7;
     by = x & 3;
     bx = (bx >> 3) * 2 + (x >> 2);
   } else if (a.xmap == 2) {
-    const int x = bx & 7;
-    bz = x & 1;
-    bx = (bx >> 3) * 4 + (x >> 1);
+    // blocks b and b + 8 share an XCD: both batch tiles of weight slice (b / 16) * 8 + b % 8 run on
+    // one XCD, so each 16-row weight slice crosses the fabric once (round 4; the round-3 order put
+    // batch tile x & 1 on XCD x and fetched every slice into two XCDs' L2s: 2.04x the algorithmic
+    // bytes)
+    const int j = bx & 15;
+    bz = j >> 3;
+    bx = (bx >> 4) * 8 + (j & 7);
   }
   const int n0 = bx * 16;
   const int r0 = bz * (NT * 16);  // first batch row of this block's tile (grid.z batch tiles)
@@ -1896,7 +1911,7 @@ static void launch_mfma2(const GemvArgs& a, hipStream_t s, bool btile = false) {
   dim3 grid((a.N + 15) / 16), block((K / 192) * 64);
   if (btile && a.B > 16) {  // 16-row batch tiles in grid.z: half the operand bytes per block
     grid.z = (a.B + 15) / 16;
-    if (grid.z == 2 && grid.x % 4 == 0 && !(g_opt_exp & 16)) {  // XCD-aligned order (xmap 2)
+    if (grid.z == 2 && grid.x % 8 == 0 && !(opts().exp & 16)) {  // XCD-aligned order (xmap 2)
       GemvArgs b = a;
       b.xmap = 2;
       hipLaunchKernelGGL((ar_mfma2_kernel<K, 1, OUT, K, XM>), dim3(grid.x * 2), block, 0, s, b);
@@ -1996,7 +2011,7 @@ static void launch_mproj_split(const GemvArgs& a, hipStream_t s) {
   static_assert(DFF == YCOPIES * 768, "one pending copy per K slice");
   dim3 grid((a.N + 15) / 16, YCOPIES), block(256);
   GemvArgs b = a;
-  if (YCOPIES == 4 && grid.x % 2 == 0 && !(g_opt_exp & 16)) {  // XCD-aligned order (xmap 1): 1-D grid
+  if (YCOPIES == 4 && grid.x % 2 == 0 && !(opts().exp & 16)) {  // XCD-aligned order (xmap 1): 1-D grid
     b.xmap = 1;
     grid = dim3(grid.x * 4);
   }
@@ -2507,7 +2522,7 @@ __global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_qkv_ksplit_f32_kernel(
   }
 }
 
-int g_opt_f32b = 1;  // 1: batched fp32 parity steps (3 <= B <= 64) on exact-fp32 MFMA; 0: the GEMV family
+// option f32b (default 1, Opts in lvx_internal.h): 1: batched fp32 parity steps (3 <= B <= 64) on exact-fp32 MFMA; 0: the GEMV family
 
 // 16-row batch tiles (NT = 1) for every op: a block's time is the bytes it loads (the N = 768 ops:
 // 96 blocks of 16 rows instead of 48 of 32; round 3, c_fc and lm_head too: B = 32 248.3 -> 246.0
@@ -2515,7 +2530,7 @@ int g_opt_f32b = 1;  // 1: batched fp32 parity steps (3 <= B <= 64) on exact-fp3
 // bits either way (a column's dot product is its own).
 template <int K, int IN, int OUT, int KTOT = K>
 static void launch_f32b(const GemvArgs& a, hipStream_t s) {
-  const bool nt1 = a.B <= 16 || !(g_opt_exp & 8);
+  const bool nt1 = a.B <= 16 || !(opts().exp & 8);
   dim3 grid((a.N + 15) / 16, nt1 ? (a.B + 15) / 16 : (a.B + 31) / 32, KTOT / K), block(K / 192 * 64);
   if (nt1) hipLaunchKernelGGL((ar_f32b_kernel<K, 1, IN, OUT, KTOT>), grid, block, 0, s, a);
   else hipLaunchKernelGGL((ar_f32b_kernel<K, 2, IN, OUT, KTOT>), grid, block, 0, s, a);
@@ -2526,8 +2541,8 @@ static void launch_f32b(const GemvArgs& a, hipStream_t s) {
 // time of these short GEMMs: B = 8 / 16 / 32 v2 149 / 162 / 191 vs v3 172 / 181 / 203 (16-row
 // tiles, separate merge); a fused merge re-reads ns_max partials per row and block: 271 / 302 / 266.
 // v3 therefore runs only where v2 has no kernels (32 < B <= 64: 250 us, 16-row tiles).
-int g_opt_exp = 0;  // development A/B bits (lvx_set_option "exp"), 0 = production kernels
-int g_opt_bt = 1;  // 1: batched path v3 for 32 < B <= 64; 2: v3 for every batched B (cross-check of v2); 0: off
+// option exp (default 0, Opts in lvx_internal.h): development A/B bits (lvx_set_option "exp"), 0 = production kernels
+// option bt (default 1, Opts in lvx_internal.h): 1: batched path v3 for 32 < B <= 64; 2: v3 for every batched B (cross-check of v2); 0: off
 
 template <int K, int IN, int OUT>
 static void launch_bt(const GemvArgs& a, hipStream_t s) {
@@ -2579,7 +2594,7 @@ static bool use_mfma(int B) {
 }
 template <typename TW>
 static bool use_bt(int B) {
-  return use_mfma<TW>(B) && g_opt_bt && (B > 32 || g_opt_bt == 2);
+  return use_mfma<TW>(B) && opts().bt && (B > 32 || opts().bt == 2);
 }
 
 // batched path v3: one kernel per op (plus the attention), final x rows at every boundary
@@ -2617,7 +2632,7 @@ static void launch_op_bt(int op, GemvArgs& a, const ArWeights& w, int l, int kvd
 template <typename TW>
 static bool defer_select(int B) {
   static_assert(LM_SEL_BLOCKS <= LM_MAX_BLOCKS && LM_SEL_BLOCKS % 64 == 0, "deferred select granules");
-  return g_opt_defer_select && B <= 2 && !use_mfma<TW>(B);
+  return opts().defer_select && B <= 2 && !use_mfma<TW>(B);
 }
 template <typename TW>
 static bool use_f32b(int B);
@@ -2629,14 +2644,14 @@ static bool defer_select_batched(int B) {
   // 16: 128.4 / 125.5, 32: 150.3 / 147.3, 64: 213.4 / 206.8
   // fp32 parity mode (round 3): with the K-split c_attn (its layer-0 rows kernel becomes
   // ar_embed_select_kernel<true>); B = 32 t = 384-639: 213.9 -> 210.8 us/step
-  return g_opt_defer_select && ((use_mfma<TW>(B) && B >= 4) || use_bt<TW>(B) || (use_f32b<TW>(B) && B >= 4 && f32b_qsplit(B)));
+  return opts().defer_select && ((use_mfma<TW>(B) && B >= 4) || use_bt<TW>(B) || (use_f32b<TW>(B) && B >= 4 && f32b_qsplit(B)));
 }
 
 // measured at B = 1 (round 1): 16 h rows per block (192 blocks) 76.7 us/step; 32 rows (96 blocks)
 // +6.8 us; 12 rows (256 blocks, one per CU) 77.4 us; 8 accumulator copies slower than 4
 template <typename TW>
 static bool fused_mlp(int B) {
-  return sizeof(TW) == 2 && g_opt_fuse_mlp && B <= 2 && !use_mfma<TW>(B);
+  return sizeof(TW) == 2 && opts().fuse_mlp && B <= 2 && !use_mfma<TW>(B);
 }
 
 // c_attn as K-slice partials summed by the attention: batched bf16 steps on the v2 kernels with the
@@ -2647,11 +2662,11 @@ static bool fused_mlp(int B) {
 // 119.1; B = 16 110.8 vs 112.2; fp8 KV B = 12 / 16 / 32 103.6 / 105.4 / 110.1 vs 105.3 / 107.3 / 111.8);
 // launched one by one on the null stream it had measured faster (B = 16 123.4 vs 126.3, B = 32
 // 149.6 vs 154.3): the K split pays only against launch gaps. Bit-identical either way.
-int g_opt_ksplit = 0;
+// option ksplit (default 0, Opts in lvx_internal.h):
 template <typename TW>
 static bool qkv_ksplit(int B, int kvdtype) {
-  return g_opt_ksplit && use_mfma<TW>(B) && !use_bt<TW>(B) && B > MFMA_LN_MAX && B <= 32 &&
-         (kvdtype == LVX_DTYPE_BF16 || kvdtype == LVX_DTYPE_FP8) && !(g_opt_exp & 1);
+  return opts().ksplit && use_mfma<TW>(B) && !use_bt<TW>(B) && B > MFMA_LN_MAX && B <= 32 &&
+         (kvdtype == LVX_DTYPE_BF16 || kvdtype == LVX_DTYPE_FP8) && !(opts().exp & 1);
 }
 static void launch_qkv_ksplit(const GemvArgs& a, hipStream_t s) {
   if (a.B <= 16) hipLaunchKernelGGL(ar_qkv_ksplit_kernel<1>, dim3(36, 4), dim3(256), 0, s, a);
@@ -2660,7 +2675,7 @@ static void launch_qkv_ksplit(const GemvArgs& a, hipStream_t s) {
 
 template <typename TW>
 static bool use_f32b(int B) {
-  return sizeof(TW) == 4 && g_opt_f32b && B >= MFMA_BATCH_MIN && B <= 64;
+  return sizeof(TW) == 4 && opts().f32b && B >= MFMA_BATCH_MIN && B <= 64;
 }
 
 // batched fp32 parity steps: five exact-fp32 MFMA kernels + the attention per layer; the split-KV
@@ -2669,9 +2684,9 @@ static bool use_f32b(int B) {
 // the 16-wave blocks each loaded 392 KB on 96 CUs); the rows kernel before c_attn (layers >= 1) and
 // lm_head folds them into x and leaves the LayerNorm'd fp32 rows the GEMM stages (IN 6). Option exp
 // bit 512: the unsplit mlp c_proj with x final at every boundary and the LayerNorm in the GEMM prologue.
-static bool f32b_qsplit(int B) { return !(g_opt_exp & 512) && B <= 32 && !(g_opt_exp & 1024); }
+static bool f32b_qsplit(int B) { return !(opts().exp & 512) && B <= 32 && !(opts().exp & 1024); }
 static void launch_op_f32b(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtype, int B, hipStream_t s) {
-  const bool ksp = !(g_opt_exp & 512);
+  const bool ksp = !(opts().exp & 512);
   a.layer = l;
   a.yacc = ksp ? a.st.yacc : nullptr;
   a.add_y = 0;
@@ -2748,13 +2763,13 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
   // key) keeps the 8-wave blocks up to B = 16: B = 12 / 16, t = 128 / 640 / 896: 95.8 / 108.3 / 114.8 ->
   // 97.0 / 105.5 / 109.6 and 95.8 / 109.6 / 115.5 -> 97.0 / 106.8 / 110.2 us; bf16 KV there loses
   // (B = 16: 97.0 / 109.9 / 128.1 -> 100.8 / 112.5 / 130.5).
-  const bool a8 = mf && B >= 5 && (B <= 8 || (kvdtype == LVX_DTYPE_FP8 && (B <= 16 || ((g_opt_exp & 128) && B <= 32)))) && !(g_opt_exp & 64);
-  const int nsm = mf ? (((B > 8 && !(g_opt_exp & 32)) || a8) ? 1 : attn_ns_max(B)) : NSPLIT;
-  const bool pk = mf && !(g_opt_exp & 2);  // fragment-packed weights for the MFMA GEMMs (exp bit 2: row-major)
+  const bool a8 = mf && B >= 5 && (B <= 8 || (kvdtype == LVX_DTYPE_FP8 && (B <= 16 || ((opts().exp & 128) && B <= 32)))) && !(opts().exp & 64);
+  const int nsm = mf ? (((B > 8 && !(opts().exp & 32)) || a8) ? 1 : attn_ns_max(B)) : NSPLIT;
+  const bool pk = mf && !(opts().exp & 2);  // fragment-packed weights for the MFMA GEMMs (exp bit 2: row-major)
   // fragment-packed operand rows on the v2 steps with the rows kernel (9 <= B <= 32; exp bit 4: row-major)
-  a.xpk = (mf && B > MFMA_LN_MAX && B <= 32 && !(g_opt_exp & 4)) ? 1 : 0;
+  a.xpk = (mf && B > MFMA_LN_MAX && B <= 32 && !(opts().exp & 4)) ? 1 : 0;
   a.layer = l;
-  a.epi_late = (g_opt_exp & 4096) ? 1 : 0;
+  a.epi_late = (opts().exp & 4096) ? 1 : 0;
   a.yacc = mf ? a.st.yacc : nullptr;
   a.yfx = fm ? a.st.yfx : nullptr;
   a.add_y = l > 0;

@@ -653,7 +653,7 @@ __global__ __launch_bounds__(256) void gemm2_splitk_reduce(GemmArgs g) {
   }
 }
 
-int g_opt_codec_g2 = 1;  // 1: large-M bf16 GEMMs on gemm_bf16_kernel; 0: on gemm_mfma (cross-check)
+// option codec_g2 (default 1, Opts in lvx_internal.h): 1: large-M bf16 GEMMs on gemm_bf16_kernel; 0: on gemm_mfma (cross-check)
 // smallest M that takes gemm_bf16_kernel (measured: M = 256 0.86 vs 1.04 ms, M = 10 0.64 vs 0.59).
 // 256-row tiles (one block per CU) measured slower (32 x 256 frames: 3.51 vs 2.99 ms; 64 x 256: 7.04
 // vs 5.16): one resident block per CU exposes the load latency that two 128-row blocks hide for each other.
@@ -906,12 +906,12 @@ __global__ __launch_bounds__(512, NS == 2 ? 2 : 1) void gemm_glds_kernel(GemmArg
   }
 }
 
-int g_opt_codec_g3 = 1;  // 1: large-M bf16 GEMMs on gemm_glds_kernel; 0: off (cross-check)
-int g_opt_codec_g3f = 1;  // 1: large-M fp32 (parity mode) GEMMs on gemm_glds_kernel<float>; 0: gemm_mfma
+// option codec_g3 (default 1, Opts in lvx_internal.h): 1: large-M bf16 GEMMs on gemm_glds_kernel; 0: off (cross-check)
+// option codec_g3f (default 1, Opts in lvx_internal.h): 1: large-M fp32 (parity mode) GEMMs on gemm_glds_kernel<float>; 0: gemm_mfma
 // the LDS-DMA kernel needs enough 128 x 192 tiles to fill the chip
 template <typename TA = bf16_t>
 static bool g3_ok(const GemmArgs& g) {
-  return g_opt_codec_g3 && g.K % (128 / (int)sizeof(TA)) == 0 && ((g.M + G3_BM - 1) / G3_BM) * ((g.N + G3_BN - 1) / G3_BN) >= 192;
+  return opts().codec_g3 && g.K % (128 / (int)sizeof(TA)) == 0 && ((g.M + G3_BM - 1) / G3_BM) * ((g.N + G3_BN - 1) / G3_BN) >= 192;
 }
 template <int AMODE, int EPI, typename TC, typename TA = bf16_t>
 static void g3_launch(GemmArgs g, hipStream_t s) {
@@ -1059,7 +1059,7 @@ static bool skinny_launch(const GemmArgs& g, hipStream_t s) {
   if (g.M <= 128) return w8 ? skinny_go<AMODE, EPI, TC, 2, 1, 8>(g, s) : skinny_go<AMODE, EPI, TC, 2, 1, 4>(g, s);
   return w8 ? skinny_go<AMODE, EPI, TC, 2, 2, 8>(g, s) : skinny_go<AMODE, EPI, TC, 2, 2, 4>(g, s);
 }
-int g_opt_codec_skinny = 1;  // 1: bf16 weight GEMMs with M <= SKINNY_MAX_M on gemm_skinny_kernel; 0: off (cross-check)
+// option codec_skinny (default 1, Opts in lvx_internal.h): 1: bf16 weight GEMMs with M <= SKINNY_MAX_M on gemm_skinny_kernel; 0: off (cross-check)
 
 // weight GEMMs: bf16 weights -> bf16 MFMA (gemm_bf16_kernel for large M); fp32 weights -> exact
 // fp32 MFMA (parity mode). TA / TC: activation types of the operand / output (bf16 only in bf16 mode)
@@ -1067,14 +1067,14 @@ template <typename TW, typename TA, int AMODE, int EPI, typename TC = float>
 static void gemm_w(const GemmArgs& g, hipStream_t s) {
   if constexpr (sizeof(TW) == 2) {
     if (g.wscale) gemm2_launch<TA, fp8_t, AMODE, EPI, TC>(g, s);  // fp8 codec weights: any M
-    else if (sizeof(TA) == 2 && g_opt_codec_skinny && g.M <= SKINNY_MAX_M && skinny_launch<AMODE, EPI, TC>(g, s))
+    else if (sizeof(TA) == 2 && opts().codec_skinny && g.M <= SKINNY_MAX_M && skinny_launch<AMODE, EPI, TC>(g, s))
       return;
     else if (sizeof(TA) == 2 && EPI != E_SCALE && g3_ok(g)) g3_launch<AMODE, (EPI == E_SCALE ? E_BIAS : EPI), TC>(g, s);
-    else if (g_opt_codec_g2 && g.M >= CODEC_G2_MIN_M) gemm2_launch<TA, bf16_t, AMODE, EPI, TC>(g, s);
+    else if (opts().codec_g2 && g.M >= CODEC_G2_MIN_M) gemm2_launch<TA, bf16_t, AMODE, EPI, TC>(g, s);
     else gemm_launch<true, TA, bf16_t, AMODE, EPI, TC>(g, 1, s);
   } else {
     static_assert(sizeof(TA) == 4 && sizeof(TC) == 4, "parity mode keeps fp32 activations");
-    if (EPI != E_SCALE && g_opt_codec_g3f && g3_ok<float>(g)) g3_launch<AMODE, (EPI == E_SCALE ? E_BIAS : EPI), float, float>(g, s);
+    if (EPI != E_SCALE && opts().codec_g3f && g3_ok<float>(g)) g3_launch<AMODE, (EPI == E_SCALE ? E_BIAS : EPI), float, float>(g, s);
     else gemm_launch<false, float, float, AMODE, EPI, float>(g, 1, s);
   }
 }
@@ -1220,10 +1220,10 @@ __global__ __launch_bounds__(256) void gn_apply1_kernel(const float* __restrict_
 }
 // codec A/B bits (development): 1 the general gn_apply at every L; 6: dwconv FT at >= 2,048 frames
 // (0: 4, 2: 16, 4: 32, 6: 8); 8: library exp / sin / cos in the bf16 iSTFT
-int g_opt_codec_exp = 0;
+// option codec_exp (default 0, Opts in lvx_internal.h):
 template <bool SWISH, typename TO>
 static void gn_apply_launch(const float* x, int B, int L, const float* gw, const float* gb, TO* y, hipStream_t s) {
-  if (L * 6 <= 8 * 256 && !(g_opt_codec_exp & 1)) hipLaunchKernelGGL((gn_apply1_kernel<SWISH, TO>), dim3(GN_G, B), dim3(256), 0, s, x, L, gw, gb, y);
+  if (L * 6 <= 8 * 256 && !(opts().codec_exp & 1)) hipLaunchKernelGGL((gn_apply1_kernel<SWISH, TO>), dim3(GN_G, B), dim3(256), 0, s, x, L, gw, gb, y);
   else hipLaunchKernelGGL((gn_apply_kernel<SWISH, TO>), dim3(GN_G, B), dim3(256), 0, s, x, L, gw, gb, y);
 }
 
@@ -1749,7 +1749,7 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
   hipLaunchKernelGGL(gn_adaln_kernel, dim3(M), dim3(256), 0, s, x, L, sc.stats, w.pn_w, w.pn_b,
                      w.ada_scale + (size_t)bw * CD, w.ada_shift + (size_t)bw * CD, x);
   for (int i = 0; i < 12; ++i) {  // ConvNeXt blocks (modules.py:43-60)
-    const int dwft = (g_opt_codec_exp >> 1) & 3;
+    const int dwft = (opts().codec_exp >> 1) & 3;
     if (M >= 2048 && dwft == 3)
       hipLaunchKernelGGL((dwconv_adaln_tile_kernel<TAct, 8>), dim3((L + 7) / 8, B), dim3(256), 0, s, x, L, w.dw_w[i],
                          w.dw_b[i], w.cn_scale[i] + (size_t)bw * CD, w.cn_shift[i] + (size_t)bw * CD, t2a);
@@ -1782,7 +1782,7 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
     h.A = t2a; h.lda = CD; h.W = w.head_w; h.wscale = w.head_s; h.bias = w.head_b; h.C = sc.spec; h.ldc = 2 * NB;
     gemm_w<TW, TAct, A_PLAIN, E_BIAS>(h, s);
   }
-  if (sizeof(TAct) == 2 && !(g_opt_codec_exp & 8))
+  if (sizeof(TAct) == 2 && !(opts().codec_exp & 8))
     hipLaunchKernelGGL(istft_frames_kernel<true>, dim3(M), dim3(256), 0, s, sc.spec,
                        reinterpret_cast<const float2*>(w.twiddle), w.window, sc.frames);
   else

@@ -22,15 +22,20 @@
 
 using namespace lvx;
 
+namespace lvx {
+static const Opts kDefaultOpts{};
+static thread_local const Opts* t_opts = nullptr;
+const Opts& opts() { return t_opts ? *t_opts : kDefaultOpts; }
+OptScope::OptScope(const Opts* o) : prev(t_opts) { t_opts = o; }
+OptScope::~OptScope() { t_opts = prev; }
+}  // namespace lvx
+
 static constexpr int kMaxCodecL = 4096;
 static constexpr int kGraphSteps = 16;  // decode steps per captured graph
 
 namespace {
 
 thread_local std::string g_err;
-// bumped by every lvx_set_option (the switches are process-wide): a context whose graphs were
-// captured under an older epoch drops them before its next replay
-std::atomic<unsigned> g_opt_epoch{0};
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -163,9 +168,17 @@ struct lvx_ctx {
   std::map<GraphKey, hipGraphExec_t> graphs;
   std::vector<hipGraph_t> graph_defs;
   bool use_graphs = true;
-  unsigned graph_epoch = 0;  // g_opt_epoch when the cached graphs were captured
+  Opts opts;                 // this context's kernel options (lvx_set_option, under mu)
+  unsigned opt_epoch = 0;    // bumped by every lvx_set_option on this context (under mu)
+  unsigned graph_epoch = 0;  // opt_epoch when the cached graphs were captured
   hipStream_t capture_stream = nullptr;  // graphs of null-stream callers are captured here
   std::mutex mu;
+
+  // a snapshot of the options, taken under mu: the caller binds it (OptScope) for its launches
+  Opts opts_snapshot() {
+    std::lock_guard<std::mutex> lk(mu);
+    return opts;
+  }
 
   template <typename T>
   int dalloc(T** p, size_t n) {
@@ -607,22 +620,23 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   if (!c || !name) return fail(LVX_E_ARG, "null argument");
   std::string n(name);
   std::lock_guard<std::mutex> lk(c->mu);
-  if (n == "defer_select") g_opt_defer_select = value != 0;
-  else if (n == "fuse_mlp") g_opt_fuse_mlp = value != 0;
-  else if (n == "bt") g_opt_bt = std::min(std::max(value, 0), 2);
-  else if (n == "codec_g2") g_opt_codec_g2 = value != 0;
-  else if (n == "codec_skinny") g_opt_codec_skinny = value != 0;
-  else if (n == "codec_g3") g_opt_codec_g3 = value != 0;
-  else if (n == "codec_g3f") g_opt_codec_g3f = value != 0;
-  else if (n == "codec_exp") g_opt_codec_exp = value;
-  else if (n == "exp") g_opt_exp = value;
-  else if (n == "f32b") g_opt_f32b = value != 0;
-  else if (n == "persist") g_opt_persist = value != 0;
-  else if (n == "pexp") g_opt_pexp = value;
-  else if (n == "ksplit") g_opt_ksplit = value != 0;
-  else if (n == "ln_max") g_mfma_ln_max = std::min(std::max(value, 2), 8);
+  Opts& o = c->opts;  // this context only (round 4: the switches were process-wide globals)
+  if (n == "defer_select") o.defer_select = value != 0;
+  else if (n == "fuse_mlp") o.fuse_mlp = value != 0;
+  else if (n == "bt") o.bt = std::min(std::max(value, 0), 2);
+  else if (n == "codec_g2") o.codec_g2 = value != 0;
+  else if (n == "codec_skinny") o.codec_skinny = value != 0;
+  else if (n == "codec_g3") o.codec_g3 = value != 0;
+  else if (n == "codec_g3f") o.codec_g3f = value != 0;
+  else if (n == "codec_exp") o.codec_exp = value;
+  else if (n == "exp") o.exp = value;
+  else if (n == "f32b") o.f32b = value != 0;
+  else if (n == "persist") o.persist = value != 0;
+  else if (n == "pexp") o.pexp = value;
+  else if (n == "ksplit") o.ksplit = value != 0;
+  else if (n == "ln_max") o.ln_max = std::min(std::max(value, 2), 8);
   else return fail(LVX_E_NAME, "unknown option " + n);
-  g_opt_epoch.fetch_add(1);  // every context's captured kernels change (checked in cached_graph)
+  ++c->opt_epoch;  // this context's captured kernels change (checked in cached_graph)
   return LVX_OK;
 }
 
@@ -668,6 +682,8 @@ int lvx_ar_forward_row(lvx_ctx* c, int slot, int pos, const float* emb_row, floa
                                     std::to_string(c->cfg.max_positions));
   if (!emb_row || !logits) return fail(LVX_E_ARG, "null emb_row/logits");
   HIP_TRY(hipSetDevice(c->cfg.device));
+  const Opts o = c->opts_snapshot();
+  OptScope os(&o);
   ar_launch_step(c->arw, c->st, c->cfg.weight_dtype, c->cfg.kv_dtype, 1, 1, emb_row, slot, pos, logits,
                  (hipStream_t)stream);
   HIP_TRY(hipGetLastError());
@@ -679,7 +695,7 @@ int lvx_ar_forward_row(lvx_ctx* c, int slot, int pos, const float* emb_row, floa
 // replayed on the null stream. Caller holds c->mu.
 static int cached_graph(lvx_ctx* c, const GraphKey& key, hipStream_t s,
                         const std::function<void(hipStream_t)>& launch, hipGraphExec_t* out) {
-  const unsigned epoch = g_opt_epoch.load();
+  const unsigned epoch = c->opt_epoch;  // (caller holds c->mu)
   if (c->graph_epoch != epoch) {  // an option changed since these graphs were captured
     for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
     c->graphs.clear();
@@ -728,6 +744,8 @@ static int ar_step_impl(lvx_ctx* c, int n_steps, int B, const int32_t* slots, co
   // null-stream callers (torch's default stream) launch the steps one by one: replaying the same
   // steps as graphs on a stream of their own measured no faster (round 1)
   if (!c->use_graphs || s == nullptr) {
+    const Opts o = c->opts_snapshot();
+    OptScope os(&o);
     for (int i = 0; i < n_steps; ++i)
       ar_launch_step(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, 0, nullptr, 0, 0, nullptr, s);
     ar_launch_steps_end(st, c->cfg.weight_dtype, B, s);
@@ -735,6 +753,8 @@ static int ar_step_impl(lvx_ctx* c, int n_steps, int B, const int32_t* slots, co
     return LVX_OK;
   }
   std::lock_guard<std::mutex> lk(c->mu);
+  const Opts o = c->opts;  // the options the cached graphs were captured under (epoch checked under mu)
+  OptScope os(&o);
   // graphs of kGraphSteps consecutive steps (one replay per kGraphSteps tokens) + 1-step graph
   auto get_graph = [&](int nst, hipGraphExec_t* out) -> int {
     GraphKey key{B, plan_stride, nst, slots, text_plan, rowstep, tok_plan, margin_plan, stream};
@@ -792,6 +812,9 @@ int lvx_check_errors(lvx_ctx* c, void* stream) {
       (void)hipStreamSynchronize((hipStream_t)stream);
       return fail(LVX_E_HIP, "a persistent decode step's dependency wait timed out (results of that call are invalid)");
     }
+    if (v & 32)
+      return fail(LVX_E_STATE, "a non-finite or out-of-range (|v| >= 2^25) partial in the fused MLP's fixed-point "
+                               "accumulation (B <= 2): its logits are invalid");
     if (v & 4) return fail(LVX_E_INDEX, "index out of range in self (a text id outside [0, 386) or a code "
                                          "outside [0, 4096) given to lvx_text_embed / lvx_codes_to_features / lvx_codec_decode_codes)");
     if (v & 8) return fail(LVX_E_STATE, "ISTFT window envelope <= 1e-11 (spectral_ops.py:72 assertion)");
@@ -808,6 +831,9 @@ int lvx_probe_kernel(lvx_ctx* c, int which, int B, const int32_t* slots, int ite
   ArState st = c->st;  // no plan bound: text_plan / rowstep / tok_plan stay null
   st.slots = const_cast<int32_t*>(slots);
   hipStream_t s = (hipStream_t)stream;
+  std::lock_guard<std::mutex> lk(c->mu);
+  const Opts o = c->opts;
+  OptScope os(&o);
   // a dry run (no launches) validates the op id / fused case before anything is captured
   const int pr = ar_probe(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, which, 0, s);
   if (pr < 0) return fail(LVX_E_ARG, "unknown probe kernel id");
@@ -820,7 +846,6 @@ int lvx_probe_kernel(lvx_ctx* c, int which, int B, const int32_t* slots, int ite
   // the `iters` launches are replayed as one graph, as the decode step is: launched one by one
   // from the host, back-to-back kernels of 3-5 us measured the host's launch rate as much as
   // the kernel (the first call of a (op, B, slots, iters) captures; time the second)
-  std::lock_guard<std::mutex> lk(c->mu);
   GraphKey key{B, -1 - which, iters, slots, nullptr, nullptr, nullptr, nullptr, stream};
   hipGraphExec_t gx;
   if (int r = cached_graph(c, key, s, [&](hipStream_t cs) {
@@ -850,6 +875,8 @@ int lvx_select_probe(lvx_ctx* c, int path, int B, const int32_t* slots, const fl
   st.tok_plan = tok_plan;
   st.margin_plan = margin_plan;
   HIP_TRY(hipMemcpyAsync(st.logits, logits, (size_t)B * VOCAB * 4, hipMemcpyDeviceToDevice, s));
+  const Opts o = c->opts_snapshot();
+  OptScope os(&o);
   ar_select_probe(c->arw, st, B, path, s);
   HIP_TRY(hipGetLastError());
   return LVX_OK;
@@ -870,6 +897,8 @@ int lvx_codec_decode_features(lvx_ctx* c, const float* feats, int B, int L, int 
   if (int r = codec_check(c, B, L, bw)) return r;
   if (!feats || !pcm) return fail(LVX_E_ARG, "null feats/pcm");
   HIP_TRY(hipSetDevice(c->cfg.device));
+  const Opts o = c->opts_snapshot();
+  OptScope os(&o);
   codec_launch_decode(c->cw, c->cs, c->cfg.weight_dtype, feats, nullptr, B, L, bw, pcm, (hipStream_t)stream);
   HIP_TRY(hipGetLastError());
   return LVX_OK;
@@ -880,6 +909,8 @@ int lvx_codec_decode_codes(lvx_ctx* c, const int32_t* codes, int B, int L, int b
   if (int r = codec_check(c, B, L, bw)) return r;
   if (!codes || !pcm) return fail(LVX_E_ARG, "null codes/pcm");
   HIP_TRY(hipSetDevice(c->cfg.device));
+  const Opts o = c->opts_snapshot();
+  OptScope os(&o);
   codec_launch_decode(c->cw, c->cs, c->cfg.weight_dtype, nullptr, codes, B, L, bw, pcm, (hipStream_t)stream);
   HIP_TRY(hipGetLastError());
   return LVX_OK;

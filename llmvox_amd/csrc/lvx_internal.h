@@ -24,9 +24,33 @@ __host__ __device__ inline size_t kv_at(size_t layer, size_t chunks, size_t stre
 #endif
 constexpr int YCOPIES = LVX_YCOPIES;  // accumulator copies of the fused MLP (spreads atomic contention)
 constexpr int LM_MAX_BLOCKS = 1024;  // lm_head blocks of the fused argmax tail (4096 rows / 8 per block = 512)
-extern int g_opt_defer_select, g_opt_fuse_mlp, g_opt_bt, g_opt_codec_g2, g_opt_codec_skinny, g_opt_codec_g3, g_opt_codec_g3f, g_opt_codec_exp, g_opt_exp,
-    g_opt_f32b, g_opt_persist, g_opt_pexp, g_mfma_ln_max, g_opt_ksplit;
-size_t persist_ctr_words();  // words of ArState::pctr  // cross-check switches (lvx_set_option)
+// Kernel-variant switches of ONE context (lvx_set_option; defaults = the production kernels). Each
+// C-ABI call that launches or captures kernels binds a snapshot of its context's options to the
+// calling thread for the duration of the call (OptScope); the launch helpers read them through
+// opts(). Options set on one context therefore never change another context's kernels, and a
+// launch never reads an option while another thread writes it.
+struct Opts {
+  int defer_select = 1;  // greedy select deferred into the next step's first kernel; 0: argmax kernel
+  int fuse_mlp = 1;      // bf16, B <= 2: c_fc + gelu + mlp c_proj in one kernel; 0: two GEMV kernels
+  int bt = 1;            // 1: batched v3 for 32 < B <= 64; 2: v3 for every batched B (cross-check); 0: off
+  int codec_g2 = 1, codec_skinny = 1, codec_g3 = 1, codec_g3f = 1;  // codec GEMM kernels (cross-checks)
+  int codec_exp = 0;     // codec A/B bits (bit-identical variants)
+  int exp = 0;           // AR A/B bits (bit-identical variants, tests/test_gpu_batched.py, test_gpu_f32b.py)
+  int f32b = 1;          // fp32 batched steps on exact-fp32 MFMA; 0: the GEMV family
+  int persist = 0;       // bf16, 17 <= B <= 32: the decode step as one persistent launch
+  int pexp = 0;          // persistent-step A/B bits
+  int ksplit = 0;        // batched bf16 c_attn as K-slice partials summed by the attention
+  int ln_max = 8;        // batched steps with the LayerNorm fused into the GEMM prologue for B <= ln_max
+};
+const Opts& opts();  // the calling thread's bound options (the defaults when none is bound)
+struct OptScope {    // binds `o` to this thread until the scope ends
+  explicit OptScope(const Opts* o);
+  ~OptScope();
+  OptScope(const OptScope&) = delete;
+  OptScope& operator=(const OptScope&) = delete;
+  const Opts* prev;
+};
+size_t persist_ctr_words();  // words of ArState::pctr
 
 // Device-resident AR weights. Matrices are [out][in] row-major (torch Linear layout),
 // in the context's weight dtype; vectors and gathered tables are fp32.

@@ -183,40 +183,52 @@ class TTSService:
         return errs[0] if all(e is not None for e in errs) else None
 
     # -- request side --
-    def _place(self) -> _Worker:
-        """Request k goes to device k mod G (skipping devices out of service)."""
+    def _candidates(self) -> List[_Worker]:
+        """The devices in the order request k tries them: k mod G first, then round robin."""
         with self._rr:
-            for _ in range(len(self.workers)):
-                w = self.workers[self._next % len(self.workers)]
-                self._next += 1
-                if w.error is None:
-                    return w
-        raise RuntimeError("TTS scheduler thread failed") from self.workers[0].error
+            k = self._next
+            self._next += 1
+        G = len(self.workers)
+        return [self.workers[(k + i) % G] for i in range(G)]
 
     def submit(self, text: str) -> _Session:
-        w = self._place()
+        """Open the request's two replica streams on the first device (round robin from k mod G)
+        that is in service and has two free KV slots. Requests run for different lengths, so the
+        devices fill unevenly: a full device passes the request on instead of refusing it (ADVICE
+        r03); only when no device has room is it refused."""
         queues = [Queue(), Queue()]
-        with w.lock:
-            if len(w.sched.free_slots) < 2:
-                raise RuntimeError("no free KV slots: too many concurrent requests")
-            streams = [w.sched.open_stream(index=i, dump_size=self.dumps[i], sink=queues[i], eoa_id=self.eoa_id)
-                       for i in range(2)]
-            s = _Session(streams, queues, w)
+        in_service = False
+        for w in self._candidates():
+            if w.error is not None:
+                continue
+            in_service = True
+            with w.lock:
+                if w.error is not None or len(w.sched.free_slots) < 2:
+                    continue
+                return self._open(w, text, queues)
+        if not in_service:
+            raise RuntimeError("TTS scheduler thread failed") from self.workers[0].error
+        raise RuntimeError("no free KV slots: too many concurrent requests")
 
-            class _Feed:  # route_text puts words on "queues"; here they go straight to the streams
-                def __init__(self, st):
-                    self.st = st
+    def _open(self, w: _Worker, text: str, queues) -> _Session:  # (caller holds w.lock)
+        streams = [w.sched.open_stream(index=i, dump_size=self.dumps[i], sink=queues[i], eoa_id=self.eoa_id)
+                   for i in range(2)]
+        s = _Session(streams, queues, w)
 
-                def put(self, word):
-                    self.st.feed(word)
+        class _Feed:  # route_text puts words on "queues"; here they go straight to the streams
+            def __init__(self, st):
+                self.st = st
 
-            if self.stream_model is None:
-                route_text(text.split() + [self.eos], [_Feed(streams[0]), _Feed(streams[1])], eos=self.eos)
-            else:  # the LLM's reply, routed as it streams (text_streamer_producer on its own thread)
-                threading.Thread(target=self._produce, args=(text, s), name="lvx-llm-producer",
-                                 daemon=True).start()
-            w.sessions.append(s)
-            w.lock.notify_all()
+            def put(self, word):
+                self.st.feed(word)
+
+        if self.stream_model is None:
+            route_text(text.split() + [self.eos], [_Feed(streams[0]), _Feed(streams[1])], eos=self.eos)
+        else:  # the LLM's reply, routed as it streams (text_streamer_producer on its own thread)
+            threading.Thread(target=self._produce, args=(text, s), name="lvx-llm-producer",
+                             daemon=True).start()
+        w.sessions.append(s)
+        w.lock.notify_all()
         return s
 
     def _produce(self, prompt: str, s: _Session):

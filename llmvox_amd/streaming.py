@@ -467,11 +467,17 @@ class FusedScheduler:
             from ._lib import LvxCapacityError
             if not isinstance(e, LvxCapacityError):
                 raise
-            edge = {st for st in ready if st.m.position + n >= self.engine.max_positions}
-            if not edge:  # not a position overflow of a known row (e.g. a plan overrun): nothing is trusted
+            # a row that ran past max_positions had its last positions clamped: those tokens are
+            # invalid. A row that ends exactly AT max_positions set the flag with the commit of its
+            # last step, but all n of its tokens came from positions <= max_positions - 1: they are
+            # valid and consumed below; the row is then reported at capacity with the others
+            P = self.engine.max_positions
+            edge = {st for st in ready if st.m.position + n > P}
+            at_cap = {st for st in ready if st.m.position + n == P}
+            if not edge and not at_cap:  # not a position overflow of a known row (e.g. a plan overrun)
                 raise
             cap_err = e
-            cap_err.streams = sorted(edge, key=lambda st: st.slot)
+            cap_err.streams = sorted(edge | at_cap, key=lambda st: st.slot)
         dumps = []  # (stream, tokens)
         order: Dict[FusedStream, List[tuple]] = {st: [] for st in ready}
         for r, st in enumerate(ready):

@@ -111,6 +111,24 @@ def test_multidevice_service_matches_single_device_bytes(G):
         assert len(a) > 0 and a == b
 
 
+def test_full_device_passes_the_request_on():
+    """a request whose round-robin device has no two free KV slots goes to the next device
+    with room (devices fill unevenly), with the same bytes; only when no device has room is it refused."""
+    ref, _ = _serve(StateEngine(max_streams=16), TEXTS[:3])
+    got, placed = _serve([StateEngine(max_streams=2, name="small"), StateEngine(max_streams=8, name="big")], TEXTS[:3])
+    assert placed == [0, 1, 1]  # request 2's turn is device 0, which request 0 filled
+    assert got == ref and all(len(r) > 0 for r in ref)
+    from llmvox_amd.server import TTSService
+    svc = TTSService([StateEngine(max_streams=2), StateEngine(max_streams=2)], max_chunk=16, max_tokens=40)
+    try:
+        a, b = svc.submit(TEXTS[0]), svc.submit(TEXTS[1])
+        assert {a.worker.index, b.worker.index} == {0, 1}
+        with pytest.raises(RuntimeError, match="no free KV slots"):
+            svc.submit(TEXTS[2])
+    finally:
+        svc.shutdown()
+
+
 def test_multidevice_service_with_end_of_audio_switches():
     """With an end-of-audio id the segments end and the replicas switch (chunk -> switch -> other
     replica -> switch back -> end): still the same bytes on 1 and on 2 devices."""
@@ -149,6 +167,32 @@ def test_capacity_error_keeps_the_other_streams_complete():
     while len(c.tokens) < len(b.tokens):
         sch2.run_chunk()
     assert c.tokens[:len(b.tokens)] == b.tokens
+
+
+def test_row_ending_exactly_at_capacity_keeps_its_tokens():
+    """a row whose chunk ends exactly at max_positions (its last step ran at position
+    P - 1) sets the capacity flag with its last commit, but all its tokens are valid: they are consumed
+    and delivered, and the stream is then reported at capacity."""
+    eng = StateEngine(max_streams=4, max_positions=64)
+    sch = S.FusedScheduler(eng, max_chunk=8, to_bytes=False)
+    a = sch.open_stream(index=0, dump_size=4)
+    for w in "some words that keep going for a long while.".split():
+        a.feed(w)
+    eng.set_slot(a.slot, 60, 7)  # the 4-token chunk runs positions 60..63 = P - 1
+    a.m.gen_index = 60
+    with pytest.raises(LvxCapacityError) as ei:
+        sch.run_chunk()
+    assert ei.value.streams == [a]
+    assert len(a.tokens) == 4
+    pcm = [x for x in a.events if isinstance(x, np.ndarray)]
+    assert sum(len(x) for x in pcm) == 320 * 4
+    ref = StateEngine(max_streams=4, max_positions=64)
+    toks = []
+    prev = 7
+    for j, p in enumerate(range(60, 64)):
+        prev = ref._tok(int(sch.plan_h[0, j]), prev, p)
+        toks.append(prev)
+    assert a.tokens == toks
 
 
 def test_capacity_edge_ends_only_its_request():
