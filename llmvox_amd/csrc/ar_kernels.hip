@@ -1082,14 +1082,11 @@ __device__ __forceinline__ void qsplit_make(const float (&q)[24], QSplit& qs) {
 __device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float c) {
   return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a), __builtin_bit_cast(bf16x2_t, b), c, false);
 }
-__device__ __forceinline__ void slot_softmax_step_bf16(float& m, float& l, f32x2_t (&o)[12], const QSplit& qs,
-                                                       const uint4 (&kp)[3], const uint4 (&vp)[3], bool valid) {
-  uint32_t k[12], v[12];
+// the score of the lane quad's key (every lane of the quad: the same bits)
+__device__ __forceinline__ float slot_score_bf16(const QSplit& qs, const uint4 (&kp)[3]) {
+  uint32_t k[12];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    k[4 * i] = kp[i].x; k[4 * i + 1] = kp[i].y; k[4 * i + 2] = kp[i].z; k[4 * i + 3] = kp[i].w;
-    v[4 * i] = vp[i].x; v[4 * i + 1] = vp[i].y; v[4 * i + 2] = vp[i].z; v[4 * i + 3] = vp[i].w;
-  }
+  for (int i = 0; i < 3; ++i) { k[4 * i] = kp[i].x; k[4 * i + 1] = kp[i].y; k[4 * i + 2] = kp[i].z; k[4 * i + 3] = kp[i].w; }
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
@@ -1098,7 +1095,15 @@ __device__ __forceinline__ void slot_softmax_step_bf16(float& m, float& l, f32x2
     s2 = dot2_bf16(qs.lo[j], k[j], s2);
     s3 = dot2_bf16(qs.lo[6 + j], k[6 + j], s3);
   }
-  const float sc = quad_sum((s0 + s1) + (s2 + s3));
+  return quad_sum((s0 + s1) + (s2 + s3));
+}
+// the slot's online-softmax update with that score (split from the score so that a caller can
+// compute the scores of two tiles before either update: independent chains, same bits)
+__device__ __forceinline__ void slot_update_bf16(float& m, float& l, f32x2_t (&o)[12], float sc, const uint4 (&vp)[3],
+                                                 bool valid) {
+  uint32_t v[12];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) { v[4 * i] = vp[i].x; v[4 * i + 1] = vp[i].y; v[4 * i + 2] = vp[i].z; v[4 * i + 3] = vp[i].w; }
   if (!valid) return;
   const float mn = fmaxf(m, sc);
   // 2^(x log2 e) on v_exp_f32 (arguments <= 0; m = -inf gives 0): ~1 ulp, two instructions instead
@@ -1113,6 +1118,10 @@ __device__ __forceinline__ void slot_softmax_step_bf16(float& m, float& l, f32x2
     o[j] = __builtin_elementwise_fma(p2, vv, o[j] * a2);
   }
   m = mn;
+}
+__device__ __forceinline__ void slot_softmax_step_bf16(float& m, float& l, f32x2_t (&o)[12], const QSplit& qs,
+                                                       const uint4 (&kp)[3], const uint4 (&vp)[3], bool valid) {
+  slot_update_bf16(m, l, o, slot_score_bf16(qs, kp), vp, valid);
 }
 
 // fold the 16 slots of a wave: returns the wave's max; o / l rescaled to it (slots that saw no key: 0)
@@ -2568,12 +2577,26 @@ static int attn_ns_max(int B) {  // enough splits to fill the chip, no more (ear
 static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_t s, int ns_max = NSPLIT,
                         int direct = 0, int selcopy = 0, bool qkv = false, bool nw8 = false) {
   dim3 grid(ns_max, N_HEAD, B);
+  // (A/B, option exp bit 8192: 16 waves and 256-key tiles for the one-split blocks at B <= 8, where 8 x B
+  // blocks leave most CUs idle and each block streams its whole history)
+  if (nw8 && !qkv && B <= 8 && (opts().exp & 8192) && kvdtype == LVX_DTYPE_FP8) {
+    hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t, 2, 16>), grid, dim3(1024), 0, s, st, l, ns_max, direct, selcopy);
+    return;
+  }
+  if (nw8 && !qkv && B <= 8 && (opts().exp & 8192) && kvdtype == LVX_DTYPE_BF16) {
+    hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2, 16>), grid, dim3(1024), 0, s, st, l, ns_max, direct, selcopy);
+    return;
+  }
   if (nw8 && !qkv && kvdtype == LVX_DTYPE_BF16)  // 8 waves, 128-key tiles: twice the KV bytes in flight per block
     hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2, 8>), grid, dim3(512), 0, s, st, l, ns_max, direct, selcopy);
   else if (nw8 && !qkv && kvdtype == LVX_DTYPE_FP8)
     hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t, 2, 8>), grid, dim3(512), 0, s, st, l, ns_max, direct, selcopy);
   else if (qkv && kvdtype == LVX_DTYPE_F32)  // fp32 parity mode: ar_qkv_ksplit_f32_kernel's partials
     hipLaunchKernelGGL((ar_attn_v2_kernel<float, 2, 4, true>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
+  else if (qkv && kvdtype == LVX_DTYPE_BF16 && nw8)  // (ksplit with ln_max < B <= 8: the same 8-wave blocks)
+    hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2, 8, true>), grid, dim3(512), 0, s, st, l, ns_max, direct, selcopy);
+  else if (qkv && kvdtype == LVX_DTYPE_FP8 && nw8)  // K-slice partials, the 8-wave blocks of fp8 KV at B <= 16
+    hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t, 2, 8, true>), grid, dim3(512), 0, s, st, l, ns_max, direct, selcopy);
   else if (qkv && kvdtype == LVX_DTYPE_FP8)  // c_attn left K-slice partials (qkv_ksplit)
     hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t, 2, 4, true>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
   else if (qkv)

@@ -26,6 +26,7 @@ lib.lvx_debug_persist.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
 e = build_engine(0, "bf16", "bf16", max_streams=B, max_positions=P0 + 512, max_codec_frames=256)
 dev = e.device
 e.set_option("persist", 1)
+e.set_option("pexp", int(os.environ.get("LVX_PEXP", "0")))  # persistent-step A/B bits
 plan = torch.full((B, 64), 100, dtype=torch.int32, device=dev)
 slots = torch.arange(B, dtype=torch.int32, device=dev)
 tok = torch.zeros(B, 64, dtype=torch.int32, device=dev)

@@ -5,10 +5,11 @@
 // Mirrors the shape of that launch path without the library: a chain of dependent kernels that take
 // a 320-byte kernel-argument struct (as GemvArgs), captured with hipStreamCaptureModeThreadLocal on a
 // non-blocking side stream, instantiated once and replayed many times on that stream.
-//   usage: pmc_graph_repro [mode] [kernels per graph] [replays]
+//   usage: pmc_graph_repro [mode] [kernels per graph] [replays] [small kernargs 0/1]
 //   mode 0: graph replay on the side stream (the bench's default path)
 //        1: the same kernels launched one by one on the side stream (no graph)
 //        2: graph replay on the legacy null stream
+//        3: the kernels launched one by one on the legacy null stream
 // Exit 0 and one line "ok ..." when the chain ran and its result checks out.
 #include <hip/hip_runtime.h>
 
@@ -38,11 +39,16 @@ __global__ __launch_bounds__(256) void chain_step(Args a) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < a.n) a.x[i] = a.x[i] * 0.5f + (float)(a.k & 3);
 }
+__global__ __launch_bounds__(256) void chain_step_small(float* x, int n, int k) {  // 16 B of kernargs
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = x[i] * 0.5f + (float)(k & 3);
+}
 
 int main(int argc, char** argv) {
   const int mode = argc > 1 ? std::atoi(argv[1]) : 0;
   const int nk = argc > 2 ? std::atoi(argv[2]) : 416;   // 16 decode steps x 26 kernels
   const int reps = argc > 3 ? std::atoi(argv[3]) : 320;  // 20 bench steps x 256 / 16
+  const bool small = argc > 4 && std::atoi(argv[4]) != 0;
   const int n = 256 * 256;
   float* x = nullptr;
   CK(hipMalloc(&x, n * sizeof(float)));
@@ -55,13 +61,15 @@ int main(int argc, char** argv) {
   auto enqueue = [&](hipStream_t q) -> hipError_t {
     for (int k = 0; k < nk; ++k) {
       a.k = k;
-      hipLaunchKernelGGL(chain_step, dim3(n / 256), dim3(256), 0, q, a);
+      if (small) hipLaunchKernelGGL(chain_step_small, dim3(n / 256), dim3(256), 0, q, x, n, k);
+      else hipLaunchKernelGGL(chain_step, dim3(n / 256), dim3(256), 0, q, a);
     }
     return hipGetLastError();
   };
-  if (mode == 1) {
-    for (int r = 0; r < reps; ++r) CK(enqueue(s));
-    CK(hipStreamSynchronize(s));
+  if (mode == 1 || mode == 3) {
+    hipStream_t q = mode == 3 ? nullptr : s;
+    for (int r = 0; r < reps; ++r) CK(enqueue(q));
+    CK(hipStreamSynchronize(q));
   } else {
     hipGraph_t g;
     hipGraphExec_t ge;
@@ -85,7 +93,7 @@ int main(int argc, char** argv) {
       std::fprintf(stderr, "mismatch at %d: %g vs %g\n", i, h[i], h[0]);
       return 4;
     }
-  std::printf("ok mode %d kernels/graph %d replays %d x[0] %.6f\n", mode, nk, reps, h[0]);
+  std::printf("ok mode %d kernels/graph %d replays %d small-kernargs %d x[0] %.6f\n", mode, nk, reps, (int)small, h[0]);
   CK(hipStreamDestroy(s));
   CK(hipFree(x));
   return 0;
