@@ -170,11 +170,7 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
  *                     XCD-aligned 1-D order (bit-identical);
  *   "f32b"         1: fp32 weights, 3 <= B <= 64: batched steps on exact-fp32 MFMA (ar_f32b_kernel);
  *                     0: the fp32 GEMV family (same ids against the reference: tests/test_gpu_f32b.py);
- *   "persist"      1: bf16 weights + bf16 KV, 17 <= B <= 32: each decode step is ONE persistent dataflow
- *                     launch (ar_persist_kernel); 0 (default, measured faster): the 26 launches of the
- *                     batched path (bit-identical: tests/test_gpu_persist.py);
- *   "pexp"         persistent-step development bits (1: no KV-history prefetch).
- *   "ksplit"       (default 0) c_attn as four K-slice partials summed by the attention (9 <= B <= 32):
+  *   "ksplit"       (default 0) c_attn as four K-slice partials summed by the attention (9 <= B <= 32):
  *                  bit-identical to the one-launch c_attn; faster only when steps are launched one
  *                  by one (the null stream), slower under graph replay.
  *   "ln_max"       (2..8, default 8) largest B whose batched GEMMs normalise in their own prologue;

@@ -1038,7 +1038,7 @@ template <> struct KvPiece<fp8_t> {
 // tile (4 lanes x 24 dims) and keeps its own (m, l, o[24]) over the keys it sees, so a tile needs no
 // wave-wide reduction (the wave-uniform form spent two DPP + readlane reductions and a 24-deep FMA
 // chain per 64-key tile: the tile loop, not the KV stream, bounded the decode attention, ~0.65 us
-// per tile whether the keys came from HBM or from LDS, tools/persist_timeline.py). The score is
+// per tile whether the keys came from HBM or from LDS, in the round-3 persistent step's timeline). The score is
 // four 6-term FMA chains summed pairwise. The slots are folded into the wave (max, rescale, DPP
 // sums) once at the end. fp32 KV (the bit-exact parity mode) keeps the wave-uniform form.
 __device__ __forceinline__ void slot_softmax_step(float& m, float& l, float (&o)[24], const float (&q)[24],
@@ -2894,9 +2894,6 @@ static GemvArgs make_args(const ArWeights& w, const ArState& st, int kvdtype, in
   return a;
 }
 
-#include "ar_persist.inc"
-
-size_t persist_ctr_words() { return PG_CTR_WORDS; }
 
 // returns whether the greedy select is deferred into the next step (no argmax kernel after lm_head)
 template <typename TW>
@@ -2905,10 +2902,6 @@ static bool ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B,
   GemvArgs a = make_args<TW>(w, st, kvdtype, B, emb_row);
   a.defer_sel = (select && !emb_row) ? (defer_select<TW>(B) ? 1 : defer_select_batched<TW>(B) ? 2 : 0) : 0;
   if (emb_row) hipLaunchKernelGGL(ar_row_state_kernel, dim3(1), dim3(1), 0, s, st, slot, pos);
-  if (!emb_row && a.defer_sel == 2 && logits_dst == st.logits && use_persist<TW>(B, kvdtype, st)) {
-    launch_persist(w, st, B, s);  // the whole step as one dataflow launch
-    return true;
-  }
   for (int l = 0; l < N_LAYER; ++l)
     for (int op = 0; op < 5; ++op) launch_op<TW>(op, a, w, l, kvdtype, B, s);
   a.dst = logits_dst;
@@ -3064,22 +3057,6 @@ void launch_codes_to_features(const float* codebook, const int64_t* codes, int B
 }  // namespace lvx
 
 #ifdef LVX_TIMING
-// timing build only (tools/persist_timeline.py): copy / clear the persistent step's task records
-extern "C" int lvx_debug_persist_att(void* dst, size_t bytes) {
-  if (bytes > sizeof(lvx::g_pg_att)) bytes = sizeof(lvx::g_pg_att);
-  if (dst && hipMemcpyFromSymbol(dst, HIP_SYMBOL(lvx::g_pg_att), bytes) != hipSuccess) return -3;
-  return (int)bytes;
-}
-extern "C" int lvx_debug_persist(void* dst, size_t bytes, int clear) {
-  if (bytes > sizeof(lvx::g_pg_ts)) bytes = sizeof(lvx::g_pg_ts);
-  if (dst && hipMemcpyFromSymbol(dst, HIP_SYMBOL(lvx::g_pg_ts), bytes) != hipSuccess) return -3;
-  if (clear) {
-    void* p = nullptr;
-    if (hipGetSymbolAddress(&p, HIP_SYMBOL(lvx::g_pg_ts)) != hipSuccess) return -3;
-    if (hipMemset(p, 0, sizeof(lvx::g_pg_ts)) != hipSuccess) return -3;
-  }
-  return (int)bytes;
-}
 // timing build only (tools/step_timeline.py): copy / clear the step timeline records
 extern "C" int lvx_debug_timeline(void* dst, size_t bytes, int clear) {
   if (bytes > sizeof(lvx::g_lvx_ts)) bytes = sizeof(lvx::g_lvx_ts);

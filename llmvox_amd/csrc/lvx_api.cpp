@@ -507,19 +507,9 @@ int lvx_finalize(lvx_ctx* c) {
       (r = c->dalloc(&st.xb, (size_t)S16 * D)) || (r = c->dalloc(&st.xstat, (size_t)(D / 16) * S * 2)) ||
       (r = c->dalloc(&st.lmbest, (size_t)LM_MAX_BLOCKS * 4 * 2)) ||
       (r = c->dalloc(&st.yacc, (size_t)YCOPIES * S * D)) || (r = c->dalloc(&st.qkvp, (size_t)4 * S * 3 * D)) ||
-      (r = c->dalloc(&st.xa, (size_t)S16 * D)) || (r = c->dalloc(&st.pctr, persist_ctr_words())) ||
-      (r = c->dalloc(&st.pdone, 4)) || (r = c->dalloc(&st.ptmo, 4)) || (r = c->dalloc(&st.yfx, (size_t)YCOPIES * S * D)))
+      (r = c->dalloc(&st.yfx, (size_t)YCOPIES * S * D)))
     return r;
   HIP_TRY(hipMemset(st.yfx, 0, (size_t)YCOPIES * S * D * 8));
-  HIP_TRY(hipMemset(st.pctr, 0, persist_ctr_words() * 4));
-  HIP_TRY(hipMemset(st.pdone, 0, 16));
-  HIP_TRY(hipMemset(st.ptmo, 0, 16));
-  HIP_TRY(hipMemset(st.xa, 0, (size_t)S16 * D * 2));
-  {  // the persistent step's grid: one workgroup per CU (every workgroup resident at once)
-    hipDeviceProp_t prop;
-    HIP_TRY(hipGetDeviceProperties(&prop, c->cfg.device));
-    st.pgrid = prop.multiProcessorCount;
-  }
   HIP_TRY(hipMemset(st.yacc, 0, (size_t)YCOPIES * S * D * 4));
   HIP_TRY(hipMemset(st.selp, 0, 16));
   HIP_TRY(hipMemset(st.part_o, 0, (size_t)S * N_HEAD * NSPLIT * HD * 4));
@@ -631,8 +621,6 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   else if (n == "codec_exp") o.codec_exp = value;
   else if (n == "exp") o.exp = value;
   else if (n == "f32b") o.f32b = value != 0;
-  else if (n == "persist") o.persist = value != 0;
-  else if (n == "pexp") o.pexp = value;
   else if (n == "ksplit") o.ksplit = value != 0;
   else if (n == "ln_max") o.ln_max = std::min(std::max(value, 2), 8);
   else return fail(LVX_E_NAME, "unknown option " + n);
@@ -805,13 +793,6 @@ int lvx_check_errors(lvx_ctx* c, void* stream) {
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   if (v) {
     (void)hipMemsetAsync(c->st.err, 0, 4, (hipStream_t)stream);
-    if (v & 16) {  // a persistent step's wait timed out: its counters are in an unknown state
-      (void)hipMemsetAsync(c->st.pctr, 0, persist_ctr_words() * 4, (hipStream_t)stream);
-      (void)hipMemsetAsync(c->st.pdone, 0, 4, (hipStream_t)stream);
-      (void)hipMemsetAsync(c->st.ptmo, 0, 4, (hipStream_t)stream);
-      (void)hipStreamSynchronize((hipStream_t)stream);
-      return fail(LVX_E_HIP, "a persistent decode step's dependency wait timed out (results of that call are invalid)");
-    }
     if (v & 32)
       return fail(LVX_E_STATE, "a non-finite or out-of-range (|v| >= 2^25) partial in the fused MLP's fixed-point "
                                "accumulation (B <= 2): its logits are invalid");

@@ -37,8 +37,6 @@ struct Opts {
   int codec_exp = 0;     // codec A/B bits (bit-identical variants)
   int exp = 0;           // AR A/B bits (bit-identical variants, tests/test_gpu_batched.py, test_gpu_f32b.py)
   int f32b = 1;          // fp32 batched steps on exact-fp32 MFMA; 0: the GEMV family
-  int persist = 0;       // bf16, 17 <= B <= 32: the decode step as one persistent launch
-  int pexp = 0;          // persistent-step A/B bits
   int ksplit = 0;        // batched bf16 c_attn as K-slice partials summed by the attention
   int ln_max = 8;        // batched steps with the LayerNorm fused into the GEMM prologue for B <= ln_max
 };
@@ -50,7 +48,6 @@ struct OptScope {    // binds `o` to this thread until the scope ends
   OptScope& operator=(const OptScope&) = delete;
   const Opts* prev;
 };
-size_t persist_ctr_words();  // words of ArState::pctr
 
 // Device-resident AR weights. Matrices are [out][in] row-major (torch Linear layout),
 // in the context's weight dtype; vectors and gathered tables are fp32.
@@ -113,11 +110,6 @@ struct ArState {
   float* yacc = nullptr;        // [max_streams][YCOPIES][768] batched mlp c_proj K-slice partials (fp32);
                                 // a row's copies adjacent: spaced by max_streams rows they shared
                                 // L2 channels (B = 1: 82.6 vs 69.6 us/step at max_streams 32)
-  bf16_t* xa = nullptr;         // [max_streams rounded to 16][768] attention outputs of the persistent step (xfrag)
-  uint32_t* pctr = nullptr;     // persistent step: dependency counters (PG_CTR_WORDS, zero between launches)
-  uint32_t* pdone = nullptr;    // [1] its workgroups finished
-  uint32_t* ptmo = nullptr;     // [1] sticky timeout flag of its waits (cleared by lvx_check_errors)
-  int pgrid = 0;                // its workgroups (one per CU)
   void* kc = nullptr;           // [4][kv_chunks][max_streams][8][KV_CHUNK][96] (kv_at)
   void* vc = nullptr;
   int max_pos = 0, max_streams = 0, kv_chunks = 0;
