@@ -682,7 +682,9 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
     # the codec of chunk c runs after the AR of chunk c on the same stream. A second stream
     # (--codec-overlap) was measured slower: the latency-bound AR chain stalls while the codec's
     # kernels are in flight (22.4 ms AR + 1.2 ms codec = 23.6 ms serial vs 25.5 ms overlapped per
-    # 256-token chunk; CU-partitioned or prioritised streams 28 ms, round 1).
+    # 256-token chunk; CU-partitioned or prioritised streams 28 ms, round 1; configs[2], round 4: the
+    # codec on 32 / 48 CUs and the AR on the rest 197.8k / 186.1k vs 227-228k tok/s serial, the AR step
+    # 131 -> 160-168 us without its CUs).
     # tok_plan / pcm are double-buffered so the overlapped variant stays correct.
     codec_stream = torch.cuda.Stream(device=dev) if codec_overlap else torch.cuda.current_stream(dev)
     tok_bufs = [tok_plan, torch.zeros_like(tok_plan)]

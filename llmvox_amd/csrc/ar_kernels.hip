@@ -1134,6 +1134,8 @@ __device__ __forceinline__ float slot_fold_wave(float m, float& l, float (&o)[24
   return M;
 }
 
+// (round 4, measured slower: the per-key-slot form for fp32 KV too, B = 32 t = 384-639 214.1 vs
+// 210.7 us/step; the fp32 parity mode keeps the wave-uniform form)
 template <typename TKV, int DEPTH, int NW, bool QKV = false>
 __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int layer, int ns_max, int direct,
                                                          int selcopy) {
@@ -2577,16 +2579,8 @@ static int attn_ns_max(int B) {  // enough splits to fill the chip, no more (ear
 static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_t s, int ns_max = NSPLIT,
                         int direct = 0, int selcopy = 0, bool qkv = false, bool nw8 = false) {
   dim3 grid(ns_max, N_HEAD, B);
-  // (A/B, option exp bit 8192: 16 waves and 256-key tiles for the one-split blocks at B <= 8, where 8 x B
-  // blocks leave most CUs idle and each block streams its whole history)
-  if (nw8 && !qkv && B <= 8 && (opts().exp & 8192) && kvdtype == LVX_DTYPE_FP8) {
-    hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t, 2, 16>), grid, dim3(1024), 0, s, st, l, ns_max, direct, selcopy);
-    return;
-  }
-  if (nw8 && !qkv && B <= 8 && (opts().exp & 8192) && kvdtype == LVX_DTYPE_BF16) {
-    hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2, 16>), grid, dim3(1024), 0, s, st, l, ns_max, direct, selcopy);
-    return;
-  }
+  // (round 4, measured slower: 16 waves and 256-key tiles for the one-split blocks at B <= 8, B = 8
+  // t = 384-639 fp8 KV 103.9 vs 98.3 us/step, bf16 KV 109.6 vs 100.1)
   if (nw8 && !qkv && kvdtype == LVX_DTYPE_BF16)  // 8 waves, 128-key tiles: twice the KV bytes in flight per block
     hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2, 8>), grid, dim3(512), 0, s, st, l, ns_max, direct, selcopy);
   else if (nw8 && !qkv && kvdtype == LVX_DTYPE_FP8)
