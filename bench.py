@@ -96,7 +96,6 @@ def attn_splits(B, wbytes):
 
 
 KSPLIT = False  # library option "ksplit" (bench.py --opt ksplit=1)
-FUSE_ATTN = True  # library option "fuse_attn" (default 1; bench.py --opt fuse_attn=0)
 
 
 def kernel_bytes(which, B, t, wbytes, kvbytes):
@@ -109,9 +108,7 @@ def kernel_bytes(which, B, t, wbytes, kvbytes):
     D, F, V = 768, 3072, 4096
     act = 4 * B
     mfma = wbytes == 2 and 3 <= B <= 64
-    # the fused c_attn + attention launch (library option fuse_attn, default; bf16 KV, 9 <= B <= 32)
-    # hands the attention the same K-slice partials
-    ksplit = (KSPLIT or (FUSE_ATTN and kvbytes == 2)) and mfma and kvbytes <= 2 and 9 <= B <= 32
+    ksplit = KSPLIT and mfma and kvbytes <= 2 and 9 <= B <= 32
     ns = attn_splits(B, wbytes)
     parts = act * 8 * ns * 98 if ns > 1 else 0           # split-KV partials written / read once
     rows_bf16 = 2 * D * B                                  # one bf16 operand row set
@@ -248,8 +245,7 @@ def _probe_pass(eng, slots, t, wbytes, kvbytes, iters):
         except LvxError as e:
             if e.code != -2:  # LVX_E_STATE: fused into the previous op at this B
                 raise
-            res[k - 1]["name"] = {1: "ar_qkv_attn (c_attn + attention, one launch)",
-                                  4: "ar_mlp fused (c_fc+gelu+c_proj)"}[k]
+            res[k - 1]["name"] = "ar_mlp fused (c_fc+gelu+c_proj)"
             res[k - 1]["bytes"] += kernel_bytes(k, B, t, wbytes, kvbytes)
             res[k - 1]["gbs"] = res[k - 1]["bytes"] / (res[k - 1]["avg_us"] * 1e-6) / 1e9
             continue
@@ -894,14 +890,12 @@ def main():
                        codec_dtype=args.codec_dtype)
     dev = eng.device
     torch.cuda.set_device(dev)
-    global KSPLIT, FUSE_ATTN
+    global KSPLIT
     for kv in filter(None, args.opt.split(",")):
         k, v = kv.split("=")
         eng.set_option(k, int(v))
         if k == "ksplit":
             KSPLIT = int(v) != 0
-        if k == "fuse_attn":
-            FUSE_ATTN = int(v) != 0
     if args.no_graphs:
         eng.set_graphs(False)
     if not args.null_stream:

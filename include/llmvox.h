@@ -174,11 +174,7 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
  *                  bit-identical to the one-launch c_attn; faster only when steps are launched one
  *                  by one (the null stream), slower under graph replay.
  *   "ln_max"       (2..8, default 8) largest B whose batched GEMMs normalise in their own prologue;
- *                  larger B run the rows kernel + K-split c_attn structure;
- *   "fuse_attn"    (default 1) bf16 weights + bf16 KV, ln_max < B <= 32: c_attn (K-split) and the
- *                  decode attention in ONE launch, the attention blocks waiting in-launch for their
- *                  head's c_attn blocks (bit-identical to the two launches: tests/test_gpu_batched.py);
- *                  0: two launches. */
+ *                  larger B run the rows kernel + K-split c_attn structure. */
 int lvx_set_option(lvx_ctx* ctx, const char* name, int value);
 /* Enable/disable HIP-graph replay of lvx_ar_step for a given B (default on). */
 int lvx_set_graphs(lvx_ctx* ctx, int enable);

@@ -195,27 +195,6 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
 typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
 
-// ---- in-launch hand-offs (ar_qkv_attn_kernel; cdna_hip_programming.md Guideline 16, the sc1 form):
-// every handed-off byte stored write-through (sc1 vector stores), every storing wave drains
-// (s_waitcnt vmcnt(0)), the workgroup barrier, then one lane adds to its XCD's counter shard (relaxed,
-// agent scope); the consumer polls the shards with sc1 loads and reads the bytes with sc1 loads only.
-typedef int hx_i32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ int hx_xcc() { return __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7; }
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t hx_rsrc(const void* p) {  // p wave-uniform
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
-}
-__device__ __forceinline__ void hx_st16f(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, float4 v) {  // sc1 store
-  __builtin_amdgcn_raw_buffer_store_b128(hx_i32x4{(int)__float_as_uint(v.x), (int)__float_as_uint(v.y),
-                                                  (int)__float_as_uint(v.z), (int)__float_as_uint(v.w)},
-                                         r, byte_off, 0, 16);
-}
-__device__ __forceinline__ unsigned hx_ld4(const void* p) {  // sc1 load
-  return __hip_atomic_load((gu32*)const_cast<void*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void hx_st4(void* p, unsigned v) {  // sc1 store
-  __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // Deferred select: lm_head (OUT 9) leaves one 16-byte granule {index << 32 | top1 bits, top2 bits}
 // per (block, row) in st.lmbest; the next step's c_attn layer 0 (IN 5) or ar_select_final_kernel
 // reduces a row's 512 granules with one wave: every load in flight at once, then a shuffle tree.
@@ -1961,14 +1940,20 @@ static void launch_mfma2(const GemvArgs& a, hipStream_t s, bool btile = false) {
 // block instead of 24.6 + 49 KB. Each wave stores its 16 x 32 partial (one 16-B store per
 // lane and batch tile) to st.qkvp[slice]; the attention sums the four slices in the order the
 // one-launch kernel summed its waves and appends the new key (bit-identical to ar_mfma2_kernel OUT 0).
-// SC1: the partials are stored write-through (sc1), for a consumer in the same launch
-// (ar_qkv_attn_kernel); the caller provides the LDS operand buffer xs (NT * 16 * 200 bf16)
-template <int NT, bool SC1>
-__device__ __forceinline__ void qkv_ksplit_task(const GemvArgs& a, int nb, int ks, bf16_t* xs) {
+template <int NT>
+__global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_qkv_ksplit_kernel(GemvArgs a) {
+  // The batched GEMM launches are bound by the bytes each CU loads (~30 GB/s per CU from entry to
+  // operands landed, tools/step_timeline.py: 72 KB per CU 2.8 us, 36 KB 1.5 us, nothing 0.5 us), so
+  // the block's operand slice (NT * 16 rows x 192 columns), which all four waves multiply, is loaded
+  // once and shared through LDS: four waves each loading it measured as slow as the one-launch layout.
+  // B = 32, t = 512: c_attn 3.9 -> 2.0 us per launch, 154.3 -> 149.6 us per step.
   constexpr int XR = NT * 16, XS = 200;  // rows, bf16 row stride (400 B: 16 rows hit distinct bank groups)
+  __shared__ __attribute__((aligned(16))) bf16_t xs[XR * XS];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int n0 = (nb * 4 + wave) * 16;
+  const int n0 = (blockIdx.x * 4 + wave) * 16, ks = blockIdx.y;
   const int B = a.B;
+  TS_DECL;
+  TS_MARK(0);
   const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(a.W);
   const bf16_t* __restrict__ X = a.st.xn;
   // operand slice first (vmcnt retires in issue order: the LDS fill then waits for it alone): the
@@ -2014,32 +1999,14 @@ __device__ __forceinline__ void qkv_ksplit_task(const GemvArgs& a, int nb, int k
     for (int t = 0; t < NT; ++t)
       acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[kk]),
                                                        __builtin_bit_cast(bf16x8_t, xf[t][kk]), acc[t], 0, 0, 0);
+  TS_MARK(1);
   // lane: C[n0 + 4 (lane >> 4) + i][t * 16 + (lane & 15)], i = 0..3
   float* dst = a.st.qkvp + (size_t)ks * a.st.max_streams * (3 * D) + n0 + 4 * (lane >> 4);
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int b = t * 16 + (lane & 15);
-    const float4 v = make_float4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
-    if (b < B) {
-      if constexpr (SC1)
-        hx_st16f(hx_rsrc(a.st.qkvp), (uint32_t)(((size_t)ks * a.st.max_streams * (3 * D) + n0 + 4 * (lane >> 4) + (size_t)b * (3 * D)) * 4), v);
-      else *reinterpret_cast<float4*>(dst + (size_t)b * (3 * D)) = v;
-    }
+    if (b < B) *reinterpret_cast<float4*>(dst + (size_t)b * (3 * D)) = make_float4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
   }
-}
-
-template <int NT>
-__global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_qkv_ksplit_kernel(GemvArgs a) {
-  // The batched GEMM launches are bound by the bytes each CU loads (~30 GB/s per CU from entry to
-  // operands landed, tools/step_timeline.py: 72 KB per CU 2.8 us, 36 KB 1.5 us, nothing 0.5 us), so
-  // the block's operand slice (NT * 16 rows x 192 columns), which all four waves multiply, is loaded
-  // once and shared through LDS: four waves each loading it measured as slow as the one-launch layout.
-  // B = 32, t = 512: c_attn 3.9 -> 2.0 us per launch, 154.3 -> 149.6 us per step.
-  __shared__ __attribute__((aligned(16))) bf16_t xs[NT * 16 * 200];
-  TS_DECL;
-  TS_MARK(0);
-  qkv_ksplit_task<NT, false>(a, blockIdx.x, blockIdx.y, xs);
-  TS_MARK(1);
   TS_SAVE(1, a.layer, blockIdx.x + gridDim.x * blockIdx.y);
 }
 static_assert(3 * D == 4 * 16 * 36, "qkv_ksplit: 36 blocks of 64 rows");
@@ -2723,229 +2690,6 @@ static void launch_qkv_ksplit(const GemvArgs& a, hipStream_t s) {
   else hipLaunchKernelGGL(ar_qkv_ksplit_kernel<2>, dim3(36, 4), dim3(256), 0, s, a);
 }
 
-// ---------------------------------------------------------------------------------
-// c_attn + attention in ONE launch (round 4; bf16 weights + bf16 KV, ln_max < B <= 32, option
-// fuse_attn): the grid's first 144 blocks are the K-split c_attn (qkv_ksplit_task, its partials
-// stored write-through), the next 8 x B blocks the one-split decode attention of (row, head)
-// (ar_attn_v2_kernel<bf16, 2, 4, true>, direct 2: the same tile order and arithmetic, bit-identical).
-// An attention block issues its first two KV tiles (history written by earlier launches) at once,
-// then waits for the c_attn blocks that cover its head (a per-head counter, sharded per XCD) and
-// reads their partials with sc1 loads: its ramp (entry to the first tiles landed) runs under c_attn
-// instead of after a kernel boundary. The c_attn blocks come first in the grid and never wait, so
-// every wait completes whatever the residency; every wait is bounded (error bit 16, lvx_check_errors
-// re-zeroes the counters); the last block out zeroes them for the next launch.
-// ---------------------------------------------------------------------------------
-constexpr int HX_SHARDS = 8, HX_LINE = 32;  // a counter shard = one 128-B line per XCD
-constexpr uint64_t HX_TIMEOUT = 20000000;   // 200 ms of s_memrealtime (100 MHz); a launch takes ~15 us
-constexpr int QKV_TASKS = 36 * 4;           // c_attn blocks: 36 row blocks of 64 rows x 4 K slices
-size_t hx_ctr_words() { return (size_t)N_HEAD * HX_SHARDS * HX_LINE; }
-__device__ __forceinline__ uint32_t* hx_ctr(const ArState& st, int head, int shard) {
-  return st.hctr + ((size_t)head * HX_SHARDS + shard) * HX_LINE;
-}
-// c_attn blocks touching head h's q / k / v columns: a 64-row block lies inside one 768-wide
-// section (768 = 12 x 64) and covers heads [r / 96, (r + 63) / 96] of it
-__device__ __forceinline__ unsigned qkv_head_tasks(int h) {
-  unsigned n = 0;
-  for (int nb = 0; nb < 12; ++nb) {  // blocks of one section (the same count in q, k and v)
-    const int r = nb * 64;
-    if (r / 96 <= h && h <= (r + 63) / 96) ++n;
-  }
-  return n * 3 * 4;
-}
-// wait until head h's shards sum to >= target: wave 0 polls (lanes 0-7, one shard each), the others
-// wait at the barrier; on timeout (or after another block's) the wait gives up
-__device__ void hx_wait(const ArState& st, int head, unsigned target) {
-  if ((threadIdx.x >> 6) == 0) {
-    const int lane = threadIdx.x & 63;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    for (int it = 0;; ++it) {
-      const unsigned v = lane < HX_SHARDS ? hx_ld4(hx_ctr(st, head, lane)) : 0u;
-      unsigned sum = 0;
-#pragma unroll
-      for (int i = 0; i < HX_SHARDS; ++i) sum += (unsigned)__builtin_amdgcn_readlane((int)v, i);
-      if (sum >= target) break;
-      if ((it & 15) == 15) {
-        if (hx_ld4(st.htmo)) break;  // another block timed out: drain
-        if (__builtin_amdgcn_s_memrealtime() - t0 > HX_TIMEOUT) {
-          if (lane == 0) {
-            hx_st4(st.htmo, 1u);
-            atomicOr(st.err, 16);
-          }
-          break;
-        }
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction) loads stay below the poll
-  __syncthreads();
-}
-
-template <int NT>
-__global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_qkv_attn_kernel(GemvArgs a) {
-  constexpr int NW = 4, TK = NW * 16, DEPTH = 2;
-  __shared__ __attribute__((aligned(16))) bf16_t xs[NT * 16 * 200];  // c_attn: the operand slice
-  __shared__ float wm_s[NW], wl_s[NW];
-  __shared__ float wo_s[NW][4][HD];
-  __shared__ float qs_s[HD];
-  __shared__ __attribute__((aligned(16))) bf16_t kvh_s[2][HD];  // the new key's K, V
-  __shared__ unsigned last_s;
-  const ArState& st = a.st;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  if ((int)blockIdx.x < QKV_TASKS) {
-    // ---- c_attn K slice ----
-    const int nb = blockIdx.x % 36, ks = blockIdx.x / 36;
-    qkv_ksplit_task<NT, true>(a, nb, ks, xs);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's write-through stores drained
-    __syncthreads();
-    if (tid == 0) {
-      const int r = (nb % 12) * 64, h0 = r / 96, h1 = (r + 63) / 96, x = hx_xcc();
-      __hip_atomic_fetch_add((gu32*)hx_ctr(st, h0, x), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (h1 != h0) __hip_atomic_fetch_add((gu32*)hx_ctr(st, h1, x), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the adds have landed before this block counts out
-    }
-  } else {
-    // ---- attention of (row b, head), one split ----
-    const int j = blockIdx.x - QKV_TASKS, b = j / N_HEAD, head = j % N_HEAD;
-    const int4 ri = st.rowinfo[b];  // written by an earlier launch
-    if (ri.x >= 0) {  // (block-uniform) idle rows: nothing, as ar_attn_v2_kernel
-      const int s = ri.x, t = ri.y + 1, k1 = t;
-      const size_t base = kv_at(a.layer, st.kv_chunks, st.max_streams, s, head, 0);
-      const size_t cstride = (size_t)st.max_streams * N_HEAD * KV_CHUNK * HD;
-      const bf16_t* __restrict__ Kg = reinterpret_cast<const bf16_t*>(st.kc) + base;
-      const bf16_t* __restrict__ Vg = reinterpret_cast<const bf16_t*>(st.vc) + base;
-      auto krow = [&](int k) { return (size_t)(k / KV_CHUNK) * cstride + (size_t)(k % KV_CHUNK) * HD; };
-      const int part = tid & 3, kq = tid >> 2;
-      const int klast = ((k1 - 1) / ATK) * ATK;
-      KvPiece<bf16_t> kpr[DEPTH][3], vpr[DEPTH][3];
-      auto issue = [&](int kb, KvPiece<bf16_t>(&kp)[3], KvPiece<bf16_t>(&vp)[3]) {
-        const size_t off = (size_t)min(kb / KV_CHUNK, klast / KV_CHUNK) * cstride + (size_t)kq * HD + part * 24;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          kp[i].load(Kg + off + i * 8);
-          vp[i].load(Vg + off + i * 8);
-        }
-      };
-      // the first tiles are history (key t - 1, the new one, is taken from LDS below): issued now
-#pragma unroll
-      for (int d = 0; d < DEPTH; ++d) issue(d * TK, kpr[d], vpr[d]);
-      hx_wait(st, head, qkv_head_tasks(head));
-      float pq[2][4];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int e = min(tid + 256 * h, 3 * HD - 1);
-        const float* pp = st.qkvp + (size_t)b * (3 * D) + (e / HD) * D + head * HD + e % HD;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) pq[h][k] = __uint_as_float(hx_ld4(pp + (size_t)k * st.max_streams * (3 * D)));
-      }
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int e = tid + 256 * h;
-        float v = 0.f;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v += pq[h][k];
-        if (e < HD) {
-          qs_s[e] = v;
-        } else if (e < 3 * HD) {  // K / V of the new key: appended (read by later launches), kept in LDS
-          const int which = e / HD - 1, d = e % HD;
-          const bf16_t hv = f32_to_bf16(v);
-          kvh_s[which][d] = hv;
-          reinterpret_cast<bf16_t*>(which ? st.vc : st.kc)[base + krow(ri.y) + d] = hv;
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      float q[24];
-#pragma unroll
-      for (int i = 0; i < 24; ++i) q[i] = qs_s[part * 24 + i] * 0.10206207261596575f;
-      QSplit qsp;
-      qsplit_make(q, qsp);
-      float m = -INFINITY, l = 0.f, o[24];
-      f32x2_t o2[12];
-#pragma unroll
-      for (int jj = 0; jj < 12; ++jj) o2[jj] = f32x2_t{0.f, 0.f};
-      auto tile = [&](int kb, const KvPiece<bf16_t>(&kp)[3], const KvPiece<bf16_t>(&vp)[3]) {
-        const bool valid = kb + kq < k1;
-        uint4 ku[3], vu[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) { ku[i] = kp[i].u; vu[i] = vp[i].u; }
-        if (kb + TK >= k1) {  // (uniform) the tile holding key t - 1: that lane takes it from LDS
-          if (kb + kq == t - 1) {
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-              ku[i] = reinterpret_cast<const uint4*>(kvh_s[0])[part * 3 + i];
-              vu[i] = reinterpret_cast<const uint4*>(kvh_s[1])[part * 3 + i];
-            }
-          }
-        }
-        slot_softmax_step_bf16(m, l, o2, qsp, ku, vu, valid);
-      };
-      for (int kb = 0; kb < k1; kb += DEPTH * TK) {
-#pragma unroll
-        for (int d = 0; d < DEPTH; ++d) {
-          if (d > 0 && kb + d * TK >= k1) break;
-          tile(kb + d * TK, kpr[d], vpr[d]);
-          issue(kb + (d + DEPTH) * TK, kpr[d], vpr[d]);
-        }
-      }
-#pragma unroll
-      for (int jj = 0; jj < 12; ++jj) { o[2 * jj] = o2[jj].x; o[2 * jj + 1] = o2[jj].y; }
-      m = slot_fold_wave(m, l, o);
-      l = wave_sum(part == 0 ? l : 0.f);
-#pragma unroll
-      for (int i = 0; i < 24; ++i) {
-        float v = o[i];
-        v += dpp_f32<0x128>(v);
-        v += dpp_f32<0x124>(v);
-        o[i] = v;
-      }
-      if ((lane & 15) < 4) {
-#pragma unroll
-        for (int i = 0; i < 24; ++i) wo_s[wave][lane >> 4][(lane & 3) * 24 + i] = o[i];
-      }
-      if (lane == 0) { wm_s[wave] = m; wl_s[wave] = l; }
-      __syncthreads();
-      if (tid < HD) {
-        float M = wm_s[0];
-#pragma unroll
-        for (int w = 1; w < NW; ++w) M = fmaxf(M, wm_s[w]);
-        float ov = 0.f, lv = 0.f;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-          const float f = (wm_s[w] == -INFINITY) ? 0.f : expf(wm_s[w] - M);
-          ov += f * ((wo_s[w][0][tid] + wo_s[w][1][tid]) + (wo_s[w][2][tid] + wo_s[w][3][tid]));
-          lv += f * wl_s[w];
-        }
-        st.xn[xfrag(b, head * HD + tid, D)] = f32_to_bf16(ov * (1.0f / lv));  // read by the next launch
-      }
-    }
-  }
-  // the last block out zeroes the counters for the next launch (every block has left its wait and
-  // every add has landed by then)
-  __syncthreads();
-  if (tid == 0)
-    last_s = __hip_atomic_fetch_add((gu32*)st.hdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-  __syncthreads();
-  if (last_s) {
-    for (int i = tid; i < N_HEAD * HX_SHARDS; i += 256) hx_st4(st.hctr + (size_t)i * HX_LINE, 0u);
-    if (tid == 0) hx_st4(st.hdone, 0u);
-  }
-}
-
-// option fuse_attn (default 1, Opts in lvx_internal.h): c_attn + attention as one launch where the
-// batched bf16 steps run the rows-kernel structure (ln_max < B <= 32, bf16 KV)
-template <typename TW>
-static bool fuse_attn(int B, int kvdtype, const ArState& st) {
-  return opts().fuse_attn && use_mfma<TW>(B) && !use_bt<TW>(B) && B > MFMA_LN_MAX && B <= 32 &&
-         kvdtype == LVX_DTYPE_BF16 && !(opts().exp & 5) && st.hctr;  // (exp bit 4: row-major rows)
-}
-static void launch_qkv_attn(const GemvArgs& a, hipStream_t s) {
-  const dim3 grid(QKV_TASKS + N_HEAD * a.B);
-  if (a.B <= 16) hipLaunchKernelGGL(ar_qkv_attn_kernel<1>, grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(ar_qkv_attn_kernel<2>, grid, dim3(256), 0, s, a);
-}
-
 template <typename TW>
 static bool use_f32b(int B) {
   return sizeof(TW) == 4 && opts().f32b && B >= MFMA_BATCH_MIN && B <= 64;
@@ -3051,8 +2795,7 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       a.W = w.w_attn[l]; a.Wf = pk ? w.f_attn[l] : nullptr; a.N = 3 * D; a.ln_w = w.ln1[l];
       if (mf && l == 0 && a.defer_sel == 2) {  // embedding + the previous step's select, then c_attn
         hipLaunchKernelGGL(ar_embed_select_kernel<>, dim3(B), dim3(256), 0, s, a);
-        if (fuse_attn<TW>(B, kvdtype, a.st)) launch_qkv_attn(a, s);
-        else if (qkv_ksplit<TW>(B, kvdtype)) launch_qkv_ksplit(a, s);
+        if (qkv_ksplit<TW>(B, kvdtype)) launch_qkv_ksplit(a, s);
         else launch_mfma2<768, 0>(a, s);
       } else if (mf && B <= MFMA_LN_MAX) {
         if (l == 0) launch_mfma_ln<0, 3>(a, s);
@@ -3060,8 +2803,7 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       } else if (mf) {  // rows kernel: LayerNorm (layer 0: of the embedding; else of x + the MLP copies)
         if (l == 0) hipLaunchKernelGGL((ar_rows_kernel<3>), dim3(B), dim3(64), 0, s, a);
         else hipLaunchKernelGGL((ar_rows_kernel<4>), dim3(B), dim3(64), 0, s, a);
-        if (fuse_attn<TW>(B, kvdtype, a.st)) launch_qkv_attn(a, s);
-        else if (qkv_ksplit<TW>(B, kvdtype)) launch_qkv_ksplit(a, s);
+        if (qkv_ksplit<TW>(B, kvdtype)) launch_qkv_ksplit(a, s);
         else launch_mfma2<768, 0>(a, s);
       } else if (l == 0 && a.defer_sel) {
         launch_gemv<TW, 768, 1, 2, 5, 0>(a, s);  // + the previous step's select
@@ -3074,7 +2816,6 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       }
       break;
     case 1:
-      if (fuse_attn<TW>(B, kvdtype, a.st)) return false;  // inside c_attn's launch (ar_qkv_attn_kernel)
       launch_attn(a.st, kvdtype, B, l, s, nsm, (mf && nsm == 1) ? 1 + a.xpk : 0, a.defer_sel == 1 && l == 0,
                   qkv_ksplit<TW>(B, kvdtype), a8);
       break;

@@ -507,13 +507,9 @@ int lvx_finalize(lvx_ctx* c) {
       (r = c->dalloc(&st.xb, (size_t)S16 * D)) || (r = c->dalloc(&st.xstat, (size_t)(D / 16) * S * 2)) ||
       (r = c->dalloc(&st.lmbest, (size_t)LM_MAX_BLOCKS * 4 * 2)) ||
       (r = c->dalloc(&st.yacc, (size_t)YCOPIES * S * D)) || (r = c->dalloc(&st.qkvp, (size_t)4 * S * 3 * D)) ||
-      (r = c->dalloc(&st.yfx, (size_t)YCOPIES * S * D)) || (r = c->dalloc(&st.hctr, hx_ctr_words())) ||
-      (r = c->dalloc(&st.hdone, 4)) || (r = c->dalloc(&st.htmo, 4)))
+      (r = c->dalloc(&st.yfx, (size_t)YCOPIES * S * D)))
     return r;
   HIP_TRY(hipMemset(st.yfx, 0, (size_t)YCOPIES * S * D * 8));
-  HIP_TRY(hipMemset(st.hctr, 0, hx_ctr_words() * 4));
-  HIP_TRY(hipMemset(st.hdone, 0, 16));
-  HIP_TRY(hipMemset(st.htmo, 0, 16));
   HIP_TRY(hipMemset(st.yacc, 0, (size_t)YCOPIES * S * D * 4));
   HIP_TRY(hipMemset(st.selp, 0, 16));
   HIP_TRY(hipMemset(st.part_o, 0, (size_t)S * N_HEAD * NSPLIT * HD * 4));
@@ -627,7 +623,6 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   else if (n == "f32b") o.f32b = value != 0;
   else if (n == "ksplit") o.ksplit = value != 0;
   else if (n == "ln_max") o.ln_max = std::min(std::max(value, 2), 8);
-  else if (n == "fuse_attn") o.fuse_attn = value != 0;
   else return fail(LVX_E_NAME, "unknown option " + n);
   ++c->opt_epoch;  // this context's captured kernels change (checked in cached_graph)
   return LVX_OK;
@@ -798,13 +793,6 @@ int lvx_check_errors(lvx_ctx* c, void* stream) {
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   if (v) {
     (void)hipMemsetAsync(c->st.err, 0, 4, (hipStream_t)stream);
-    if (v & 16) {  // a fused c_attn + attention launch's wait timed out: its counters are in an unknown state
-      (void)hipMemsetAsync(c->st.hctr, 0, hx_ctr_words() * 4, (hipStream_t)stream);
-      (void)hipMemsetAsync(c->st.hdone, 0, 4, (hipStream_t)stream);
-      (void)hipMemsetAsync(c->st.htmo, 0, 4, (hipStream_t)stream);
-      (void)hipStreamSynchronize((hipStream_t)stream);
-      return fail(LVX_E_HIP, "a fused c_attn + attention launch's wait timed out (results of that call are invalid)");
-    }
     if (v & 32)
       return fail(LVX_E_STATE, "a non-finite or out-of-range (|v| >= 2^25) partial in the fused MLP's fixed-point "
                                "accumulation (B <= 2): its logits are invalid");

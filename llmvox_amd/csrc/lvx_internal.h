@@ -39,9 +39,7 @@ struct Opts {
   int f32b = 1;          // fp32 batched steps on exact-fp32 MFMA; 0: the GEMV family
   int ksplit = 0;        // batched bf16 c_attn as K-slice partials summed by the attention
   int ln_max = 8;        // batched steps with the LayerNorm fused into the GEMM prologue for B <= ln_max
-  int fuse_attn = 1;     // bf16 + bf16 KV, ln_max < B <= 32: c_attn and the attention in one launch
 };
-size_t hx_ctr_words();   // words of ArState::hctr
 const Opts& opts();  // the calling thread's bound options (the defaults when none is bound)
 struct OptScope {    // binds `o` to this thread until the scope ends
   explicit OptScope(const Opts* o);
@@ -112,9 +110,6 @@ struct ArState {
   float* yacc = nullptr;        // [max_streams][YCOPIES][768] batched mlp c_proj K-slice partials (fp32);
                                 // a row's copies adjacent: spaced by max_streams rows they shared
                                 // L2 channels (B = 1: 82.6 vs 69.6 us/step at max_streams 32)
-  uint32_t* hctr = nullptr;     // ar_qkv_attn_kernel: per-head c_attn counters [8][8 XCD shards][32] (zero between launches)
-  uint32_t* hdone = nullptr;    // [1] its blocks finished (the last one zeroes the counters)
-  uint32_t* htmo = nullptr;     // [1] sticky timeout flag of its waits (cleared by lvx_check_errors)
   void* kc = nullptr;           // [4][kv_chunks][max_streams][8][KV_CHUNK][96] (kv_at)
   void* vc = nullptr;
   int max_pos = 0, max_streams = 0, kv_chunks = 0;

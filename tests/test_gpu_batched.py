@@ -154,31 +154,6 @@ def test_qkv_ksplit_matches_one_launch_cattn(B, kv):
         e.close()
 
 
-@pytest.mark.parametrize("B", [9, 16, 17, 32])
-def test_fused_cattn_attention_matches_two_launches(B):
-    """Round 4: c_attn and the attention in one launch (ar_qkv_attn_kernel, option fuse_attn = 1, the
-    default at ln_max < B <= 32 with bf16 KV): the attention blocks wait in-launch for the c_attn
-    K-slice partials of their head. Against the two launches (fuse_attn = 0, the one-launch c_attn with
-    the KV append in its epilogue): tokens and logits bit for bit, permuted slots, ragged positions,
-    and again over a second call (the in-launch counters re-zeroed by every launch)."""
-    from llmvox_amd.engine import build_engine
-    e = build_engine(0, "bf16", "bf16", max_streams=64, max_positions=512, max_codec_frames=256)
-    try:
-        texts = _texts(B, 128, seed=23)
-        order = list(np.random.default_rng(B + 1).permutation(B))
-        prefix = set(range(1, B, 4))
-        res = []
-        for fa in (1, 0, 1):
-            e.set_option("fuse_attn", fa)
-            res.append(_run(e, order, texts, prefix, 37, 80))
-        for r in (res[1], res[2]):
-            np.testing.assert_array_equal(res[0][0], r[0])
-            np.testing.assert_array_equal(res[0][1], r[1])
-    finally:
-        e.set_option("fuse_attn", 1)
-        e.close()
-
-
 @pytest.mark.parametrize("B,kv", [(8, "bf16"), (8, "fp8"), (6, "bf16")])
 def test_rows_structure_at_small_b(B, kv):
     """Option ln_max below B runs a small batch on the rows-kernel structure (rows kernel + K-split
