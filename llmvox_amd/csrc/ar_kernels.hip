@@ -2585,6 +2585,8 @@ static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_
     hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2, 8>), grid, dim3(512), 0, s, st, l, ns_max, direct, selcopy);
   else if (nw8 && !qkv && kvdtype == LVX_DTYPE_FP8)
     hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t, 2, 8>), grid, dim3(512), 0, s, st, l, ns_max, direct, selcopy);
+  // (round 4, fp32 KV at B = 32, measured slower: 8 waves with 128-key tiles 212.6, 3 tiles in flight
+  // per wave 218.0 vs 211.7 us/step)
   else if (qkv && kvdtype == LVX_DTYPE_F32)  // fp32 parity mode: ar_qkv_ksplit_f32_kernel's partials
     hipLaunchKernelGGL((ar_attn_v2_kernel<float, 2, 4, true>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
   else if (qkv && kvdtype == LVX_DTYPE_BF16 && nw8)  // (ksplit with ln_max < B <= 8: the same 8-wave blocks)
