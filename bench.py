@@ -780,7 +780,7 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
     return dt, tok_bufs[(K - 1) & 1], codec_stream, tok_bufs, pcm_bufs
 
 
-def parity_mode_line(S, chunk, K=4, Wm=1):
+def parity_mode_line(S, chunk, K=4, Wm=1, codec_overlap=False):
     """The fp32 parity mode (weights, KV and codec in fp32: bit-exact ids against the reference,
     tests/test_gpu_parity.py, test_gpu_f32b.py) on the headline's workload: K = 4 chunks of one
     1,024-token utterance per stream (KV positions 0..1,023, as configs[2]'s utterances; VERDICT r03
@@ -794,7 +794,7 @@ def parity_mode_line(S, chunk, K=4, Wm=1):
         plans = np.stack([plan_for(sentence_ids(SENTENCE if g == 0 else random_sentence(rng)), 0, n_pos)
                           for g in range(S)])
         mine = torch.from_numpy(plans).to(eng.device)
-        dt, _, _, _, _ = run_chunks(eng, mine, S, chunk, K, Wm)
+        dt, _, _, _, _ = run_chunks(eng, mine, S, chunk, K, Wm, codec_overlap=codec_overlap)
         return {"value": round(S * K * chunk / dt, 1), "unit": "speech tokens/s", "ms_per_step": round(dt / K * 1e3, 3),
                 "steps": K, "warmup": Wm, "dtype": "fp32", "kv_dtype": "fp32", "codec_weights": "fp32",
                 "streams": S, "kv_positions": f"0..{K * chunk - 1}",
@@ -1015,7 +1015,7 @@ def main():
 
     parity = None
     if rank == 0 and world == 1 and not args.no_parity_line and args.dtype == "bf16" and args.config in (1, 2):
-        parity = parity_mode_line(S, chunk, K=max(1, min(4, utt // chunk)))
+        parity = parity_mode_line(S, chunk, K=max(1, min(4, utt // chunk)), codec_overlap=args.codec_overlap)
         parity["ratio_to_headline"] = round(parity["value"] / value, 4)
 
     cpu = None

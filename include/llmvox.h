@@ -155,11 +155,15 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
  *   "codec_g2"     1: large-M bf16 codec GEMMs on the 128 x 128 MFMA tile kernel; 0: the general one;
  *   "codec_skinny" 1: bf16 codec weight GEMMs with M <= 384 frames on the K-split-over-waves kernel
  *                     (no split-K combine); 0: the tile kernels;
- *   "codec_g3f"    1: fp32 (parity mode) codec GEMMs with >= 192 tiles of 128 x 192 on the LDS-DMA
- *                     kernel (exact-fp32 v_mfma_f32_16x16x4_f32); 0: the 64 x 64 register-staged one;
+ *   "codec_g3f"    fp32 (parity mode) codec GEMMs with >= 192 tiles of 128 x 192: 2 (default): the
+ *                     LDS-DMA kernel with fp32 operands split into bf16 hi + lo, hi.hi + lo.hi + hi.lo
+ *                     on v_mfma_f32_16x16x32_bf16 (fp32 accumulation); 1: the LDS-DMA kernel with
+ *                     exact-fp32 v_mfma_f32_16x16x4_f32; 0: the 64 x 64 register-staged exact one;
  *   "codec_exp"    codec development bits, 0 = production kernels; bit 0: the general GroupNorm
  *                     kernel at every L (same bits); bits 1-2: dwconv+AdaLN frames per block at
- *                     >= 2,048 frames (0: 4, 1: 16, 2: 32, 3: 8; same bits);
+ *                     >= 2,048 frames (0: 4, 1: 16, 2: 32, 3: 8; same bits); bit 3: library
+ *                     exp / sin / cos in the bf16 iSTFT; bit 4: fp32 bf16x3 GEMMs split their
+ *                     operands in registers, no split-image producers (same bits);
  *   "exp"          development bits, 0 = production kernels; bit 1: the one-launch c_attn even with
  *                     option ksplit = 1 (bit-identical: tests/test_gpu_batched.py); bit 2: the
  *                     batched MFMA GEMMs read the row-major weights instead of the fragment-packed

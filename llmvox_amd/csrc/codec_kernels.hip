@@ -47,6 +47,8 @@ struct GemmArgs {
   uint32_t* tick;            // gemm_mfma_kernel split-K: per-tile arrival counters of the in-launch
                              // combine (zero between launches: the last arriver resets its own), or
                              // null for the separate reduce kernel
+  int asplit;                // fp32 parity mode, bf16x3 GEMM: A is a split image (split_store), not fp32
+  int csplit;                // fp32 parity mode, bf16x3 GEMM (bias + GELU): C written as a split image
 };
 
 template <typename T> __device__ __forceinline__ void load8(const T* p, float* v);
@@ -704,12 +706,50 @@ __device__ __forceinline__ void glds16(const void* src, unsigned char* lds) {
                                    (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
 }
 
-template <int AMODE, int EPI, typename TC, int NS, typename TA = bf16_t>
+// fp32 -> bf16x3 operand split (SPLIT form of gemm_glds_kernel<float>): x = hi + lo + r with
+// hi = bf16_rn(x), lo = bf16_rn(x - hi) (x - hi is exact in fp32), |r| <= 2^-17 |x|. The 8 elements are
+// the two 16-B fragments of one row (k 4 g + e of the k-tile's two 16-k halves, g = lane >> 4); the
+// weights' split image (upload_cw in lvx_api.cpp) holds the same k order, precomputed
+__device__ __forceinline__ void split_bf16x3(const f32x4v& x0, const f32x4v& x1, bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const __bf16 h0 = (__bf16)x0[e], h1 = (__bf16)x1[e];
+    hi[e] = h0;
+    hi[4 + e] = h1;
+    lo[e] = (__bf16)(x0[e] - (float)h0);
+    lo[4 + e] = (__bf16)(x1[e] - (float)h1);
+  }
+}
+
+// the split image of an fp32 row [K] (K % 32 == 0), as the bf16x3 GEMM's operands are read: per 32-k
+// block, 16-B segment g < 4 holds bf16 hi of k = 4 g + e and 16 + 4 g + e (e < 4), segment 4 + g the lo
+// parts; same size as the fp32 row. Element c of a row: hi at bf16 index split_pos(c), lo 32 later
+__device__ __forceinline__ int split_pos(int c) {
+  const int r = c & 31;
+  return 2 * (c & ~31) + ((r >> 2) & 3) * 8 + (r >> 4) * 4 + (r & 3);
+}
+__device__ __forceinline__ void split_store(float* row, int c, float v) {
+  bf16_t* o = reinterpret_cast<bf16_t*>(row) + split_pos(c);
+  const bf16_t hi = f32_to_bf16(v);
+  o[0] = hi;
+  o[32] = f32_to_bf16(v - bf16_to_f32(hi));
+}
+
+// SPLIT bits (TA = float): 1 bf16x3 products, 2 A is a split image (no in-register split), 4 C written
+// as a split image (the next GEMM's A; E_BIAS_GELU, N % 32 == 0)
+template <int AMODE, int EPI, typename TC, int NS, typename TA = bf16_t, int SPLIT = 0>
 __global__ __launch_bounds__(512, NS == 2 ? 2 : 1) void gemm_glds_kernel(GemmArgs g) {
   // TA = bf16: 64-deep k-tiles, v_mfma_f32_16x16x32_bf16. TA = float (the fp32 parity mode): the same
   // 128-B LDS rows hold 32 k of fp32, and each 16-B fragment (4 consecutive k of one row) feeds four
   // exact-fp32 v_mfma_f32_16x16x4_f32, MFMA e taking element e from every lane group (A and B
-  // permuted alike: the k order inside a 16-k block is 4 g + e)
+  // permuted alike: the k order inside a 16-k block is 4 g + e). TA = float, SPLIT: the k-tile's two
+  // fragments of a row are split into bf16 hi / lo (split_bf16x3) and multiplied as
+  // hi.hi + lo.hi + hi.lo by three v_mfma_f32_16x16x32_bf16 (fp32 accumulation; the lo.lo term,
+  // <= 2^-16 of a product, dropped): 3 MFMAs of 16 cycles per 32 k and 16 x 16 tile instead of 8 of
+  // 32. The weights come as their split image (stored right behind the fp32 matrix, g.N rows of
+  // g.ldw: upload_cw), whose 128-B rows the DMA stages like fp32 rows: segment g = hi, 4 + g = lo
+  static_assert(!SPLIT || sizeof(TA) == 4, "the split is of fp32 operands");
+  static_assert(!(SPLIT & 4) || (EPI == E_BIAS_GELU && sizeof(TC) == 4), "split output: fp32 GELU epilogue");
   constexpr int EPS = 16 / (int)sizeof(TA);  // elements per 16-B segment
   constexpr int BKE = 8 * EPS;               // elements per k-tile (64 bf16 / 32 fp32)
   __shared__ __attribute__((aligned(1024))) unsigned char smem[NS * G3_STAGE];  // the only LDS object
@@ -723,7 +763,7 @@ __global__ __launch_bounds__(512, NS == 2 ? 2 : 1) void gemm_glds_kernel(GemmArg
   const int gm = min(8, ntm - grp * 8);
   const int m0 = (grp * 8 + within % gm) * G3_BM, n0 = (within / gm) * G3_BN;
   const TA* __restrict__ A = reinterpret_cast<const TA*>(g.A);
-  const TA* __restrict__ W = reinterpret_cast<const TA*>(g.W);
+  const TA* __restrict__ W = reinterpret_cast<const TA*>(g.W) + (SPLIT ? (size_t)g.N * g.ldw : 0);
   const int nkt = g.K / BKE;  // K % BKE == 0 (checked by the launcher)
   // DMA geometry: lane -> row lane / 8 of a 1-KB piece, LDS slot lane % 8 <- global segment gseg
   const int lrow = lane >> 3, gseg = (lane & 7) ^ lrow;
@@ -795,6 +835,31 @@ __global__ __launch_bounds__(512, NS == 2 ? 2 : 1) void gemm_glds_kernel(GemmArg
       for (int j = 0; j < 3; ++j)
         fb[kk][j] = *reinterpret_cast<const Frag*>(sb + (wn * 48 + j * 16 + frow) * 128 + slot);
     }
+    if constexpr (SPLIT) {
+      bf16x8 bh[3], bl[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        bh[j] = __builtin_bit_cast(bf16x8, fb[0][j]);
+        bl[j] = __builtin_bit_cast(bf16x8, fb[1][j]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        bf16x8 ah, al;
+        if constexpr ((SPLIT & 2) != 0) {
+          ah = __builtin_bit_cast(bf16x8, fa[0][i]);
+          al = __builtin_bit_cast(bf16x8, fa[1][i]);
+        } else {
+          split_bf16x3(fa[0][i], fa[1][i], ah, al);
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[j], ah, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[j], ah, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[j], al, acc[i][j], 0, 0, 0);
+        }
+      }
+      continue;
+    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -856,7 +921,18 @@ __global__ __launch_bounds__(512, NS == 2 ? 2 : 1) void gemm_glds_kernel(GemmArg
         const int row = m0 + wm * 64 + i * 16 + frow;
         if (col < g.N && row < g.M) {
           TC* p = C + (size_t)row * g.ldc + col;
-          if constexpr (sizeof(TC) == 2) {
+          if constexpr ((SPLIT & 4) != 0) {  // 4 consecutive k of the split image: 8-B hi, 8-B lo
+            uint32_t h[4], l[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const bf16_t hb = f32_to_bf16(acc[i][j][e]);
+              h[e] = hb;
+              l[e] = f32_to_bf16(acc[i][j][e] - bf16_to_f32(hb));
+            }
+            bf16_t* o = reinterpret_cast<bf16_t*>(C + (size_t)row * g.ldc) + split_pos(col);
+            *reinterpret_cast<uint2*>(o) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+            *reinterpret_cast<uint2*>(o + 32) = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
+          } else if constexpr (sizeof(TC) == 2) {
             *reinterpret_cast<uint2*>(p) =
                 make_uint2((uint32_t)f32_to_bf16(acc[i][j][0]) | ((uint32_t)f32_to_bf16(acc[i][j][1]) << 16),
                            (uint32_t)f32_to_bf16(acc[i][j][2]) | ((uint32_t)f32_to_bf16(acc[i][j][3]) << 16));
@@ -907,21 +983,27 @@ __global__ __launch_bounds__(512, NS == 2 ? 2 : 1) void gemm_glds_kernel(GemmArg
 }
 
 // option codec_g3 (default 1, Opts in lvx_internal.h): 1: large-M bf16 GEMMs on gemm_glds_kernel; 0: off (cross-check)
-// option codec_g3f (default 1, Opts in lvx_internal.h): 1: large-M fp32 (parity mode) GEMMs on gemm_glds_kernel<float>; 0: gemm_mfma
+// option codec_g3f (default 2, Opts in lvx_internal.h): large-M fp32 (parity mode) GEMMs on gemm_glds_kernel<float>,
+// 2: bf16x3 split products, 1: exact fp32 products (cross-check); 0: gemm_mfma (exact fp32, cross-check)
 // the LDS-DMA kernel needs enough 128 x 192 tiles to fill the chip
 template <typename TA = bf16_t>
 static bool g3_ok(const GemmArgs& g) {
   return opts().codec_g3 && g.K % (128 / (int)sizeof(TA)) == 0 && ((g.M + G3_BM - 1) / G3_BM) * ((g.N + G3_BN - 1) / G3_BN) >= 192;
 }
-template <int AMODE, int EPI, typename TC, typename TA = bf16_t>
+// the fp32 parity mode's bf16x3 form of gemm_glds_kernel (option codec_g3f = 2)
+static bool g3_split(const GemmArgs& g) { return opts().codec_g3f == 2 && g3_ok<float>(g); }
+// its operand given as a split image by the producer kernel (codec_exp bit 16: every bf16x3 GEMM splits
+// its fp32 operand in registers instead; the same hi / lo bits either way)
+static bool g3_split_in(const GemmArgs& g) { return g3_split(g) && !(opts().codec_exp & 16); }
+template <int AMODE, int EPI, typename TC, typename TA = bf16_t, int SPLIT = 0>
 static void g3_launch(GemmArgs g, hipStream_t s) {
   static_assert(EPI != E_SCALE, "weight GEMMs only");
   dim3 grid((g.N + G3_BN - 1) / G3_BN, (g.M + G3_BM - 1) / G3_BM);
   // more tiles than CUs: two blocks per CU (2 stages, 80 KB each), else one (3 stages, 120 KB).
   // Kernel traces of the 32 x 256-frame decode: N = 2,304 (768 tiles) 52.5 vs 61 us, N = 768 (256
   // tiles) 40.4 vs 47 us; 16 x 256 frames (N = 2,304: 384 tiles) 1.57 vs 1.70 ms per decode
-  if (grid.x * grid.y > 256) hipLaunchKernelGGL((gemm_glds_kernel<AMODE, EPI, TC, 2, TA>), grid, dim3(512), 0, s, g);
-  else hipLaunchKernelGGL((gemm_glds_kernel<AMODE, EPI, TC, 3, TA>), grid, dim3(512), 0, s, g);
+  if (grid.x * grid.y > 256) hipLaunchKernelGGL((gemm_glds_kernel<AMODE, EPI, TC, 2, TA, SPLIT>), grid, dim3(512), 0, s, g);
+  else hipLaunchKernelGGL((gemm_glds_kernel<AMODE, EPI, TC, 3, TA, SPLIT>), grid, dim3(512), 0, s, g);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1074,7 +1156,16 @@ static void gemm_w(const GemmArgs& g, hipStream_t s) {
     else gemm_launch<true, TA, bf16_t, AMODE, EPI, TC>(g, 1, s);
   } else {
     static_assert(sizeof(TA) == 4 && sizeof(TC) == 4, "parity mode keeps fp32 activations");
-    if (EPI != E_SCALE && opts().codec_g3f && g3_ok<float>(g)) g3_launch<AMODE, (EPI == E_SCALE ? E_BIAS : EPI), float, float>(g, s);
+    constexpr int EW = EPI == E_SCALE ? E_BIAS : EPI;
+    if (EPI != E_SCALE && g3_split(g)) {
+      // A / C as split images only where the orchestration asked for them (decode_impl's ConvNeXt loop)
+      if constexpr (AMODE == A_PLAIN && EW == E_BIAS_GELU) {
+        if (g.asplit && g.csplit) return g3_launch<AMODE, EW, float, float, 7>(g, s);
+        if (g.csplit) return g3_launch<AMODE, EW, float, float, 5>(g, s);
+      }
+      if (g.asplit) return g3_launch<AMODE, EW, float, float, 3>(g, s);
+      g3_launch<AMODE, EW, float, float, 1>(g, s);
+    } else if (EPI != E_SCALE && opts().codec_g3f == 1 && g3_ok<float>(g)) g3_launch<AMODE, EW, float, float>(g, s);
     else gemm_launch<false, float, float, AMODE, EPI, float>(g, 1, s);
   }
 }
@@ -1144,9 +1235,30 @@ __device__ __forceinline__ void store4(bf16_t* p, float4 v) {
                                             (uint32_t)f32_to_bf16(v.z) | ((uint32_t)f32_to_bf16(v.w) << 16));
 }
 
+// 4 consecutive channels c..c+3 (c % 4 == 0) of row `row`: plain, or (SPO, fp32 parity mode) into the
+// row's split image for a bf16x3 conv / 1x1 GEMM (split_store's layout: 8-B hi, 8-B lo)
+template <bool SPO, typename TO>
+__device__ __forceinline__ void gn_store(TO* row, int c, float4 o) {
+  if constexpr (SPO) {
+    const float v[4] = {o.x, o.y, o.z, o.w};
+    uint32_t h[4], l[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const bf16_t hb = f32_to_bf16(v[e]);
+      h[e] = hb;
+      l[e] = f32_to_bf16(v[e] - bf16_to_f32(hb));
+    }
+    bf16_t* p = reinterpret_cast<bf16_t*>(row) + split_pos(c);
+    *reinterpret_cast<uint2*>(p) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+    *reinterpret_cast<uint2*>(p + 32) = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
+  } else {
+    store4(row + c, o);
+  }
+}
+
 // GroupNorm (+ swish) of one (stream, group), decoder/models.py:15-16,58-78 (ResnetBlock norms)
 // and :107-127 (AttnBlock norm): y = swish?((x - mean) * rstd * w + b)
-template <bool SWISH, typename TO>
+template <bool SWISH, typename TO, bool SPO = false>
 __global__ __launch_bounds__(256) void gn_apply_kernel(const float* __restrict__ x, int L, const float* __restrict__ gw,
                                                        const float* __restrict__ gb, TO* __restrict__ y) {
   __shared__ float red[4];
@@ -1172,7 +1284,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const float* __restrict__
     float4 o = make_float4((v.x - mean) * rstd * w.x + bb.x, (v.y - mean) * rstd * w.y + bb.y,
                            (v.z - mean) * rstd * w.z + bb.z, (v.w - mean) * rstd * w.w + bb.w);
     if (SWISH) o = make_float4(swishf(o.x), swishf(o.y), swishf(o.z), swishf(o.w));
-    store4(y + off + (size_t)t * CD + q * 4, o);
+    gn_store<SPO>(y + ((size_t)b * L + t) * CD, gi * CG + q * 4, o);
   }
 }
 
@@ -1180,7 +1292,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const float* __restrict__
 // thread, issued before the affine operands (gn_apply_kernel waited for those at its loop head: one
 // more round trip ahead of the data), values kept in registers (no LDS copy: 4 blocks per CU). Same
 // sums in the same order as gn_apply_kernel: same bits.
-template <bool SWISH, typename TO>
+template <bool SWISH, typename TO, bool SPO = false>
 __global__ __launch_bounds__(256) void gn_apply1_kernel(const float* __restrict__ x, int L, const float* __restrict__ gw,
                                                         const float* __restrict__ gb, TO* __restrict__ y) {
   __shared__ float red[4];
@@ -1215,14 +1327,23 @@ __global__ __launch_bounds__(256) void gn_apply1_kernel(const float* __restrict_
     float4 o = make_float4((v[u].x - mean) * rstd * w.x + bb.x, (v[u].y - mean) * rstd * w.y + bb.y,
                            (v[u].z - mean) * rstd * w.z + bb.z, (v[u].w - mean) * rstd * w.w + bb.w);
     if (SWISH) o = make_float4(swishf(o.x), swishf(o.y), swishf(o.z), swishf(o.w));
-    store4(y + off + (size_t)t * CD + qq * 4, o);
+    gn_store<SPO>(y + ((size_t)b * L + t) * CD, gi * CG + qq * 4, o);
   }
 }
 // codec A/B bits (development): 1 the general gn_apply at every L; 6: dwconv FT at >= 2,048 frames
-// (0: 4, 2: 16, 4: 32, 6: 8); 8: library exp / sin / cos in the bf16 iSTFT
+// (0: 4, 2: 16, 4: 32, 6: 8); 8: library exp / sin / cos in the bf16 iSTFT; 16: fp32 bf16x3 GEMMs
+// split their operands in registers (no split-image producers; same bits)
 // option codec_exp (default 0, Opts in lvx_internal.h):
 template <bool SWISH, typename TO>
-static void gn_apply_launch(const float* x, int B, int L, const float* gw, const float* gb, TO* y, hipStream_t s) {
+static void gn_apply_launch(const float* x, int B, int L, const float* gw, const float* gb, TO* y, hipStream_t s,
+                            bool spo = false) {  // spo: y as split images (fp32, the consumer GEMM's asplit)
+  if constexpr (sizeof(TO) == 4) {
+    if (spo) {
+      if (L * 6 <= 8 * 256 && !(opts().codec_exp & 1)) hipLaunchKernelGGL((gn_apply1_kernel<SWISH, TO, true>), dim3(GN_G, B), dim3(256), 0, s, x, L, gw, gb, y);
+      else hipLaunchKernelGGL((gn_apply_kernel<SWISH, TO, true>), dim3(GN_G, B), dim3(256), 0, s, x, L, gw, gb, y);
+      return;
+    }
+  }
   if (L * 6 <= 8 * 256 && !(opts().codec_exp & 1)) hipLaunchKernelGGL((gn_apply1_kernel<SWISH, TO>), dim3(GN_G, B), dim3(256), 0, s, x, L, gw, gb, y);
   else hipLaunchKernelGGL((gn_apply_kernel<SWISH, TO>), dim3(GN_G, B), dim3(256), 0, s, x, L, gw, gb, y);
 }
@@ -1290,7 +1411,8 @@ __global__ __launch_bounds__(256) void gn_adaln_kernel(const float* __restrict__
 // frames = 1.9 TB/s). Taps outside [0, L) read a clamped frame and are dropped by a select, in the
 // guarded sum's order; the LayerNorm reductions follow row_ln's order (same bits as that form).
 // FT = 16 for large M, 4 when there are few frames.
-template <typename TO, int FT>
+// SPO (fp32 parity mode): y written as the split image of its rows (split_store) for pwconv1's bf16x3 GEMM
+template <typename TO, int FT, bool SPO = false>
 __global__ __launch_bounds__(256) void dwconv_adaln_tile_kernel(const float* __restrict__ x, int L,
                                                                 const float* __restrict__ dwt,
                                                                 const float* __restrict__ dwb,
@@ -1365,14 +1487,17 @@ __global__ __launch_bounds__(256) void dwconv_adaln_tile_kernel(const float* __r
     const float rstd = 1.0f / sqrtf(r * (1.0f / CD) + 1e-6f);
     if (t0 + f < L) {
 #pragma unroll
-      for (int j = 0; j < 3; ++j)
-        store_out<TO>(y + ((size_t)b * L + t0 + f) * CD + tid + 256 * j, v[j][f] * rstd * sc[j] + sh[j]);
+      for (int j = 0; j < 3; ++j) {
+        const float o = v[j][f] * rstd * sc[j] + sh[j];
+        if constexpr (SPO) split_store(reinterpret_cast<float*>(y + ((size_t)b * L + t0 + f) * CD), tid + 256 * j, o);
+        else store_out<TO>(y + ((size_t)b * L + t0 + f) * CD + tid + 256 * j, o);
+      }
     }
   }
 }
 
-// final_layer_norm (affine, eps 1e-6)
-template <typename TO>
+// final_layer_norm (affine, eps 1e-6); SPO: y as split images (fp32 parity mode, bf16x3 head GEMM)
+template <typename TO, bool SPO = false>
 __global__ __launch_bounds__(256) void ln_affine_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                         const float* __restrict__ bb, TO* __restrict__ y) {
   __shared__ float red[4];
@@ -1389,7 +1514,8 @@ __global__ __launch_bounds__(256) void ln_affine_kernel(const float* __restrict_
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int c = tid + 256 * j;
-    store_out<TO>(y + (size_t)m * CD + c, v[j] * wv[j] + bv[j]);
+    if constexpr (SPO) split_store(reinterpret_cast<float*>(y + (size_t)m * CD), c, v[j] * wv[j] + bv[j]);
+    else store_out<TO>(y + (size_t)m * CD + c, v[j] * wv[j] + bv[j]);
   }
 }
 
@@ -1686,27 +1812,33 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
   g.C = x; g.ldc = CD; g.bias = w.embed_b;
   gemm_w<TW, TAct, A_CONV, E_BIAS>(g, s);
 
+  // fp32 parity mode: a GroupNorm output that feeds a bf16x3 GEMM goes to HBM as split images (the
+  // GroupNorm is that operand's only producer and the GEMM its only reader)
+  auto spl = [&](GemmArgs& c) {
+    if constexpr (sizeof(TW) == 4) c.asplit = g3_split_in(c);
+    return c.asplit != 0;
+  };
   auto resnet = [&](int i) {  // models.py:58-78
-    gn_apply_launch<true, TAct>(x, B, L, w.rn_n1w[i], w.rn_n1b[i], gn, s);
     GemmArgs c{};
     c.ws = sc.ws;
     c.L = L; c.M = M; c.cin = CD; c.taps = 3; c.K = 3 * CD; c.N = CD; c.ldw = 3 * CD;
     c.A = gn; c.lda = CD;
     c.W = w.rn_c1w[i]; c.wscale = w.rn_c1s[i]; c.bias = w.rn_c1b[i]; c.C = t1; c.ldc = CD;
+    gn_apply_launch<true, TAct>(x, B, L, w.rn_n1w[i], w.rn_n1b[i], gn, s, spl(c));
     gemm_w<TW, TAct, A_CONV, E_BIAS>(c, s);
-    gn_apply_launch<true, TAct>(t1, B, L, w.rn_n2w[i], w.rn_n2b[i], gn, s);
+    gn_apply_launch<true, TAct>(t1, B, L, w.rn_n2w[i], w.rn_n2b[i], gn, s, c.asplit != 0);
     c.W = w.rn_c2w[i]; c.wscale = w.rn_c2s[i]; c.bias = w.rn_c2b[i]; c.C = x; c.res = x; c.ldr = CD;
     gemm_w<TW, TAct, A_CONV, E_BIAS_RES>(c, s);
   };
   resnet(0);
   resnet(1);
   {  // AttnBlock (models.py:107-127)
-    gn_apply_launch<false, TAct>(x, B, L, w.at_nw, w.at_nb, gn, s);
     GemmArgs c{};
     c.ws = sc.ws;
     c.L = L; c.M = M; c.K = CD; c.N = 3 * CD; c.ldw = CD;
     c.A = gn; c.lda = CD;
     c.W = w.at_qkv_w; c.wscale = w.at_qkv_s; c.bias = w.at_qkv_b; c.C = t1; c.ldc = CFF;
+    gn_apply_launch<false, TAct>(x, B, L, w.at_nw, w.at_nb, gn, s, spl(c));
     gemm_w<TW, TAct, A_PLAIN, E_BIAS>(c, s);
     const int ldS = (L + 3) & ~3;
     float* S = sc.att;            // [B][L][ldS]
@@ -1750,7 +1882,28 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
                      w.ada_scale + (size_t)bw * CD, w.ada_shift + (size_t)bw * CD, x);
   for (int i = 0; i < 12; ++i) {  // ConvNeXt blocks (modules.py:43-60)
     const int dwft = (opts().codec_exp >> 1) & 3;
-    if (M >= 2048 && dwft == 3)
+    GemmArgs c{};
+    c.ws = sc.ws;
+    c.M = M; c.L = L; c.N = CFF; c.K = CD; c.ldw = CD;
+    c.A = t2a; c.lda = CD; c.W = w.pw1_w[i]; c.wscale = w.pw1_s[i]; c.bias = w.pw1_b[i]; c.C = t1a; c.ldc = CFF;
+    GemmArgs d{};
+    d.ws = sc.ws;
+    d.M = M; d.L = L; d.N = CD; d.K = CFF; d.ldw = CFF;
+    d.A = t1a; d.lda = CFF; d.W = w.pw2_w[i]; d.wscale = w.pw2_s[i]; d.bias = w.pw2_b[i]; d.gamma = w.gamma[i];
+    d.C = x; d.ldc = CD; d.res = x; d.ldr = CD;
+    // fp32 parity mode with both GEMMs on the bf16x3 kernel: the dwconv output and pwconv1's output
+    // go to HBM as split images (hi / lo bf16 of each element, split_store: the same bits the GEMMs'
+    // in-register split makes, computed once per element instead of once per reading block)
+    if constexpr (sizeof(TW) == 4) {
+      const bool s1 = g3_split_in(c) && dwft == 0, s2 = g3_split_in(d);
+      c.asplit = s1;
+      c.csplit = s1 && s2;
+      d.asplit = s1 && s2;
+    }
+    if (c.asplit)
+      hipLaunchKernelGGL((dwconv_adaln_tile_kernel<TAct, 4, true>), dim3((L + 3) / 4, B), dim3(256), 0, s, x, L, w.dw_w[i],
+                         w.dw_b[i], w.cn_scale[i] + (size_t)bw * CD, w.cn_shift[i] + (size_t)bw * CD, t2a);
+    else if (M >= 2048 && dwft == 3)
       hipLaunchKernelGGL((dwconv_adaln_tile_kernel<TAct, 8>), dim3((L + 7) / 8, B), dim3(256), 0, s, x, L, w.dw_w[i],
                          w.dw_b[i], w.cn_scale[i] + (size_t)bw * CD, w.cn_shift[i] + (size_t)bw * CD, t2a);
     else if (M >= 2048 && dwft == 2)
@@ -1762,24 +1915,16 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
     else
       hipLaunchKernelGGL((dwconv_adaln_tile_kernel<TAct, 4>), dim3((L + 3) / 4, B), dim3(256), 0, s, x, L, w.dw_w[i],
                          w.dw_b[i], w.cn_scale[i] + (size_t)bw * CD, w.cn_shift[i] + (size_t)bw * CD, t2a);
-    GemmArgs c{};
-    c.ws = sc.ws;
-    c.M = M; c.L = L; c.N = CFF; c.K = CD; c.ldw = CD;
-    c.A = t2a; c.lda = CD; c.W = w.pw1_w[i]; c.wscale = w.pw1_s[i]; c.bias = w.pw1_b[i]; c.C = t1a; c.ldc = CFF;
     gemm_w<TW, TAct, A_PLAIN, E_BIAS_GELU, TAct>(c, s);
-    GemmArgs d{};
-    d.ws = sc.ws;
-    d.M = M; d.L = L; d.N = CD; d.K = CFF; d.ldw = CFF;
-    d.A = t1a; d.lda = CFF; d.W = w.pw2_w[i]; d.wscale = w.pw2_s[i]; d.bias = w.pw2_b[i]; d.gamma = w.gamma[i];
-    d.C = x; d.ldc = CD; d.res = x; d.ldr = CD;
     gemm_w<TW, TAct, A_PLAIN, E_BIAS_GAMMA_RES>(d, s);
   }
-  hipLaunchKernelGGL(ln_affine_kernel<TAct>, dim3(M), dim3(256), 0, s, x, w.fln_w, w.fln_b, t2a);
-  {  // ISTFTHead.out Linear(768 -> 1282)
+  {  // final LayerNorm, ISTFTHead.out Linear(768 -> 1282)
     GemmArgs h{};
     h.ws = sc.ws;
     h.M = M; h.L = L; h.N = 2 * NB; h.K = CD; h.ldw = CD;
     h.A = t2a; h.lda = CD; h.W = w.head_w; h.wscale = w.head_s; h.bias = w.head_b; h.C = sc.spec; h.ldc = 2 * NB;
+    if (spl(h)) hipLaunchKernelGGL((ln_affine_kernel<TAct, true>), dim3(M), dim3(256), 0, s, x, w.fln_w, w.fln_b, t2a);
+    else hipLaunchKernelGGL(ln_affine_kernel<TAct>, dim3(M), dim3(256), 0, s, x, w.fln_w, w.fln_b, t2a);
     gemm_w<TW, TAct, A_PLAIN, E_BIAS>(h, s);
   }
   if (sizeof(TAct) == 2 && !(opts().codec_exp & 8))

@@ -209,9 +209,36 @@ struct lvx_ctx {
   }
   // codec GEMM weights: the weight dtype, or e4m3fn with one scale per output row (codec_dtype FP8:
   // s = max|w_row| / 448, q = RNE(w / s) saturated; dequantised exactly to bf16 in the GEMM loader)
+  //
+  // fp32 (parity mode) with K % 32 == 0: the matrix [rows][K] is followed in the same allocation by its
+  // bf16x3 split image (same size, read by gemm_glds_kernel<float, SPLIT> in place of the fp32 rows):
+  // per row and 32-k block kb, 16-B segment g (g < 4) holds bf16_rn(w) of k = kb + 4 g + e and
+  // kb + 16 + 4 g + e (e = 0..3), segment 4 + g the lo parts bf16_rn(w - hi) of the same k (the k
+  // order the kernel's A fragments are read in)
   int upload_cw(const std::vector<float>& v, int rows, const void** out, const float** scale_out) {
-    if (cfg.codec_dtype != LVX_DTYPE_FP8) return upload_w(v, out);
     const size_t K = v.size() / rows;
+    if (cfg.codec_dtype != LVX_DTYPE_FP8 && cfg.weight_dtype == LVX_DTYPE_F32 && K % 32 == 0) {
+      std::vector<float> both(2 * v.size());
+      std::memcpy(both.data(), v.data(), v.size() * 4);
+      bf16_t* sp = reinterpret_cast<bf16_t*>(both.data() + v.size());
+      for (size_t n = 0; n < (size_t)rows; ++n)
+        for (size_t kb = 0; kb < K; kb += 32) {
+          bf16_t* o = sp + (n * K + kb) * 2;  // 128 B: 8 segments of 8 bf16
+          for (int g = 0; g < 4; ++g)
+            for (int h = 0; h < 2; ++h)
+              for (int e = 0; e < 4; ++e) {
+                const float x = v[n * K + kb + 16 * h + 4 * g + e];
+                const bf16_t hi = f32_to_bf16(x);
+                const uint32_t hb = (uint32_t)hi << 16;
+                float hf;
+                std::memcpy(&hf, &hb, 4);
+                o[g * 8 + h * 4 + e] = hi;
+                o[(4 + g) * 8 + h * 4 + e] = f32_to_bf16(x - hf);
+              }
+        }
+      return upload_f32(both, reinterpret_cast<const float**>(out));
+    }
+    if (cfg.codec_dtype != LVX_DTYPE_FP8) return upload_w(v, out);
     std::vector<uint8_t> q(v.size());
     std::vector<float> sc(rows);
     for (int n = 0; n < rows; ++n) {
@@ -617,7 +644,7 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   else if (n == "codec_g2") o.codec_g2 = value != 0;
   else if (n == "codec_skinny") o.codec_skinny = value != 0;
   else if (n == "codec_g3") o.codec_g3 = value != 0;
-  else if (n == "codec_g3f") o.codec_g3f = value != 0;
+  else if (n == "codec_g3f") o.codec_g3f = std::min(std::max(value, 0), 2);
   else if (n == "codec_exp") o.codec_exp = value;
   else if (n == "exp") o.exp = value;
   else if (n == "f32b") o.f32b = value != 0;

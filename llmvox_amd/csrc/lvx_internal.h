@@ -33,7 +33,7 @@ struct Opts {
   int defer_select = 1;  // greedy select deferred into the next step's first kernel; 0: argmax kernel
   int fuse_mlp = 1;      // bf16, B <= 2: c_fc + gelu + mlp c_proj in one kernel; 0: two GEMV kernels
   int bt = 1;            // 1: batched v3 for 32 < B <= 64; 2: v3 for every batched B (cross-check); 0: off
-  int codec_g2 = 1, codec_skinny = 1, codec_g3 = 1, codec_g3f = 1;  // codec GEMM kernels (cross-checks)
+  int codec_g2 = 1, codec_skinny = 1, codec_g3 = 1, codec_g3f = 2;  // codec GEMM kernels (cross-checks)
   int codec_exp = 0;     // codec A/B bits (bit-identical variants)
   int exp = 0;           // AR A/B bits (bit-identical variants, tests/test_gpu_batched.py, test_gpu_f32b.py)
   int f32b = 1;          // fp32 batched steps on exact-fp32 MFMA; 0: the GEMV family
