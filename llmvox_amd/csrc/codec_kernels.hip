@@ -1537,13 +1537,15 @@ __global__ void feats_transpose_kernel(const float* __restrict__ f, int L, TO* _
 }
 
 // codes [B*L] -> [B*L][512]
+// SPO (fp32 parity mode): the rows as split images for the embed conv's bf16x3 GEMM (gn_store)
+template <bool SPO = false>
 __global__ void codes_gather_kernel(const float* __restrict__ cb, const int32_t* __restrict__ codes, float* __restrict__ out, int32_t* __restrict__ err) {
   const int m = blockIdx.x;
   const int raw = codes[m];
   const int code = min(max(raw, 0), 4095);  // clamped for the load; flagged (lvx_check_errors -> LVX_E_INDEX)
   if (threadIdx.x == 0 && raw != code) atomicOr(err, 4);
   const float4 v = reinterpret_cast<const float4*>(cb + (size_t)code * CIN)[threadIdx.x];
-  reinterpret_cast<float4*>(out + (size_t)m * CIN)[threadIdx.x] = v;
+  gn_store<SPO>(out + (size_t)m * CIN, 4 * threadIdx.x, v);
 }
 // bf16 mode: the rows as the embed conv's bf16 operand
 __global__ void codes_gather_bf16_kernel(const float* __restrict__ cb, const int32_t* __restrict__ codes,
@@ -1793,15 +1795,14 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
   TAct* t1a = reinterpret_cast<TAct*>(t1);    // GELU(pwconv1) (pwconv2 operand)
   // a3: features, time-major [M][512]
   TAct* feats = reinterpret_cast<TAct*>(sc.feats);
-  if (codes) {
-    if constexpr (sizeof(TAct) == 2) hipLaunchKernelGGL(codes_gather_bf16_kernel, dim3(M), dim3(CIN / 4), 0, s, w.codebook, codes, feats, sc.err);
-    else hipLaunchKernelGGL(codes_gather_kernel, dim3(M), dim3(CIN / 4), 0, s, w.codebook, codes, feats, sc.err);
-  } else {
-    hipLaunchKernelGGL(feats_transpose_kernel<TAct>, dim3((L + 31) / 32, CIN / 32, B), dim3(256), 0, s, feats_in, L, feats);
-  }
-
   g_ws_floats = sc.ws_floats;
   g_tick = sc.tick;
+  // fp32 parity mode: a producer whose output feeds a bf16x3 GEMM writes it as split images (the
+  // GEMM's operand has no other reader)
+  auto spl = [&](GemmArgs& c) {
+    if constexpr (sizeof(TW) == 4) c.asplit = g3_split_in(c);
+    return c.asplit != 0;
+  };
   GemmArgs g{};
   g.ws = sc.ws;
   g.L = L;
@@ -1810,14 +1811,17 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
   g.A = feats; g.lda = CIN; g.cin = CIN; g.taps = 7;
   g.W = w.embed_w; g.wscale = w.embed_s; g.ldw = 7 * CIN; g.K = 7 * CIN; g.N = CD;
   g.C = x; g.ldc = CD; g.bias = w.embed_b;
+  spl(g);
+  if (codes) {
+    if constexpr (sizeof(TAct) == 2) hipLaunchKernelGGL(codes_gather_bf16_kernel, dim3(M), dim3(CIN / 4), 0, s, w.codebook, codes, feats, sc.err);
+    else if (g.asplit) hipLaunchKernelGGL(codes_gather_kernel<true>, dim3(M), dim3(CIN / 4), 0, s, w.codebook, codes, feats, sc.err);
+    else hipLaunchKernelGGL(codes_gather_kernel<>, dim3(M), dim3(CIN / 4), 0, s, w.codebook, codes, feats, sc.err);
+  } else {
+    g.asplit = 0;  // features handed in: transposed as plain rows
+    hipLaunchKernelGGL(feats_transpose_kernel<TAct>, dim3((L + 31) / 32, CIN / 32, B), dim3(256), 0, s, feats_in, L, feats);
+  }
   gemm_w<TW, TAct, A_CONV, E_BIAS>(g, s);
 
-  // fp32 parity mode: a GroupNorm output that feeds a bf16x3 GEMM goes to HBM as split images (the
-  // GroupNorm is that operand's only producer and the GEMM its only reader)
-  auto spl = [&](GemmArgs& c) {
-    if constexpr (sizeof(TW) == 4) c.asplit = g3_split_in(c);
-    return c.asplit != 0;
-  };
   auto resnet = [&](int i) {  // models.py:58-78
     GemmArgs c{};
     c.ws = sc.ws;

@@ -4,7 +4,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 export PYTHONPATH=.
-O=gpurun_out/r04g; mkdir -p $O
+O=gpurun_out/r04h; mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_gpu_codec_variants.py tests/test_gpu_large_dumps.py tests/test_gpu_parity.py -x -v -s --timeout 200 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; grep -E "split|LDS-DMA|passed|failed|Error" $O/tests.log | tail -12; [ $rc = 0 ] || exit $rc
 
