@@ -691,6 +691,10 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
     pcm_bufs = [pcm, torch.empty_like(pcm)]
     ev_ar = [torch.cuda.Event(), torch.cuda.Event()]
     ev_codec = [torch.cuda.Event(), torch.cuda.Event()]
+    # the PCM's copy to the host runs on its own stream (the DMA engine), so the next chunk's AR steps
+    # do not queue behind it; pcm_bufs[i] is rewritten only after its copy is done (ev_copy)
+    copy_stream = torch.cuda.Stream(device=dev)
+    ev_copy = [torch.cuda.Event(), torch.cuda.Event()]
     # per-chunk AR time (the decode steps alone), timing events on the decode stream around
     # ar_steps: read after the timed region for the whole-step roofline (no host sync inside it)
     ar_t = []
@@ -718,11 +722,15 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
             timing.append((e0, e1))
         with torch.cuda.stream(codec_stream):
             codec_stream.wait_event(ev_ar[i])
+            codec_stream.wait_event(ev_copy[i])
             eng.decode_codes(tok_bufs[i], 0, out=pcm_bufs[i])
             if dist is not None:
                 gather_pcm(pcm_bufs[i], dist, rank, world)  # PCM back to rank 0 (outbound exchange)
-            pcm_host.copy_(pcm_bufs[i], non_blocking=True)
             ev_codec[i].record(codec_stream)
+        with torch.cuda.stream(copy_stream):
+            copy_stream.wait_event(ev_codec[i])
+            pcm_host.copy_(pcm_bufs[i], non_blocking=True)
+            ev_copy[i].record(copy_stream)
 
     def reset_all():
         for s in range(S):
