@@ -691,9 +691,11 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
     pcm_bufs = [pcm, torch.empty_like(pcm)]
     ev_ar = [torch.cuda.Event(), torch.cuda.Event()]
     ev_codec = [torch.cuda.Event(), torch.cuda.Event()]
-    # the PCM's copy to the host runs on its own stream (the DMA engine), so the next chunk's AR steps
-    # do not queue behind it; pcm_bufs[i] is rewritten only after its copy is done (ev_copy)
-    copy_stream = torch.cuda.Stream(device=dev)
+    # the PCM's copy to the host stays on the codec stream: on a stream of its own (so the next chunk's
+    # AR would not queue behind it) it measured 192-193k vs 227-229k tok/s, the AR step 157-158 vs
+    # 131-132 us (round 4, alternating A/B on one box, profiles/r04/copy_stream_ab.txt): with a second
+    # stream in use every one of the step's 26 dependent dispatches took ~1 us longer
+    copy_stream = codec_stream
     ev_copy = [torch.cuda.Event(), torch.cuda.Event()]
     # per-chunk AR time (the decode steps alone), timing events on the decode stream around
     # ar_steps: read after the timed region for the whole-step roofline (no host sync inside it)
