@@ -78,8 +78,6 @@ _SIGS = {
     "lvx_stream_position": (_I, [_P, _I, ctypes.POINTER(_I), _P]),
     "lvx_set_graphs": (_I, [_P, _I]),
     "lvx_set_option": (_I, [_P, ctypes.c_char_p, _I]),
-    "lvx_stream_create": (_I, [_P, _I, _I, ctypes.POINTER(_P)]),
-    "lvx_device_cus": (_I, [_P, ctypes.POINTER(_I)]),
     "lvx_codec_decode_features": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "lvx_codec_decode_codes": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "lvx_enc_create": (_I, [_I, ctypes.c_longlong, ctypes.POINTER(_P)]),

@@ -340,7 +340,7 @@ void lvx_destroy(lvx_ctx* c) {
   for (auto g : c->graph_defs) (void)hipGraphDestroy(g);
   if (c->capture_stream) (void)hipStreamDestroy(c->capture_stream);
   for (void* p : c->allocs) (void)hipFree(p);
-  delete c;  // lvx_stream_create streams are not destroyed: they live until process exit
+  delete c;
 }
 
 int lvx_set_weight(lvx_ctx* c, const char* name, const float* data, int64_t numel) {
@@ -658,31 +658,6 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
 int lvx_set_graphs(lvx_ctx* c, int enable) {
   if (!c) return fail(LVX_E_ARG, "null ctx");
   c->use_graphs = enable != 0;
-  return LVX_OK;
-}
-
-int lvx_device_cus(lvx_ctx* c, int* cus_out) {
-  if (!c || !cus_out) return fail(LVX_E_ARG, "null argument");
-  hipDeviceProp_t prop;
-  HIP_TRY(hipGetDeviceProperties(&prop, c->cfg.device));
-  *cus_out = prop.multiProcessorCount;
-  return LVX_OK;
-}
-
-int lvx_stream_create(lvx_ctx* c, int cu_first, int cu_count, void** stream_out) {
-  if (!c || !stream_out) return fail(LVX_E_ARG, "null argument");
-  int n = 0;
-  if (int r = lvx_device_cus(c, &n)) return r;
-  if (cu_count == 0) cu_count = n - cu_first;
-  if (cu_first < 0 || cu_count < 1 || cu_first + cu_count > n)
-    return fail(LVX_E_ARG, "CU range [" + std::to_string(cu_first) + ", " + std::to_string(cu_first + cu_count) +
-                               ") outside [0, " + std::to_string(n) + ")");
-  std::vector<uint32_t> mask((n + 31) / 32, 0u);
-  for (int cu = cu_first; cu < cu_first + cu_count; ++cu) mask[cu / 32] |= 1u << (cu % 32);
-  HIP_TRY(hipSetDevice(c->cfg.device));
-  hipStream_t st;
-  HIP_TRY(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
-  *stream_out = st;
   return LVX_OK;
 }
 

@@ -125,17 +125,6 @@ class Engine:
     def set_option(self, name: str, value: int):
         _lib.check(self.lib.lvx_set_option(self.h, name.encode(), int(value)))
 
-    def device_cus(self) -> int:
-        n = ctypes.c_int()
-        _lib.check(self.lib.lvx_device_cus(self.h, ctypes.byref(n)))
-        return n.value
-
-    def cu_stream(self, cu_first: int, cu_count: int = 0):
-        """torch stream confined to CUs [cu_first, cu_first + cu_count) (owned by the engine)."""
-        p = ctypes.c_void_p()
-        _lib.check(self.lib.lvx_stream_create(self.h, int(cu_first), int(cu_count), ctypes.byref(p)))
-        return torch.cuda.ExternalStream(p.value, device=self.device)
-
     def set_graphs(self, enable: bool):
         _lib.check(self.lib.lvx_set_graphs(self.h, int(enable)))
 
