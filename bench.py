@@ -979,7 +979,12 @@ def main():
         rl = {"bound": "hbm", "kernel": dom["name"], "achieved": round(dom["gbs"], 1), "peak": HBM_PEAK_GBS,
               "unit": "GB/s", "frac": round(dom["gbs"] / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(key, dom["name"]),
               "bytes_per_launch": dom["bytes"], "avg_us": round(dom["avg_us"], 3), "kv_positions": ppos,
-              "pmc_key": key}
+              "pmc_key": key,
+              # rocprofv3 --pmc faults under HIP-graph replay (also without this library:
+              # tools/pmc_graph_repro.hip, profiles/r04/pmc_repro_*.log), so the counters come from
+              # the same command with the steps launched kernel by kernel (--null-stream): the same
+              # kernels and grids, per-dispatch bytes
+              "traffic_launch_path": "null stream (PMC pass; the timed run replays graphs)"}
         # PMC traffic / algorithmic bytes per probed kernel (a ratio well above 1 = operand re-fetch)
         rl["traffic_ratio"] = {v["name"]: (round(pmc_traffic(key, v["name"]) / v["bytes"], 3)
                                            if pmc_traffic(key, v["name"]) else None) for v in kern.values()}
