@@ -9,7 +9,8 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-SHAPES = ((32, 256), (1, 256), (2, 160), (1, 10), (3, 7))
+SHAPES = ((32, 256), (8, 256), (1, 256), (2, 160), (1, 10), (3, 7))  # 8 x 256: pwconv1 / qkv on the
+# bf16x3 kernel, pwconv2 / the convs / head not (mixed split-image producers in the fp32 mode)
 DEFAULT_G3F = 2  # the library's default of option codec_g3f (round 4: bf16x3 split products)
 
 
@@ -74,7 +75,7 @@ def test_fp32_bf16x3_split_gemm_matches_exact_fp32():
     e = build_engine(0, "fp32", "fp32", max_streams=32, max_positions=64, max_codec_frames=8192)
     try:
         g = torch.Generator().manual_seed(5)
-        for B, L in ((32, 256), (2, 1280)):
+        for B, L in ((32, 256), (8, 256), (2, 1280)):
             codes = torch.randint(0, 4096, (B, L), generator=g, dtype=torch.int32).to(e.device)
             e.set_option("codec_g3f", 1)
             a = e.decode_codes(codes, 0).clone()
