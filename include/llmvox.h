@@ -182,15 +182,6 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
 int lvx_set_option(lvx_ctx* ctx, const char* name, int value);
 /* Enable/disable HIP-graph replay of lvx_ar_step for a given B (default on). */
 int lvx_set_graphs(lvx_ctx* ctx, int enable);
-/* A HIP stream confined to compute units [cu_first, cu_first + cu_count) of the context's device
- * (hipExtStreamCreateWithCUMask). The latency-bound AR chain and the codec then run side by side
- * without sharing CUs: a codec kernel resident on a CU delays every dependent AR kernel that needs
- * it). The stream lives until the process exits (callers' allocators may still reference it when
- * the context is destroyed); create a few per process, not per request. cu_count = 0 -> all CUs
- * from cu_first. */
-int lvx_stream_create(lvx_ctx* ctx, int cu_first, int cu_count, void** stream_out);
-/* Number of compute units of the context's device (hipDeviceProp_t::multiProcessorCount). */
-int lvx_device_cus(lvx_ctx* ctx, int* cus_out);
 
 /* ---- codec decoder ------------------------------------------------------- */
 /* WavTokenizer.decode(features, bandwidth_id) (decoder/pretrained.py:192-207):
