@@ -31,7 +31,10 @@ OptScope::~OptScope() { t_opts = prev; }
 }  // namespace lvx
 
 static constexpr int kMaxCodecL = 4096;
-static constexpr int kGraphSteps = 16;  // decode steps per captured graph
+#ifndef LVX_GRAPH_STEPS
+#define LVX_GRAPH_STEPS 16  // A/B builds (tools/build_variant.sh NAME -DLVX_GRAPH_STEPS=n)
+#endif
+static constexpr int kGraphSteps = LVX_GRAPH_STEPS;  // decode steps per captured graph
 
 namespace {
 
