@@ -9,8 +9,9 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-SHAPES = ((32, 256), (8, 256), (1, 256), (2, 160), (1, 10), (3, 7))  # 8 x 256: pwconv1 / qkv on the
-# bf16x3 kernel, pwconv2 / the convs / head not (mixed split-image producers in the fp32 mode)
+SHAPES = ((32, 256), (8, 256), (7, 293), (1, 256), (2, 160), (1, 10), (3, 7))  # 8 x 256, 7 x 293: pwconv1 /
+# qkv on the bf16x3 kernel, pwconv2 / the convs / head not (mixed split-image producers in the fp32
+# mode; 2,051 frames: a partial last row tile)
 DEFAULT_G3F = 2  # the library's default of option codec_g3f (round 4: bf16x3 split products)
 
 
