@@ -679,13 +679,14 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
     tok_plan = torch.zeros(S, chunk, dtype=torch.int32, device=dev)
     pcm = torch.empty(S, 320 * chunk, dtype=torch.float32, device=dev)
     pcm_host = torch.empty(S, 320 * chunk, dtype=torch.float32, pin_memory=True)
-    # the codec of chunk c runs after the AR of chunk c on the same stream. A second stream
-    # (--codec-overlap) was measured slower: the latency-bound AR chain stalls while the codec's
-    # kernels are in flight (22.4 ms AR + 1.2 ms codec = 23.6 ms serial vs 25.5 ms overlapped per
-    # 256-token chunk; CU-partitioned or prioritised streams 28 ms, round 1; configs[2], round 4: the
-    # codec on 32 / 48 CUs and the AR on the rest 197.8k / 186.1k vs 227-228k tok/s serial, the AR step
-    # 131 -> 160-168 us without its CUs).
-    # tok_plan / pcm are double-buffered so the overlapped variant stays correct.
+    # codec_overlap (the default since round 4): the codec of chunk c runs on a second stream beside
+    # the AR of chunk c + 1, paced by the host so that neither queue ever waits on the other's event
+    # (the loop below). With the waits enqueued ahead (rounds 1-4 up to here: the codec queue blocked
+    # on the AR's event for a whole chunk) every AR dispatch took ~1 us longer and the overlap lost
+    # (195.6k vs 228.1k tok/s; CU-partitioned streams 186-198k); paced: configs[2] 234.8-235.5k vs
+    # 228.1-228.3k, configs[1] 13.40-13.44k vs 12.90-12.96k, configs[4] 79.4k vs 76.7-77.0k, the
+    # fp32 parity line 143.8k vs 142.6k (profiles/r04/codec_overlap_ab.txt). --serial-codec: the
+    # codec after the AR on one stream. tok_plan / pcm are double-buffered for the overlap.
     codec_stream = torch.cuda.Stream(device=dev) if codec_overlap else torch.cuda.current_stream(dev)
     tok_bufs = [tok_plan, torch.zeros_like(tok_plan)]
     pcm_bufs = [pcm, torch.empty_like(pcm)]
@@ -704,9 +705,16 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
     timing = None
 
     def run_chunk(c):
+        ar_part(c)
+        codec_part(c)
+
+    def ar_part(c):
         i = c & 1
         main = torch.cuda.current_stream(dev)
-        main.wait_event(ev_codec[i])  # tok_bufs[i] is free again (its decode has read it)
+        if codec_overlap:
+            ev_codec[i].synchronize()  # (host) tok_bufs[i] is free again: no cross-queue wait enqueued
+        else:
+            main.wait_event(ev_codec[i])  # tok_bufs[i] is free again (its decode has read it)
         col = (c % n_plan_chunks) * chunk  # chunk c of the back-to-back utterance plans (cycled)
         if reset_every and c % reset_every == 0:  # a new utterance: KV slots reset (a new sentence)
             for s_ in range(S):
@@ -722,8 +730,14 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record(main)
             timing.append((e0, e1))
+
+    def codec_part(c):
+        i = c & 1
+        if codec_overlap:
+            ev_ar[i].synchronize()  # (host) the chunk's tokens are there: the codec queue never blocks
         with torch.cuda.stream(codec_stream):
-            codec_stream.wait_event(ev_ar[i])
+            if not codec_overlap:
+                codec_stream.wait_event(ev_ar[i])
             codec_stream.wait_event(ev_copy[i])
             eng.decode_codes(tok_bufs[i], 0, out=pcm_bufs[i])
             if dist is not None:
@@ -763,11 +777,19 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
     run_chunks.windows = []
     if seconds > 0:  # steady state: whole utterances until `seconds` have passed, windows of window_s
         c, wc, wt = 0, 0, t0
+        if codec_overlap:
+            ar_part(0)
         while True:
-            run_chunk(c)
+            if codec_overlap:  # (the overlapped loop below: the AR of c + 1 queued unless c is the last)
+                last = time.perf_counter() - t0 >= seconds and (not reset_every or (c + 1) % reset_every == 0)
+                if not last:
+                    ar_part(c + 1)
+                codec_part(c)
+            else:
+                run_chunk(c)
             c += 1
             now = time.perf_counter()
-            done = now - t0 >= seconds and (not reset_every or c % reset_every == 0)  # whole utterances
+            done = last if codec_overlap else (now - t0 >= seconds and (not reset_every or c % reset_every == 0))  # whole utterances
             if now - wt >= window_s or done:
                 torch.cuda.synchronize()
                 now = time.perf_counter()
@@ -777,6 +799,16 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
                 if done:
                     break
         K = c
+    elif codec_overlap:
+        # the codec of chunk c on its own stream beside the AR of chunk c + 1, paced by the host: the
+        # AR of c + 1 is queued before the AR of c ends, and the codec of c only once that AR has ended,
+        # so neither queue ever holds a wait on the other's event (a queue blocked on another queue's
+        # signal slowed every dispatch of the AR chain by ~1 us: profiles/r04/codec_overlap_ab.txt)
+        ar_part(0)
+        for c in range(K):
+            if c + 1 < K:
+                ar_part(c + 1)
+            codec_part(c)
     else:
         for c in range(K):
             run_chunk(c)
@@ -833,7 +865,9 @@ def main():
     ap.add_argument("--probe-pos", type=int, default=0,
                     help="KV position of the roofline probe (default: the run's mean position, steps * chunk / 2)")
     ap.add_argument("--codec-overlap", action="store_true",
-                    help="run the codec on a second HIP stream beside the next chunk's AR (measured slower)")
+                    help="(default) the codec on a second HIP stream beside the next chunk's AR, host-paced")
+    ap.add_argument("--serial-codec", action="store_true",
+                    help="the codec after each chunk's AR on the same stream (no overlap)")
     ap.add_argument("--graph-stream", action="store_true", help="(default) kept for old command lines")
     ap.add_argument("--null-stream", action="store_true",
                     help="run on torch's default (null) stream: the decode steps are launched kernel by kernel")
@@ -856,6 +890,7 @@ def main():
     ap.add_argument("--rehearse", action="store_true",
                     help="CPU-only rehearsal of the multi-rank skeleton (gloo; tests/test_bench_launcher.py)")
     args = ap.parse_args()
+    args.codec_overlap = not args.serial_codec
     if args.streams == 0:
         args.streams = {1: 1, 2: 32, 3: 1, 4: 8}[args.config]
     if args.config == 4:
@@ -1060,7 +1095,9 @@ def main():
                                       if reset_every else f", one {K * chunk}-token utterance per stream"),
                        "streams_per_gpu": S, "chunk_tokens": chunk, "utterance_tokens": utt,
                        "kv_positions": f"0..{min(K * chunk, utt) - 1}",
-                       "parallelism": f"streams sharded over {world} GPU(s), RCCL scatter text / gather PCM"},
+                       "parallelism": f"streams sharded over {world} GPU(s), RCCL scatter text / gather PCM",
+                       "codec_schedule": ("chunk c's codec on a second stream beside chunk c + 1's AR (host-paced)"
+                                          if args.codec_overlap else "codec after each chunk's AR, one stream")},
             "dist": dist_info or {"backend": None, "world_size": 1},
             "audio_samples_per_s": round(320 * value, 1),
             "realtime_factor_per_stream": round(value / (world * S) / 75.0, 1),
