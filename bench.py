@@ -903,6 +903,11 @@ def main():
     if world_env is None and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
     world = int(world_env or 1)
+    # the paced codec overlap runs on one GPU; with N > 1 ranks the PCM gather (RCCL) would sit on the
+    # codec stream beside the AR, and the 2-rank gloo rehearsal on one card measured 69k vs 345k tok/s
+    # that way (profiles/r04/codec_overlap_ab.txt): N > 1 keeps the codec after the AR
+    if world > 1:
+        args.codec_overlap = False
     if world != args.gpus:
         sys.stderr.write(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a "
                          "different GPU count than requested\n")
