@@ -373,6 +373,8 @@ def run_config3(args, eng, world, rank, local, dist):
     from llmvox_amd.streaming import FusedScheduler
     dev = eng.device
     S, N, K, Wm = args.streams, args.utt_tokens, args.steps, args.warmup
+    # (round 4: FusedScheduler's codec overlap here: 12.61-12.68k vs 12.52-12.54k tok/s, but p50 first
+    # chunk 3.9-4.0 vs 1.33-1.36 ms, its dumps delivered a chunk later: profiles/r04/codec_overlap_ab.txt)
     sched = FusedScheduler(eng, max_chunk=256, to_bytes=True)
     rng = np.random.default_rng(1234)  # rank 0 draws every rank's request texts
     pcm_bytes = [0]
