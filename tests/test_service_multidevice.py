@@ -119,7 +119,9 @@ def test_full_device_passes_the_request_on():
     assert placed == [0, 1, 1]  # request 2's turn is device 0, which request 0 filled
     assert got == ref and all(len(r) > 0 for r in ref)
     from llmvox_amd.server import TTSService
-    svc = TTSService([StateEngine(max_streams=2), StateEngine(max_streams=2)], max_chunk=16, max_tokens=40)
+    # long requests (max_tokens 4,000: ~250 chunks), so that neither ends and frees its slots before
+    # the third submit (with 40 tokens they sometimes had: a flaky "DID NOT RAISE")
+    svc = TTSService([StateEngine(max_streams=2), StateEngine(max_streams=2)], max_chunk=16, max_tokens=4000)
     try:
         a, b = svc.submit(TEXTS[0]), svc.submit(TEXTS[1])
         assert {a.worker.index, b.worker.index} == {0, 1}
@@ -237,10 +239,13 @@ class _FailingLLM:
 
     def predict(self, request):
         def gen():
-            yield "Hello"
-            yield " world."
+            # the failing request fails before its first word: with words already fed, its decode
+            # could reach max_tokens and end the request normally before the producer thread raised
+            # (then the late error is ignored, the request being over), which made this test racy
             if request["prompt"] == self.fail_on:
                 raise MemoryError("LLM out of memory")
+            yield "Hello"
+            yield " world."
             yield " Fine."
             yield "<|eot_id|>"
         return gen()
@@ -258,7 +263,11 @@ def test_llm_failure_ends_only_its_request():
         body = b"".join(svc.chunks(good, timeout=0.01))
         assert len(body) > 0 and svc.error is None
         again = b"".join(svc.chunks(svc.submit("good"), timeout=0.01))  # the service keeps serving
-        assert again == body
+        # the same speech; where max_tokens cuts a request off depends on when the producer thread's
+        # words reached the scheduler's chunks (this stand-in engine never emits end-of-audio), so
+        # the two agree up to the shorter one
+        n = min(len(again), len(body))
+        assert n > 0 and again[:n] == body[:n]
     finally:
         svc.shutdown()
 
