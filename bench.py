@@ -287,10 +287,12 @@ def cpu_baseline(n_chunks, chunk, min_seconds=10.0, max_seconds=30.0, schedule=N
     starts = np.concatenate([[0], np.cumsum(schedule)]).astype(int).tolist()
     t0 = time.perf_counter()
     done, passes = 0, 0
+    rates = []  # tokens/s of each whole pass (utterance)
     with torch.inference_mode():
         while time.perf_counter() - t0 < min_seconds:
             hist, kv, prev = None, None, None
             passes += 1
+            tp, dp = time.perf_counter(), done
             for c in range(len(schedule)):
                 toks = []
                 for i in range(starts[c], starts[c + 1]):
@@ -307,6 +309,8 @@ def cpu_baseline(n_chunks, chunk, min_seconds=10.0, max_seconds=30.0, schedule=N
                 done += len(toks)
                 if time.perf_counter() - t0 > max_seconds:
                     break
+            else:
+                rates.append((done - dp) / (time.perf_counter() - tp))
             if time.perf_counter() - t0 > max_seconds:
                 break
     dt = time.perf_counter() - t0
@@ -320,13 +324,17 @@ def cpu_baseline(n_chunks, chunk, min_seconds=10.0, max_seconds=30.0, schedule=N
     except OSError:
         pass
     return {"value": done / dt, "unit": "speech tokens/s", "cores": threads, "kind": "port",
+            "passes": passes, "pass_min": round(min(rates), 1) if rates else None,
+            "pass_max": round(max(rates), 1) if rates else None,
             "sample": f"{done} tokens: fp32 AR steps + one codec decode per dump of {schedule[:8]} tokens, "
                       f"over {passes} utterance(s) of {sum(schedule)} positions, 1 stream, oracle/reference_cpu.py, "
                       f"{dt:.1f} s on {cpu}, torch threads {threads} ({why})"}
 
 
 class _HostCollectives:
-    """torch.distributed facade for the gloo rehearsal: device tensors go through host copies."""
+    """torch.distributed facade for the gloo rehearsal: device tensors go through host copies
+    (synchronously: no async_op)."""
+    supports_async = False
 
     def __init__(self, d):
         self.d = d
@@ -373,9 +381,11 @@ def run_config3(args, eng, world, rank, local, dist):
     from llmvox_amd.streaming import FusedScheduler
     dev = eng.device
     S, N, K, Wm = args.streams, args.utt_tokens, args.steps, args.warmup
-    # (round 4: FusedScheduler's codec overlap here: 12.61-12.68k vs 12.52-12.54k tok/s, but p50 first
-    # chunk 3.9-4.0 vs 1.33-1.36 ms, its dumps delivered a chunk later: profiles/r04/codec_overlap_ab.txt)
-    sched = FusedScheduler(eng, max_chunk=256, to_bytes=True)
+    # the service's schedule (round 5): chunk c + 1's decode queued before chunk c is
+    # read back, chunk c's codec on a second stream, each dump delivered when its codec call ends
+    # (round 4's overlap delivered a chunk late: p50 first chunk 3.9-4.0 vs 1.33-1.36 ms);
+    # --serial-codec: the serial scheduler
+    sched = FusedScheduler(eng, max_chunk=256, to_bytes=True, overlap=args.codec_overlap)
     rng = np.random.default_rng(1234)  # rank 0 draws every rank's request texts
     pcm_bytes = [0]
 
@@ -441,6 +451,7 @@ def run_config3(args, eng, world, rank, local, dist):
         dist.all_reduce(t_tok, op=dist.ReduceOp.SUM)
         dt, toks = float(t_dt.item()), int(t_tok.item())
     value = toks / dt
+    sched.close()
 
     kern, rl = None, None
     if not args.no_probe:
@@ -469,6 +480,9 @@ def run_config3(args, eng, world, rank, local, dist):
             "config": {"workload": f"configs[3]: FusedScheduler service path, {S} replica stream(s)/GPU "
                                    f"(initial dump 10/160, x3 to 1280), {N} tokens per utterance, "
                                    "one codec call per dump, f32le bytes on the host",
+                       "codec_schedule": ("FusedScheduler overlap: chunk c + 1's decode queued before chunk c is "
+                                          "read back, chunk c's codec on a second stream, each dump delivered when "
+                                          "its codec ends" if args.codec_overlap else "serial FusedScheduler"),
                        "streams_per_gpu": S, "utterance_tokens": N, "dump_schedule_replica0": dump_schedule(N, 10),
                        "dump_schedule_replica1": dump_schedule(N, 160),
                        "parallelism": f"streams sharded over {world} GPU(s); rank 0 scatters the request texts and "
@@ -524,12 +538,17 @@ def spawn_ranks(n):
 
 def rehearse(args, world, rank):
     """--rehearse: the multi-rank skeleton of the bench on the CPU (gloo, no GPU): plan scatter from
-    rank 0, a stand-in per-rank 'decode', PCM gather to rank 0, barriers and the max-over-ranks
-    clock. Used by tests/test_bench_launcher.py for the launcher path."""
+    rank 0, the PCM gather to rank 0, barriers and the max-over-ranks clock. Used by
+    tests/test_bench_launcher.py for the launcher path. The gather runs both ways the bench runs it:
+    once per chunk after a stand-in 'decode' (the serial schedule), and paced as in the overlapped
+    schedule (run_chunks at N > 1: ChunkGather.issue once the chunk's 'codec' is done, asynchronously,
+    two PCM buffers, ChunkGather.wait before a buffer is written again); rank 0 checks that both give
+    every rank's chunks exactly as a single rank would compute them."""
     import torch.distributed as dist
-    from llmvox_amd.parallel import gather_pcm, scatter_plans
+    from llmvox_amd.parallel import ChunkGather, gather_pcm, scatter_plans
     dist.init_process_group("gloo")
     S, n_pos = args.streams, args.chunk
+    K = 5
     plans = None
     if rank == 0:
         rng = np.random.default_rng(1234)
@@ -538,45 +557,75 @@ def rehearse(args, world, rank):
     dist.barrier()
     t0 = time.perf_counter()
     mine = scatter_plans(plans, S, n_pos, "cpu", dist, rank)
-    got = gather_pcm(mine.float(), dist, rank, world)
+
+    def decode(c):  # stand-in codec output of chunk c: a function of this rank's plans and c
+        return (mine.float() * (c + 1) + c).repeat_interleave(4, dim=1)
+
+    serial = [gather_pcm(decode(c), dist, rank, world) for c in range(K)]
+    gather = ChunkGather(dist, rank, world, keep=True)
+    bufs = [None, None]
+    for c in range(K):  # the overlapped schedule's order: issue c - 1 after c's 'codec' was queued
+        i = c & 1
+        gather.wait(i)           # the buffer's previous gather has read it
+        bufs[i] = decode(c)      # chunk c's 'codec' into buffer i
+        if c >= 1:
+            gather.issue((c - 1) & 1, bufs[(c - 1) & 1])
+    gather.issue((K - 1) & 1, bufs[(K - 1) & 1])
+    gather.drain()
     dist.barrier()
     dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     if rank == 0:
-        ok = torch.equal(torch.cat(got).to(torch.int32), plans)
+        full = plans.float()
+        expect = [(full * (c + 1) + c).repeat_interleave(4, dim=1) for c in range(K)]
+        ok = all(torch.equal(torch.cat(serial[c]), expect[c]) for c in range(K))
+        ok_paced = len(gather.gathered) == K and all(torch.equal(torch.cat(gather.gathered[c]), expect[c])
+                                                     for c in range(K))
         print(json.dumps({"rehearsal": True, "dist": {"backend": dist.get_backend(), "world_size": dist.get_world_size()},
                           "n_gpus": world, "streams_per_rank": S, "gathered_equals_scattered": bool(ok),
+                          "paced_gather_equals_single_rank": bool(ok_paced), "chunks": K,
                           "max_over_ranks_s": float(dt.item())}), flush=True)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def first_chunk_latency(eng, reps=12):
+def first_chunk_latency(eng, reps=12, overlap=True):
     """p50 first-chunk latency: one fresh stream through the service scheduler
     (FusedScheduler: tokenisation, text-id plan upload, 10 fused decode steps, the codec call, PCM
     to the host as f32le bytes), timed from the moment the sentence's words are enqueued to the
     first 3,200-sample dump on the host; first two runs (graph capture, warm-up) dropped."""
     from llmvox_amd.streaming import FusedScheduler
-    sched = FusedScheduler(eng, max_chunk=256, max_rows=1)
+    sched = FusedScheduler(eng, max_chunk=256, max_rows=1, overlap=overlap)
     lat = []
+
+    class FirstBytes:  # the stream's sink: the moment its first PCM bytes are delivered (with the
+        t = None       # overlap, by the delivery thread while the scheduler waits for the next chunk)
+
+        def put(self, item):
+            if self.t is None and isinstance(item, bytes):
+                self.t = time.perf_counter()
+
     for r in range(reps):
         torch.cuda.synchronize()
+        fb = FirstBytes()
         t0 = time.perf_counter()
-        st = sched.open_stream(index=0, dump_size=10)
+        st = sched.open_stream(index=0, dump_size=10, sink=fb)
         for w in SENTENCE.split(" "):
             st.feed(w)
-        while not any(isinstance(e, bytes) for e in st.events):
+        while fb.t is None:
             if sched.run_chunk() == 0:
                 raise RuntimeError("scheduler idle before the first dump")
-        t1 = time.perf_counter()
+        t1 = fb.t
         assert len(st.events[0]) == 3200 * 4
         sched.close_stream(st)
+        sched.flush()
         if r >= 2:
             lat.append((t1 - t0) * 1e3)
+    sched.close()
     return statistics.median(lat)
 
 
-def first_chunk_latency_loaded(eng, busy=31, reps=12, max_chunk=64, seed=99):
+def first_chunk_latency_loaded(eng, busy=31, reps=12, max_chunk=64, seed=99, overlap=True):
     """p50 first-chunk latency UNDER LOAD (reference: a replica's first chunk is
     produced while the other replica decodes, streaming_server.py:357-376): a fresh stream joins a
     FusedScheduler that is already decoding `busy` streams (continuous batching, chunks of up to
@@ -589,7 +638,7 @@ def first_chunk_latency_loaded(eng, busy=31, reps=12, max_chunk=64, seed=99):
     import queue
     import threading
     from llmvox_amd.streaming import FusedScheduler
-    sched = FusedScheduler(eng, max_chunk=max_chunk, to_bytes=True)
+    sched = FusedScheduler(eng, max_chunk=max_chunk, to_bytes=True, overlap=overlap)
     rng = np.random.default_rng(seed)
     words = lambda n: " ".join(random_sentence(rng) for _ in range(n)).split(" ")
     for i in range(busy):  # replica streams as the service opens them (dump 10 / 160, x3 to 1280)
@@ -656,14 +705,16 @@ def first_chunk_latency_loaded(eng, busy=31, reps=12, max_chunk=64, seed=99):
         th.join(timeout=60)
     if errors:
         raise errors[0]
+    sched.flush()
     torch.cuda.synchronize()
     for st in list(sched.streams):
         sched.close_stream(st)
+    sched.close()
     return statistics.median(lat), max(lat)
 
 
 def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, world=1, codec_overlap=False,
-               seconds=0.0, window_s=10.0):
+               seconds=0.0, window_s=10.0, record=None):
     """W untimed then K timed bench steps (one step = `chunk` fused decode steps for the S streams,
     the batched codec decode of their codes, the PCM to the host; the PCM gathered to rank 0 when
     distributed). With reset_every R, step c is chunk c % R of utterance c // R: the streams' KV
@@ -671,8 +722,10 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
     back ([S][n_utterances * R * chunk]). Returns (seconds, last token buffer, codec stream, token
     buffers, PCM buffers). seconds > 0 (steady-state mode): chunks run until that much wall time has
     passed instead of K (the plans are cycled), with a device sync every window_s seconds to record
-    the rate of each window (run_chunks.windows, run_chunks.k_done)."""
-    from llmvox_amd.parallel import gather_pcm
+    the rate of each window (run_chunks.windows, run_chunks.k_done). record (a list, tests only): every
+    chunk's tokens and PCM, copied on the codec stream before its buffers are reused
+    (tests/test_gpu_bench_schedule.py holds the overlapped schedule to the serial one with it)."""
+    from llmvox_amd.parallel import ChunkGather, gather_pcm
     n_plan_chunks = mine.shape[1] // chunk
     dev = eng.device
     slots = torch.arange(S, dtype=torch.int32, device=dev)
@@ -700,6 +753,20 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
     # stream in use every one of the step's 26 dependent dispatches took ~1 us longer
     copy_stream = codec_stream
     ev_copy = [torch.cuda.Event(), torch.cuda.Event()]
+    # N > 1 with the overlap: chunk c's PCM gather to rank 0 is issued only once
+    # the host has seen chunk c's codec event, on a communicator stream of its own, asynchronously,
+    # and waited for (host poll) before the PCM buffer is written again: neither the decode nor the
+    # codec queue ever holds the collective (round 4 put it on the codec stream, and N > 1 fell back
+    # to the serial schedule)
+    gather = (ChunkGather(dist, rank, world, torch.cuda.Stream(device=dev))
+              if (dist is not None and codec_overlap) else None)
+    gpending = [False, False]
+
+    def gather_done(i):  # (host) the chunk in buffer i has finished its codec: send its PCM
+        if gather is not None and gpending[i]:
+            ev_codec[i].synchronize()
+            gather.issue(i, pcm_bufs[i])
+            gpending[i] = False
     # per-chunk AR time (the decode steps alone), timing events on the decode stream around
     # ar_steps: read after the timed region for the whole-step roofline (no host sync inside it)
     ar_t = []
@@ -732,18 +799,24 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record(main)
             timing.append((e0, e1))
+        gather_done(i)  # chunk c - 2's PCM (its codec has ended: synchronised above)
 
     def codec_part(c):
         i = c & 1
         if codec_overlap:
             ev_ar[i].synchronize()  # (host) the chunk's tokens are there: the codec queue never blocks
+        if gather is not None:
+            gather.wait(i)  # chunk c - 2's gather has read pcm_bufs[i]
         with torch.cuda.stream(codec_stream):
             if not codec_overlap:
                 codec_stream.wait_event(ev_ar[i])
             codec_stream.wait_event(ev_copy[i])
             eng.decode_codes(tok_bufs[i], 0, out=pcm_bufs[i])
-            if dist is not None:
+            if dist is not None and gather is None:
                 gather_pcm(pcm_bufs[i], dist, rank, world)  # PCM back to rank 0 (outbound exchange)
+            gpending[i] = gather is not None
+            if record is not None and timing is not None:  # (timed chunks only)
+                record.append((tok_bufs[i].clone(), pcm_bufs[i].clone()))
             ev_codec[i].record(codec_stream)
         with torch.cuda.stream(copy_stream):
             copy_stream.wait_event(ev_codec[i])
@@ -765,6 +838,10 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
     reset_all()
     for c in range(Wm):
         run_chunk(c)
+    if gather is not None:
+        for i in range(2):
+            gather_done(i)
+        gather.drain()
     torch.cuda.synchronize()
     eng.check_errors()
     reset_all()
@@ -814,6 +891,11 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
     else:
         for c in range(K):
             run_chunk(c)
+    if gather is not None:  # the last chunks' gathers (inside the timed region)
+        for c in range(K - 2, K):
+            if c >= 0:
+                gather_done(c & 1)
+        gather.drain()
     run_chunks.k_done = K
     torch.cuda.synchronize()
     if dist is not None:
@@ -841,6 +923,10 @@ def parity_mode_line(S, chunk, K=4, Wm=1, codec_overlap=False):
         dt, _, _, _, _ = run_chunks(eng, mine, S, chunk, K, Wm, codec_overlap=codec_overlap)
         return {"value": round(S * K * chunk / dt, 1), "unit": "speech tokens/s", "ms_per_step": round(dt / K * 1e3, 3),
                 "steps": K, "warmup": Wm, "dtype": "fp32", "kv_dtype": "fp32", "codec_weights": "fp32",
+                "ar_gemm": "exact fp32 products (v_mfma_f32_16x16x4_f32), fp32 accumulate: ids bit-exact",
+                "codec_gemm": ("bf16x3 split products (hi.hi + lo.hi + hi.lo on v_mfma_f32_16x16x32_bf16, "
+                               "fp32 accumulate) in the >= 192-tile GEMMs, exact fp32 elsewhere; PCM within "
+                               "2e-4 / RMS 1e-5 of the reference (tests/test_gpu_parity.py)"),
                 "streams": S, "kv_positions": f"0..{K * chunk - 1}",
                 "ar_ms_per_chunk": round(sum(run_chunks.ar_ms) / K, 3)}
     finally:
@@ -905,11 +991,6 @@ def main():
     if world_env is None and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
     world = int(world_env or 1)
-    # the paced codec overlap runs on one GPU; with N > 1 ranks the PCM gather (RCCL) would sit on the
-    # codec stream beside the AR, and the 2-rank gloo rehearsal on one card measured 69k vs 345k tok/s
-    # that way (profiles/r04/codec_overlap_ab.txt): N > 1 keeps the codec after the AR
-    if world > 1:
-        args.codec_overlap = False
     if world != args.gpus:
         sys.stderr.write(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a "
                          "different GPU count than requested\n")
@@ -996,11 +1077,11 @@ def main():
     value = total_tokens / dt
     toks_rank0 = last_tok[0].cpu().numpy()
 
-    p50 = first_chunk_latency(eng)
+    p50 = first_chunk_latency(eng, overlap=args.codec_overlap)
     p50_loaded = None
     if args.config in (1, 2, 4) and not args.no_loaded_latency:
         eng.check_errors()
-        p50_loaded = first_chunk_latency_loaded(eng, busy=min(31, eng.max_streams - 1))
+        p50_loaded = first_chunk_latency_loaded(eng, busy=min(31, eng.max_streams - 1), overlap=args.codec_overlap)
 
     # ---- roofline: dominant kernel class at the run's mean KV position, timed live with HIP
     # events on the compute stream; traffic from a PMC pass over the same probe workload

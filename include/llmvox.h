@@ -115,7 +115,7 @@ int lvx_ar_steps(lvx_ctx* ctx, int n_steps, int B, const int32_t* slots_dev, con
                  void* stream);
 /* Copy the logits [B][4096] of the last lvx_ar_step(s) call (diagnostics / tests). */
 int lvx_ar_logits(lvx_ctx* ctx, int B, float* dst_dev, void* stream);
-/* Synchronises the stream and reports (then clears) device-side errors: an embedding id or codec
+/* Synchronises the stream and reports (then clears) device-side errors of both error words: an embedding id or codec
  * code out of range (LVX_E_INDEX), the ISTFT window envelope <= 1e-11 (LVX_E_STATE; reference:
  * the assertion of decoder/spectral_ops.py:72 -- the fixed periodic Hann envelope is >= 0.72 on the
  * trimmed span, so this is a self-check), a slot past max_positions (LVX_E_CAPACITY; reference:
@@ -123,6 +123,21 @@ int lvx_ar_logits(lvx_ctx* ctx, int B, float* dst_dev, void* stream);
  * (LVX_E_CAPACITY), or a non-finite / out-of-range (|v| >= 2^25) partial in the B <= 2 fused MLP's
  * fixed-point accumulation (LVX_E_STATE; the reference would carry the value into its logits). */
 int lvx_check_errors(lvx_ctx* ctx, void* stream);
+/* The device error bits live in two words: the AR word (decode steps, lvx_text_embed,
+ * lvx_codes_to_features) and the codec word (lvx_codec_decode_*), so a codec running on a second stream
+ * beside the decode keeps its flags apart. lvx_check_errors takes both; every condition that is set is
+ * named in lvx_last_error (the code is the most specific one: LVX_E_INDEX > LVX_E_STATE >
+ * LVX_E_CAPACITY). A take reads and clears the words atomically, in stream order: bits set later by
+ * work in flight on another stream stay for the next take. */
+#define LVX_ERRW_AR 1
+#define LVX_ERRW_CODEC 2
+/* Asynchronous take (no synchronisation): the bits of the chosen words (`which` = LVX_ERRW_AR and/or
+ * LVX_ERRW_CODEC) into bits_dev[0] (device int32: AR bits | codec bits << 16), enqueued on `stream`
+ * after the work already there; pass them to lvx_error_status once they are on the host. Lets a
+ * scheduler read a chunk's errors with its tokens, without a stream synchronisation. */
+int lvx_error_take(lvx_ctx* ctx, int which, int32_t* bits_dev, void* stream);
+/* The status (and lvx_last_error message) of taken bits, as lvx_check_errors would return it; 0 if none. */
+int lvx_error_status(int bits);
 /* Set a slot's position and previous token (rewind after a speculative run-ahead, or jump). */
 int lvx_stream_set(lvx_ctx* ctx, int slot, int pos, int prev_token, void* stream);
 /* Measurement hook (bench.py): launch one kernel class of the decode step `iters` times for the

@@ -42,8 +42,19 @@ class LvxError(RuntimeError):
         self.code = code
 
 
-class LvxCapacityError(LvxError, AssertionError):
+class LvxStreamError(LvxError):
+    """A device error that concerns particular streams; the scheduler names them in ``streams``
+    (the service then ends only their requests)."""
+    streams = ()
+
+
+class LvxCapacityError(LvxStreamError, AssertionError):
     """Capacity overflow: the reference raises AssertionError here (src/model.py:205)."""
+
+
+class LvxNumericError(LvxStreamError):
+    """A non-finite / out-of-range partial in the B <= 2 fused MLP (error bit 32): the logits of the
+    rows of that step are invalid."""
 
 
 class LvxArgError(LvxError, ValueError):
@@ -71,6 +82,8 @@ _SIGS = {
     "lvx_ar_step": (_I, [_P, _I, _P, _P, _I, _P, _P, _P, _P]),
     "lvx_ar_steps": (_I, [_P, _I, _I, _P, _P, _I, _P, _P, _P, _P]),
     "lvx_check_errors": (_I, [_P, _P]),
+    "lvx_error_take": (_I, [_P, _I, _P, _P]),
+    "lvx_error_status": (_I, [_I]),
     "lvx_ar_logits": (_I, [_P, _I, _P, _P]),
     "lvx_probe_kernel": (_I, [_P, _I, _I, _P, _I, _P]),
     "lvx_stream_set": (_I, [_P, _I, _I, _I, _P]),
@@ -111,14 +124,34 @@ def load():
     return lib
 
 
-def check(code: int):
-    if code == LVX_OK:
-        return
+ERRW_AR = 1     # LVX_ERRW_AR: the decode / drop-in gather error word
+ERRW_CODEC = 2  # LVX_ERRW_CODEC: the codec's error word
+BIT_NUMERIC = 32  # AR word: the fused MLP's fixed-point range check
+
+
+def error_for(code: int, bits: int = 0):
+    """The exception for a non-zero status (``bits``: the taken device error bits, if known)."""
     msg = _lib.lvx_last_error().decode(errors="replace") if _lib else "unknown"
     if code == LVX_E_CAPACITY:
-        raise LvxCapacityError(code, msg)
-    if code == LVX_E_INDEX:
-        raise LvxIndexError(code, msg)
-    if code in (LVX_E_ARG, LVX_E_NAME):
-        raise LvxArgError(code, msg)
-    raise LvxError(code, msg)
+        e = LvxCapacityError(code, msg)
+    elif code == LVX_E_INDEX:
+        e = LvxIndexError(code, msg)
+    elif code in (LVX_E_ARG, LVX_E_NAME):
+        e = LvxArgError(code, msg)
+    elif code == LVX_E_STATE and bits & BIT_NUMERIC:
+        e = LvxNumericError(code, msg)
+    else:
+        e = LvxError(code, msg)
+    e.bits = bits
+    return e
+
+
+def check(code: int):
+    if code != LVX_OK:
+        raise error_for(code)
+
+
+def check_bits(bits: int):
+    """Raise for device error bits taken with lvx_error_take (every set condition in the message)."""
+    if bits:
+        raise error_for(load().lvx_error_status(int(bits)), int(bits))

@@ -3039,6 +3039,19 @@ void launch_set_slot(int32_t* pos, int32_t* prev, int slot, int p, int tok, hipS
   hipLaunchKernelGGL(set_slot_kernel, dim3(1), dim3(1), 0, s, pos, prev, slot, p, tok);
 }
 
+// Take (read and clear, one atomic per word) the masked bits of the AR word words[0] and the codec
+// word words[1]: bits set meanwhile by kernels of another stream stay in their word for the next take.
+// out = AR bits | codec bits << 16.
+__global__ void err_take_kernel(int32_t* words, int32_t mask_ar, int32_t mask_codec, int32_t* out) {
+  const int32_t a = mask_ar ? (atomicAnd(words, ~mask_ar) & mask_ar) : 0;
+  const int32_t c = mask_codec ? (atomicAnd(words + 1, ~mask_codec) & mask_codec) : 0;
+  out[0] = a | (c << 16);
+}
+
+void launch_err_take(int32_t* words, int mask_ar, int mask_codec, int32_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(err_take_kernel, dim3(1), dim3(1), 0, s, words, mask_ar, mask_codec, out);
+}
+
 void launch_text_embed(const float* table, const int64_t* ids, int n, float* out, int32_t* err, hipStream_t s) {
   if (n > 0) hipLaunchKernelGGL(text_embed_kernel, dim3(n), dim3(TEXT_DIM), 0, s, table, ids, n, out, err);
 }

@@ -45,6 +45,32 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+// Status of taken error bits (AR word | codec word << 16, as err_take_kernel reports them): the message
+// names EVERY set condition; the code is the most specific one (index > state > capacity).
+int bits_status(int32_t bits) {
+  if (!bits) return LVX_OK;
+  const int32_t ar = bits & 0xffff, cd = (bits >> 16) & 0xffff;
+  std::string m;
+  int code = 0;
+  auto add = [&](int c, const char* what) {
+    if (!m.empty()) m += "; ";
+    m += what;
+    if (code == 0 || (c == LVX_E_INDEX) || (c == LVX_E_STATE && code == LVX_E_CAPACITY)) code = c;
+  };
+  if (ar & 4) add(LVX_E_INDEX, "index out of range in self (a text id outside [0, 386) given to lvx_text_embed or a code "
+                               "outside [0, 4096) given to lvx_codes_to_features)");
+  if (cd & 4) add(LVX_E_INDEX, "index out of range in self (codec: a code outside [0, 4096) given to lvx_codec_decode_codes)");
+  if (ar & 32) add(LVX_E_STATE, "a non-finite or out-of-range (|v| >= 2^25) partial in the fused MLP's fixed-point "
+                                "accumulation (B <= 2): the logits of that step's rows are invalid");
+  if (cd & 8) add(LVX_E_STATE, "ISTFT window envelope <= 1e-11 (spectral_ops.py:72 assertion)");
+  if (ar & 1) add(LVX_E_CAPACITY, "a stream exceeded its KV capacity (max_positions)");
+  if (ar & 2) add(LVX_E_CAPACITY, "a batch row ran past the end of its text plan (plan_stride)");
+  if (!code) add(LVX_E_STATE, "unknown device error bits");
+  char hex[32];
+  snprintf(hex, sizeof hex, " [error bits 0x%x]", (unsigned)bits);
+  return fail(code, m + hex);
+}
+
 #define HIP_TRY(expr)                                                                      \
   do {                                                                                     \
     hipError_t _e = (expr);                                                                \
@@ -570,7 +596,7 @@ int lvx_finalize(lvx_ctx* c) {
       (r = c->dalloc(&cs.frames, (size_t)M * 1280)) || (r = c->dalloc(&cs.tick, 4096)))
     return r;
   HIP_TRY(hipMemset(cs.tick, 0, 4096 * 4));
-  cs.err = st.err;
+  cs.err = st.err + 1;  // the codec's own word (it may run on a second stream beside the AR)
   HIP_TRY(hipDeviceSynchronize());
   c->host.clear();
   c->finalized = true;
@@ -625,15 +651,12 @@ int lvx_stream_position(lvx_ctx* c, int slot, int* pos_out, void* stream) {
   if (slot < 0 || slot >= c->cfg.max_streams || !pos_out) return fail(LVX_E_ARG, "bad slot/pos_out");
   HIP_TRY(hipSetDevice(c->cfg.device));
   int32_t v[2];
+  launch_err_take(c->st.err, 1, 0, c->st.err + 3, (hipStream_t)stream);  // the capacity bit only
   HIP_TRY(hipMemcpyAsync(&v[0], c->st.pos + slot, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
-  HIP_TRY(hipMemcpyAsync(&v[1], c->st.err, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIP_TRY(hipMemcpyAsync(&v[1], c->st.err + 3, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   *pos_out = v[0];
-  if (v[1] & 1) {
-    (void)hipMemsetAsync(c->st.err, 0, 4, (hipStream_t)stream);
-    return fail(LVX_E_CAPACITY, "a stream exceeded its KV capacity (max_positions)");
-  }
-  return LVX_OK;
+  return bits_status(v[1]);
 }
 
 int lvx_set_option(lvx_ctx* c, const char* name, int value) {
@@ -794,21 +817,26 @@ int lvx_check_errors(lvx_ctx* c, void* stream) {
   NEED_FINAL(c);
   HIP_TRY(hipSetDevice(c->cfg.device));
   int32_t v = 0;
-  HIP_TRY(hipMemcpyAsync(&v, c->st.err, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  // both words taken atomically in stream order: a bit that a codec call in flight on another stream
+  // sets afterwards stays in its word for the next check (round 4 cleared the word with a memset)
+  launch_err_take(c->st.err, -1, -1, c->st.err + 2, (hipStream_t)stream);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(&v, c->st.err + 2, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-  if (v) {
-    (void)hipMemsetAsync(c->st.err, 0, 4, (hipStream_t)stream);
-    if (v & 32)
-      return fail(LVX_E_STATE, "a non-finite or out-of-range (|v| >= 2^25) partial in the fused MLP's fixed-point "
-                               "accumulation (B <= 2): its logits are invalid");
-    if (v & 4) return fail(LVX_E_INDEX, "index out of range in self (a text id outside [0, 386) or a code "
-                                         "outside [0, 4096) given to lvx_text_embed / lvx_codes_to_features / lvx_codec_decode_codes)");
-    if (v & 8) return fail(LVX_E_STATE, "ISTFT window envelope <= 1e-11 (spectral_ops.py:72 assertion)");
-    if (v & 1) return fail(LVX_E_CAPACITY, "a stream exceeded its KV capacity (max_positions)");
-    return fail(LVX_E_CAPACITY, "a batch row ran past the end of its text plan (plan_stride)");
-  }
+  return bits_status(v);
+}
+
+int lvx_error_take(lvx_ctx* c, int which, int32_t* bits_dev, void* stream) {
+  NEED_FINAL(c);
+  if (!bits_dev || which < 1 || which > 3) return fail(LVX_E_ARG, "which must be LVX_ERRW_AR | LVX_ERRW_CODEC, bits_dev non-null");
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  launch_err_take(c->st.err, (which & LVX_ERRW_AR) ? -1 : 0, (which & LVX_ERRW_CODEC) ? -1 : 0, bits_dev,
+                  (hipStream_t)stream);
+  HIP_TRY(hipGetLastError());
   return LVX_OK;
 }
+
+int lvx_error_status(int bits) { return bits_status(bits); }
 
 int lvx_probe_kernel(lvx_ctx* c, int which, int B, const int32_t* slots, int iters, void* stream) {
   NEED_FINAL(c);

@@ -92,7 +92,10 @@ struct ArState {
   uint32_t* selrow = nullptr;    // [B] batched deferred select: row b's logits not yet committed
   int32_t* pos = nullptr;       // [max_streams] per-slot next position
   int32_t* prev = nullptr;      // [max_streams] per-slot previous token
-  int32_t* err = nullptr;       // [1] capacity overflow flag
+  int32_t* err = nullptr;       // [4] error words: [0] AR (1 KV capacity, 2 plan overrun, 4 text id / code out
+                                // of range in the drop-in gathers, 32 fused-MLP fixed-point range); [1] codec
+                                // (4 code out of range, 8 ISTFT envelope); [2] / [3] take slots of
+                                // lvx_check_errors / lvx_stream_position
   float* x = nullptr;           // [B][768] residual stream
   float* q = nullptr;           // [B][768]
   float* part_o = nullptr;      // [B][8][NSPLIT][96]
@@ -127,6 +130,7 @@ void ar_launch_rowinfo_init(const ArState& st, int B, hipStream_t s);
 void ar_launch_steps_end(const ArState& st, int wdtype, int B, hipStream_t s);  // deferred select: commit the last step
 int ar_select_probe(const ArWeights& w, const ArState& st, int B, int path, hipStream_t s);  // test hook
 void launch_set_slot(int32_t* pos, int32_t* prev, int slot, int p, int tok, hipStream_t s);
+void launch_err_take(int32_t* words, int mask_ar, int mask_codec, int32_t* out, hipStream_t s);
 void launch_text_embed(const float* table, const int64_t* ids, int n, float* out, int32_t* err, hipStream_t s);
 void launch_codes_to_features(const float* codebook, const int64_t* codes, int B, int L, float* feats,
                               int32_t* err, hipStream_t s);
@@ -180,7 +184,7 @@ struct CodecScratch {
   float* stats = nullptr;  // [B][32][2]
   float* spec = nullptr;   // [M][1282]
   float* frames = nullptr; // [M][1280]
-  int32_t* err = nullptr;  // = ArState.err: bit 4 a code outside [0, 4096), bit 8 the ISTFT envelope <= 1e-11
+  int32_t* err = nullptr;  // = ArState.err + 1, the codec's own word: bit 4 a code outside [0, 4096), bit 8 the ISTFT envelope <= 1e-11
   int max_frames = 0;
 };
 

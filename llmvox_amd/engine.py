@@ -120,7 +120,17 @@ class Engine:
         return out
 
     def check_errors(self):
-        _lib.check(self.lib.lvx_check_errors(self.h, self.stream_handle()))
+        """Synchronise the current stream and raise for the device error bits of both words (AR and
+        codec); every set condition is named in the message."""
+        code = self.lib.lvx_check_errors(self.h, self.stream_handle())
+        if code:
+            raise _lib.error_for(code)
+
+    def take_errors(self, which: int, out: torch.Tensor):
+        """Enqueue (no synchronisation) the atomic take of the AR (``_lib.ERRW_AR``) and / or codec
+        (``_lib.ERRW_CODEC``) error bits into the device int32 ``out[0]``; ``_lib.check_bits`` on the
+        host copy raises for them."""
+        _lib.check(self.lib.lvx_error_take(self.h, int(which), _ptr(out), self.stream_handle()))
 
     def set_option(self, name: str, value: int):
         _lib.check(self.lib.lvx_set_option(self.h, name.encode(), int(value)))

@@ -7,6 +7,7 @@ over torch.distributed (RCCL over xGMI on MI355X; gloo in the CPU tests).
 """
 from __future__ import annotations
 
+import time
 from typing import List, Optional
 
 import torch
@@ -27,13 +28,59 @@ def scatter_plans(full: Optional[torch.Tensor], streams_per_rank: int, n_pos: in
     return mine
 
 
-def gather_pcm(pcm: torch.Tensor, dist=None, rank: int = 0, world: int = 1) -> Optional[List[torch.Tensor]]:
-    """Every rank's [S, samples] float32 PCM to rank 0 (None elsewhere)."""
+def gather_pcm(pcm: torch.Tensor, dist=None, rank: int = 0, world: int = 1, async_op: bool = False):
+    """Every rank's [S, samples] float32 PCM to rank 0 (None elsewhere). async_op: returns (outputs,
+    work) with the collective in flight (work None when the backend ran it synchronously)."""
     if dist is None:
-        return [pcm]
+        return ([pcm], None) if async_op else [pcm]
     out = [torch.empty_like(pcm) for _ in range(world)] if rank == 0 else None
-    dist.gather(pcm, out, dst=0)
-    return out
+    if not async_op:
+        dist.gather(pcm, out, dst=0)
+        return out
+    work = dist.gather(pcm, out, dst=0, async_op=True) if getattr(dist, "supports_async", True) else \
+        dist.gather(pcm, out, dst=0)
+    return out, work
+
+
+class ChunkGather:
+    """The PCM gather of the overlapped multi-GPU schedule (bench.run_chunks at N > 1; reference: the
+    replicas' PCM reaching the client, streaming_server.py:357-376,428-469). A chunk's PCM is gathered
+    to rank 0 only once the host has seen its codec event (``issue``), on a stream of its own (``stream``:
+    neither the decode stream nor the codec stream ever waits on the collective, and no queue parks on
+    another queue's event), asynchronously; ``wait(key)`` (host-side completion poll) runs before the
+    chunk's PCM buffer is written again. ``keep``: rank 0 keeps every gathered chunk (tests)."""
+
+    def __init__(self, dist, rank: int, world: int, stream=None, keep: bool = False):
+        self.dist, self.rank, self.world, self.stream = dist, rank, world, stream
+        self.work = {}
+        self.seq = 0
+        self.keep = keep
+        self.gathered: List[List[torch.Tensor]] = []
+
+    def issue(self, key, pcm: torch.Tensor):
+        self.wait(key)
+        if self.stream is not None:
+            with torch.cuda.stream(self.stream):
+                out, work = gather_pcm(pcm, self.dist, self.rank, self.world, async_op=True)
+        else:
+            out, work = gather_pcm(pcm, self.dist, self.rank, self.world, async_op=True)
+        self.seq += 1
+        self.work[key] = (work, out, self.seq)
+
+    def wait(self, key):
+        w = self.work.pop(key, None)
+        if w is None:
+            return
+        work, out, _ = w
+        if work is not None:
+            while not work.is_completed():  # host poll: nothing is enqueued on any stream
+                time.sleep(20e-6)
+        if self.keep and out is not None:
+            self.gathered.append([o.detach().cpu() for o in out])
+
+    def drain(self):
+        for key in sorted(self.work, key=lambda k: self.work[k][2]):  # in issue order
+            self.wait(key)
 
 
 def scatter_texts(texts: Optional[List[str]], streams_per_rank: int, device, dist=None, rank: int = 0,

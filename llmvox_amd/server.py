@@ -59,12 +59,16 @@ class _Session:
 class _Worker:
     """One device of the service: its engine, a FusedScheduler over it and the thread that runs it."""
 
-    def __init__(self, svc, engine, index: int, max_chunk: int, max_tokens: Optional[int]):
+    def __init__(self, svc, engine, index: int, max_chunk: int, max_tokens: Optional[int], overlap: bool = True):
         self.svc = svc
         self.engine = engine
         self.index = index
-        self.sched = FusedScheduler(engine, max_chunk=max_chunk, to_bytes=True)
         self.max_tokens = max_tokens or max(1, engine.max_positions - max_chunk - 1)
+        # the headline's schedule (FusedScheduler overlap): chunk c + 1's decode queued before chunk c
+        # is read back, chunk c's codec on a second stream, items delivered when its codec ends; the
+        # stop rule keeps the run-ahead from planning a stream past max_tokens / the KV capacity
+        self.sched = FusedScheduler(engine, max_chunk=max_chunk, to_bytes=True, overlap=overlap,
+                                    stop_rule=self._stop_rule)
         self.sessions: List[_Session] = []
         self.lock = threading.Condition()
         self.running = True
@@ -72,11 +76,14 @@ class _Worker:
         self.thread = threading.Thread(target=self._loop, name=f"lvx-tts-scheduler-{index}", daemon=True)
         self.thread.start()
 
-    def _stopped(self, st) -> bool:
+    def _stop_rule(self, st, n_tokens: int, position: int) -> bool:
         """A fed stream stops at max_tokens, or when its segment would outgrow the KV capacity
-        within the next chunk; stopping closes its text side (the scheduler then skips it)."""
-        if not st.m.closed and (len(st.tokens) >= self.max_tokens or
-                                st.m.position + self.sched.max_chunk >= self.engine.max_positions):
+        within the next chunk."""
+        return st.fed and (n_tokens >= self.max_tokens or position + self.sched.max_chunk >= self.engine.max_positions)
+
+    def _stopped(self, st) -> bool:
+        """Stopping closes a stream's text side (the scheduler then skips it)."""
+        if not st.m.closed and self._stop_rule(st, len(st.tokens), st.m.position):
             st.m.closed = True
         return st.m.closed
 
@@ -88,12 +95,13 @@ class _Worker:
             return
         s.done = True
         s.error = error
+        if self.sched.deliverer is not None:  # the items of completed chunks first (a chunk still in
+            self.sched.deliverer.wait()       # flight holds no live row of an ending session)
         if error is None:
             for st in s.streams:
                 if st.fed and st.m.speech_outputs:
                     toks, st.m.speech_outputs = st.m.speech_outputs, []
-                    codes = torch.tensor([toks], dtype=torch.int32, device=self.engine.device)
-                    st._out(self.engine.decode_codes(codes).cpu().numpy()[0].astype("float32").tobytes())
+                    st._out(self.sched.decode_now(toks))
         for q in s.queues:
             q.put("end")
         for st in s.streams:
@@ -113,7 +121,7 @@ class _Worker:
                 self.end(s)
 
     def _loop(self):
-        from ._lib import LvxCapacityError
+        from ._lib import LvxStreamError
         while True:
             try:
                 with self.lock:
@@ -123,9 +131,10 @@ class _Worker:
                     self._cap()
                     if not n:
                         self.lock.wait(timeout=0.01)
-            except LvxCapacityError as e:
+            except LvxStreamError as e:
                 # run_chunk delivered the chunk to every stream below the capacity edge and names
-                # the streams at the edge; only their sessions fail
+                # the streams at the edge (or, for a fused-MLP range error, the rows of that chunk);
+                # only their sessions fail
                 with self.lock:
                     live = [s for s in self.sessions if not s.done]
                     edge_streams = getattr(e, "streams", None) or []
@@ -152,7 +161,7 @@ class TTSService:
 
     def __init__(self, engine, max_chunk: int = 64, max_tokens: Optional[int] = None, eos: str = C.EOS_TOKEN,
                  eoa_id: int = C.EOA_TOKEN_ID, dumps=(C.INITIAL_DUMP_SIZE_1, C.INITIAL_DUMP_SIZE_2),
-                 stream_model=None, system_prompt: str = C.SYSTEM_PROMPT):
+                 stream_model=None, system_prompt: str = C.SYSTEM_PROMPT, overlap: bool = True):
         """engine: one Engine or a list of them (one per GPU). stream_model: an
         llm_streaming.StreamModel (or anything with its predict()): the request text is then the
         LLM prompt and its streamed reply is spoken, as the reference's /tts does
@@ -166,7 +175,7 @@ class TTSService:
         self.eos = eos
         self.eoa_id = eoa_id
         self.dumps = dumps
-        self.workers = [_Worker(self, e, i, max_chunk, max_tokens) for i, e in enumerate(engines)]
+        self.workers = [_Worker(self, e, i, max_chunk, max_tokens, overlap) for i, e in enumerate(engines)]
         self.sched = self.workers[0].sched
         self.max_tokens = self.workers[0].max_tokens
         self._next = 0
@@ -282,6 +291,7 @@ class TTSService:
                 w.lock.notify_all()
         for w in self.workers:
             w.thread.join(timeout=5)
+            w.sched.close()
 
 
 def create_app(service):

@@ -16,7 +16,9 @@ Two layers:
 from __future__ import annotations
 
 import asyncio
+import copy
 import re
+import threading
 from collections import deque
 from dataclasses import dataclass, field
 from queue import Empty, Queue
@@ -366,28 +368,102 @@ class FusedStream:
         self.sink.put(item)
 
 
+def _copy_machine(m: SegmentMachine) -> SegmentMachine:
+    """A speculative copy of a machine (its own word / id queues and speech outputs; the tokenizer
+    is shared)."""
+    c = copy.copy(m)
+    c.words = deque(m.words)
+    c.pending = deque(m.pending)
+    c.speech_outputs = list(m.speech_outputs)
+    return c
+
+
+class _Chunk:
+    """One launched AR chunk: its rows, steps, buffer set and completion event; ``bad`` holds the
+    streams whose rows it must not consume (rolled back by an end-of-audio of an older chunk)."""
+
+    def __init__(self, ready, n, buf, event):
+        self.ready, self.n, self.buf, self.event = ready, n, buf, event
+        self.bad = set()
+
+
+class _Deliverer:
+    """The overlapped scheduler's delivery thread: jobs run in submission order; each waits for its
+    codec event (if any), then hands its items to the streams, so a dump reaches its stream as soon
+    as its codec call has finished, in the reference's per-stream order."""
+
+    def __init__(self):
+        self.q: Queue = Queue()
+        self.cv = threading.Condition()
+        self.pending = 0
+        self.error: Optional[BaseException] = None
+        self.thread = threading.Thread(target=self._run, name="lvx-deliver", daemon=True)
+        self.thread.start()
+
+    def put(self, event, fn):
+        with self.cv:
+            self.pending += 1
+        self.q.put((event, fn))
+
+    def _run(self):
+        while True:
+            ev, fn = self.q.get()
+            if fn is None:
+                return
+            try:
+                if ev is not None:
+                    ev.synchronize()
+                fn()
+            except BaseException as e:  # surfaced on the scheduler thread (take_error)
+                if self.error is None:
+                    self.error = e
+            with self.cv:
+                self.pending -= 1
+                self.cv.notify_all()
+
+    def wait(self):
+        with self.cv:
+            while self.pending:
+                self.cv.wait()
+
+    def take_error(self):
+        e, self.error = self.error, None
+        if e is not None:
+            raise e
+
+    def close(self):
+        self.q.put((None, None))
+
+
 class FusedScheduler:
     """Continuous batching of many replica streams on one Engine.
 
-    Every ``run_chunk`` call: each stream with text available contributes its planned text
-    ids for the next n steps (n ends at the earliest pending dump boundary, so the first
-    chunk of a stream is decoded as soon as its tokens exist); the fused step runs n times
-    for all rows (one HIP-graph replay per step, no host traffic); tokens are read back once;
-    every stream's SegmentMachine consumes them in order; a stream that hits end-of-audio
-    drops its run-ahead tokens and its slot is rewound to position 0; all dumps of the chunk
-    are decoded (batched by length) and delivered in order.
+    A chunk: each stream with text available contributes its planned text ids for the next n steps
+    (n ends at the earliest pending dump boundary, so the first chunk of a stream is decoded as soon
+    as its tokens exist); the fused step runs n times for all rows (one HIP-graph replay per 16
+    steps, no host traffic); tokens are read back once; every stream's SegmentMachine consumes them
+    in order; a stream that hits end-of-audio drops its run-ahead tokens and its slot is rewound to
+    position 0; all dumps of the chunk are decoded (batched by length) and delivered in order.
 
-    With ``overlap=True`` the codec of chunk c runs on a second HIP stream while the AR decode of
-    chunk c+1 runs on the main one: chunk c's items are delivered by the next
-    ``run_chunk`` right after it has launched chunk c+1, or by ``flush`` (called by
-    ``run_until_idle`` and by an idle ``run_chunk``). Off by default: measured on MI355X, the
-    latency-bound AR chain stalls while codec kernels from another queue are in flight, so the
-    overlapped loop is slower than running the codec after the AR on one stream (25.5 vs
-    23.6 ms per 256-token chunk at 1 stream, 65.2 vs 64.4 ms at 32; round 1).
+    ``overlap=True`` runs the schedule of the reference's two replicas and of the bench
+    (streaming_server.py:357-376): chunk c + 1's decode steps are queued on the main
+    stream BEFORE chunk c's tokens are read back (planned from the streams' speculative state after
+    chunk c without an end-of-audio; a stream whose chunk c does end its segment has its chunk c + 1
+    row discarded, and its slot rewound behind it); chunk c's codec runs on a second HIP stream, queued
+    only once the host holds its tokens (host-paced: no queue ever waits on the other's event, which
+    costs every dispatch of the AR chain ~1 us); each chunk's items are delivered by a
+    delivery thread as soon as its codec event completes. Streams see the same items, in the same
+    order, as without overlap (tests/test_gpu_streaming.py). Run-ahead is skipped for a chunk whose
+    rows would cross max_positions (the capacity edge then behaves as without overlap). On a CPU
+    stand-in engine the same run-ahead / rollback / ordering runs with synchronous decodes.
+
+    ``stop_rule(stream, tokens, position)`` (optional): True when a stream must not be planned once it
+    has consumed ``tokens`` tokens and stands at ``position`` (the service's max_tokens / capacity
+    stop), applied to the speculative state too, so run-ahead never decodes past a stop.
     """
 
     def __init__(self, engine, max_chunk: int = 64, max_rows: Optional[int] = None, to_bytes: bool = True,
-                 overlap: bool = False):
+                 overlap: bool = False, stop_rule=None):
         import torch
         self.engine = engine
         self.torch = torch
@@ -396,26 +472,37 @@ class FusedScheduler:
         self.streams: List[FusedStream] = []
         self.free_slots = list(range(engine.max_streams - 1, -1, -1))
         self.to_bytes = to_bytes
+        self.stop_rule = stop_rule
         dev = engine.device
-        R, n = self.max_rows, max_chunk
-        self.slots_d = torch.full((R,), -1, dtype=torch.int32, device=dev)
-        self.plan_d = torch.zeros((R, n), dtype=torch.int32, device=dev)
-        self.rowstep_d = torch.zeros((R,), dtype=torch.int32, device=dev)
-        self.tok_d = torch.zeros((R, n), dtype=torch.int32, device=dev)
-        pin = torch.device(dev).type == "cuda"
-        self.plan_h = torch.zeros((R, n), dtype=torch.int32, pin_memory=pin)
-        self.slots_h = torch.full((R,), -1, dtype=torch.int32, pin_memory=pin)
-        self.overlap = bool(overlap) and pin
-        self.codec_stream = torch.cuda.Stream(device=dev) if self.overlap else None
-        self.pcm_h = None      # pinned staging buffer of the decode in flight (grown on demand)
-        self.pending = None    # (event, [(dump index, offset, samples)], order, ready) of the last chunk
+        self.cuda = torch.device(dev).type == "cuda"
+        self.overlap = bool(overlap)
+        self.codec_stream = torch.cuda.Stream(device=dev) if (self.overlap and self.cuda) else None
+        self.take = self.cuda and hasattr(engine, "take_errors")
+        self.bufs = [self._alloc() for _ in range(2 if self.overlap else 1)]
+        self._bi = 0
+        self.inflight: Deque[_Chunk] = deque()
+        self.deliverer = _Deliverer() if self.overlap else None
+
+    def _alloc(self):
+        torch, dev = self.torch, self.engine.device
+        R, n = self.max_rows, self.max_chunk
+        pin = self.cuda
+        return {"slots_d": torch.full((R,), -1, dtype=torch.int32, device=dev),
+                "plan_d": torch.zeros((R, n), dtype=torch.int32, device=dev),
+                "rowstep_d": torch.zeros((R,), dtype=torch.int32, device=dev),
+                "tok_d": torch.zeros((R, n), dtype=torch.int32, device=dev),
+                "err_d": torch.zeros((1,), dtype=torch.int32, device=dev),
+                "plan_h": torch.zeros((R, n), dtype=torch.int32, pin_memory=pin),
+                "slots_h": torch.full((R,), -1, dtype=torch.int32, pin_memory=pin),
+                "tok_h": torch.zeros((R, n), dtype=torch.int32, pin_memory=pin),
+                "err_h": torch.zeros((1,), dtype=torch.int32, pin_memory=pin)}
 
     def open_stream(self, index=0, dump_size=C.INITIAL_DUMP_SIZE_1, sink=None, **kw) -> FusedStream:
         if not self.free_slots:
             raise RuntimeError("no free KV slot")
         slot = self.free_slots.pop()
         st = FusedStream(self, slot, SegmentMachine(index=index, dump_size=dump_size, **kw), sink)
-        self.engine.reset_slot(slot)
+        self.engine.reset_slot(slot)  # (stream-ordered behind any chunk in flight on the slot)
         self.streams.append(st)
         return st
 
@@ -423,65 +510,132 @@ class FusedScheduler:
         self.streams.remove(st)
         self.free_slots.append(st.slot)
 
+    def close(self):
+        """Stop the delivery thread (after delivering what is queued)."""
+        if self.deliverer is not None:
+            self.deliverer.wait()
+            self.deliverer.close()
+            self.deliverer = None
+
     def _steps_to_dump(self, m: SegmentMachine):
         return max(1, m.dump_size - len(m.speech_outputs))
 
-    def run_chunk(self) -> int:
-        """One chunk for all ready streams; returns the number of decode steps run (0 = idle)."""
+    # -- planning ---------------------------------------------------------------------------
+    def _speculative(self):
+        """Each stream of the chunk in flight, advanced over that chunk as if it ended no segment:
+        {stream: (machine copy or None when the chunk ends its segment anyway, tokens consumed)}."""
+        spec = {}
+        for ch in self.inflight:
+            for st in ch.ready:
+                if st in ch.bad or st not in self.streams:
+                    continue
+                m0, ntok = spec.get(st, (st.m, len(st.tokens)))
+                if m0 is None:
+                    continue
+                m = _copy_machine(m0)
+                dummy = 0 if m.eoa_id != 0 else 1
+                ends = False
+                for _ in range(ch.n):
+                    if m.next_text_id() is None or any(e.kind == "signal" for e in m.consume(dummy)):
+                        ends = True  # (a max_audio_length reset: the chunk's real tokens end the segment)
+                        break
+                spec[st] = (None if ends else m, ntok + ch.n)
+        return spec
+
+    def _launch_next(self) -> int:
+        """Plan and queue the next chunk (from the speculative state of the chunk in flight, if any);
+        returns its steps, 0 when nothing is ready or run-ahead would cross the capacity edge."""
         torch = self.torch
+        spec = self._speculative() if self.inflight else {}
         ready = []
         for st in self.streams:
-            if st.m.closed:
+            m, ntok = spec.get(st, (st.m, len(st.tokens)))
+            if m is None or m.closed or m.next_text_id() is None:
                 continue
-            if st.m.next_text_id() is None:
+            if self.stop_rule is not None and self.stop_rule(st, ntok, m.position):
                 continue
-            ready.append(st)
+            ready.append((st, m))
         ready = ready[: self.max_rows]
         if not ready:
-            self.flush()
             return 0
-        n = min(self.max_chunk, min(self._steps_to_dump(st.m) for st in ready))
-        plans = {}
-        for st in ready:
-            p = st.m.plan(n)
-            plans[st] = p
+        n = min(self.max_chunk, min(self._steps_to_dump(m) for _, m in ready))
+        plans = []
+        for st, m in ready:
+            p = m.plan(n)
+            plans.append(p)
             n = min(n, len(p))
-        self.slots_h.fill_(-1)
-        for r, st in enumerate(ready):
-            self.slots_h[r] = st.slot
-            self.plan_h[r, :n] = torch.tensor(plans[st][:n], dtype=torch.int32)
+        if self.inflight and any(m.position + n > self.engine.max_positions for _, m in ready):
+            return 0  # the capacity edge: complete the chunk in flight first (no run-ahead)
+        buf = self.bufs[self._bi]
+        self._bi = (self._bi + 1) % len(self.bufs)
+        buf["slots_h"].fill_(-1)
+        for r, (st, m) in enumerate(ready):
+            buf["slots_h"][r] = st.slot
+            buf["plan_h"][r, :n] = torch.tensor(plans[r][:n], dtype=torch.int32)
         B = len(ready)
-        self.slots_d.copy_(self.slots_h, non_blocking=True)
-        self.plan_d.copy_(self.plan_h, non_blocking=True)
-        self.rowstep_d.zero_()
-        self.engine.ar_steps(n, self.slots_d[:B], self.plan_d[:B], self.rowstep_d[:B], self.tok_d[:B])
-        self.flush()  # the previous chunk's audio, decoded while this chunk's AR steps run
-        toks = self.tok_d[:B, :n].cpu().numpy()
+        buf["slots_d"].copy_(buf["slots_h"], non_blocking=True)
+        buf["plan_d"].copy_(buf["plan_h"], non_blocking=True)
+        buf["rowstep_d"].zero_()
+        self.engine.ar_steps(n, buf["slots_d"][:B], buf["plan_d"][:B], buf["rowstep_d"][:B], buf["tok_d"][:B])
+        ev = None
+        if self.cuda:
+            buf["tok_h"].copy_(buf["tok_d"], non_blocking=True)
+            if self.take:
+                from . import _lib
+                self.engine.take_errors(_lib.ERRW_AR, buf["err_d"])
+                buf["err_h"].copy_(buf["err_d"], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.engine.device))
+        self.inflight.append(_Chunk([st for st, _ in ready], n, buf, ev))
+        return n
+
+    # -- completion --------------------------------------------------------------------------
+    def _chunk_error(self, ch):
+        if not self.take:  # a stand-in engine: its own (synchronous) check
+            try:
+                self.engine.check_errors()
+            except Exception as e:
+                return e
+            return None
+        bits = int(ch.buf["err_h"][0])
+        if not bits:
+            return None
+        from . import _lib
+        return _lib.error_for(self.engine.lib.lvx_error_status(bits), bits)
+
+    def _complete(self, ch: _Chunk) -> int:
+        """Read back the chunk's tokens (waits for its event only), consume them, queue its decodes."""
+        if ch.event is not None:
+            ch.event.synchronize()
+        B, n = len(ch.ready), ch.n
+        toks = (ch.buf["tok_h"] if self.cuda else ch.buf["tok_d"])[:B, :n].numpy()
+        err = self._chunk_error(ch)
         # a KV-capacity error concerns only the rows that reached max_positions in this chunk (their
         # last positions were clamped); every other row's tokens are valid and are consumed, decoded
-        # and delivered below before the error is raised, naming the streams at the edge
-        cap_err, edge = None, set()
-        try:
-            self.engine.check_errors()
-        except Exception as e:
-            from ._lib import LvxCapacityError
-            if not isinstance(e, LvxCapacityError):
-                raise
-            # a row that ran past max_positions had its last positions clamped: those tokens are
-            # invalid. A row that ends exactly AT max_positions set the flag with the commit of its
-            # last step, but all n of its tokens came from positions <= max_positions - 1: they are
-            # valid and consumed below; the row is then reported at capacity with the others (ADVICE r03)
-            P = self.engine.max_positions
-            edge = {st for st in ready if st.m.position + n > P}
-            at_cap = {st for st in ready if st.m.position + n == P}
-            if not edge and not at_cap:  # not a position overflow of a known row (e.g. a plan overrun)
-                raise
-            cap_err = e
-            cap_err.streams = sorted(edge | at_cap, key=lambda st: st.slot)
+        # and delivered below before the error is raised, naming the streams at the edge. A fused-MLP
+        # range error (B <= 2) invalidates the logits of this chunk's rows: they are named the same way
+        from ._lib import LvxCapacityError, LvxNumericError
+        edge, at_cap = set(), set()
+        if err is not None:
+            if isinstance(err, LvxCapacityError):
+                # a row that ran past max_positions had its last positions clamped: those tokens are
+                # invalid. A row that ends exactly AT max_positions set the flag with the commit of
+                # its last step, but all n of its tokens came from positions <= max_positions - 1:
+                # they are consumed below, then the row is reported at capacity (ADVICE r03)
+                P = self.engine.max_positions
+                edge = {st for st in ch.ready if st.m.position + n > P}
+                at_cap = {st for st in ch.ready if st.m.position + n == P}
+                if not edge and not at_cap:  # not a position overflow of a known row (a plan overrun)
+                    raise err
+            elif isinstance(err, LvxNumericError):
+                edge = set(ch.ready)
+            else:
+                raise err
         dumps = []  # (stream, tokens)
-        order: Dict[FusedStream, List[tuple]] = {st: [] for st in ready}
-        for r, st in enumerate(ready):
-            if st in edge:
+        order: Dict[FusedStream, List[tuple]] = {st: [] for st in ch.ready}
+        ended = set()
+        for r, st in enumerate(ch.ready):
+            if st in edge or st in ch.bad or st not in self.streams:
                 continue
             for j in range(n):
                 tok = int(toks[r, j])
@@ -496,16 +650,40 @@ class FusedScheduler:
                         reset = True
                 if reset:
                     # run-ahead past end-of-audio: drop the rest, restart the slot at position 0
+                    # (queued behind any newer chunk in flight, whose row of this stream is discarded)
                     self.engine.set_slot(st.slot, 0, 0)
+                    for newer in self.inflight:
+                        newer.bad.add(st)
+                    ended.add(st)
                     break
+        # a row that reached the capacity exactly AND ended its segment in this chunk was rewound to
+        # position 0 by the end of audio: it continues, as the reference would
+        at_cap -= ended
         if self.overlap:
-            self._launch_decode(dumps, order, ready)
+            self._launch_decode(dumps, order, ch.ready)
         else:
-            self._deliver(self._decode(dumps), order, ready)
-        if cap_err is not None:
-            self.flush()
-            raise cap_err
+            self._deliver(self._decode(dumps), order, ch.ready)
+        if err is not None:
+            if self.deliverer is not None:
+                self.deliverer.wait()
+            err.streams = sorted(edge | at_cap, key=lambda st: st.slot)
+            if err.streams or not isinstance(err, LvxCapacityError):
+                raise err
         return n
+
+    def run_chunk(self) -> int:
+        """Serial: one chunk for all ready streams, its items delivered on return. Overlap: queue the
+        next chunk, then complete the one in flight before it (its items are delivered when its codec
+        call ends). Returns the steps queued or completed (0 = idle: everything delivered)."""
+        if self.deliverer is not None:
+            self.deliverer.take_error()
+        launched = self._launch_next()
+        if self.inflight and (len(self.inflight) > 1 or not launched or not self.overlap):
+            done = self._complete(self.inflight.popleft())
+            return launched or done
+        if not launched:
+            self.flush()
+        return launched
 
     def _deliver(self, pcm, order, ready):
         for st in ready:
@@ -530,39 +708,72 @@ class FusedScheduler:
             out = self.engine.decode_codes(codes).cpu().numpy()
             for k, i in enumerate(grp):
                 res[i] = out[k].astype("float32").tobytes() if self.to_bytes else out[k]
+        if dumps and self.take:  # the codec's own error word (host-synchronous here)
+            from . import _lib
+            e = torch.zeros((1,), dtype=torch.int32, device=self.engine.device)
+            self.engine.take_errors(_lib.ERRW_CODEC, e)
+            _lib.check_bits(int(e.item()))
         return res
 
-    def _launch_decode(self, dumps, order, ready):
-        """Queue the chunk's decodes on the codec stream, PCM into pinned host memory; no wait."""
+    def decode_now(self, tokens: List[int]):
+        """One dump decoded and returned at once (the service's end-of-request tails): on the codec
+        stream when overlapping, so it does not queue behind the decode chunk in flight."""
         torch = self.torch
+        if self.codec_stream is None:
+            return self._decode([(None, tokens)])[0]
+        with torch.cuda.stream(self.codec_stream):
+            out = self._decode([(None, tokens)])[0]
+        return out
+
+    def _launch_decode(self, dumps, order, ready):
+        """Queue the chunk's decodes on the codec stream (codes from the host: no wait on the AR
+        stream), PCM into pinned host memory, and a delivery job behind the codec's event."""
+        torch = self.torch
+        if not self.cuda:  # a stand-in engine: decode now, deliver in order through the same thread
+            pcm = self._decode(dumps)
+            self.deliverer.put(None, lambda: self._deliver(pcm, order, ready))
+            return
+        if not dumps:
+            self.deliverer.put(None, lambda: self._deliver([], order, ready))
+            return
+        from . import _lib
+        dev = self.engine.device
         total = 320 * sum(len(t) for _, t in dumps)
-        if self.pcm_h is None or self.pcm_h.numel() < total:
-            self.pcm_h = torch.empty(max(total, 1 << 16) * 2, dtype=torch.float32, pin_memory=True)
+        host = torch.empty(total, dtype=torch.float32, pin_memory=True)
+        err_h = torch.zeros((1,), dtype=torch.int32, pin_memory=True)
         spans, off = [], 0
         with torch.cuda.stream(self.codec_stream):
             for L, grp in self._groups(dumps):
-                codes = torch.tensor([dumps[i][1] for i in grp], dtype=torch.int32, device=self.engine.device)
-                out = self.engine.decode_codes(codes)
-                self.pcm_h[off:off + out.numel()].view(out.shape).copy_(out, non_blocking=True)
+                codes = torch.tensor([dumps[i][1] for i in grp], dtype=torch.int32).pin_memory()
+                out = self.engine.decode_codes(codes.to(dev, non_blocking=True))
+                host[off:off + out.numel()].view(out.shape).copy_(out, non_blocking=True)
                 for k, i in enumerate(grp):
                     spans.append((i, off + k * 320 * L, 320 * L))
                 off += out.numel()
+            err_d = torch.zeros((1,), dtype=torch.int32, device=dev)
+            self.engine.take_errors(_lib.ERRW_CODEC, err_d)
+            err_h.copy_(err_d, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self.codec_stream)
-        self.pending = (ev, spans, order, ready, len(dumps))
+        to_bytes, nd = self.to_bytes, len(dumps)
+
+        def deliver():
+            _lib.check_bits(int(err_h[0]))
+            pcm: List[object] = [None] * nd
+            for i, o, ln in spans:
+                a = host[o:o + ln].numpy()
+                pcm[i] = a.tobytes() if to_bytes else a.copy()
+            self._deliver(pcm, order, ready)
+
+        self.deliverer.put(ev, deliver)
 
     def flush(self):
-        """Deliver the items of the chunk whose decode is in flight (overlap mode)."""
-        if self.pending is None:
-            return
-        ev, spans, order, ready, nd = self.pending
-        self.pending = None
-        ev.synchronize()
-        pcm: List[object] = [None] * nd
-        for i, off, ln in spans:
-            a = self.pcm_h[off:off + ln].numpy()
-            pcm[i] = a.tobytes() if self.to_bytes else a.copy()
-        self._deliver(pcm, order, ready)
+        """Complete every chunk in flight and deliver everything queued."""
+        while self.inflight:
+            self._complete(self.inflight.popleft())
+        if self.deliverer is not None:
+            self.deliverer.wait()
+            self.deliverer.take_error()
 
     def run_until_idle(self, max_chunks: int = 1 << 30) -> int:
         total = 0

@@ -25,6 +25,7 @@ def test_gpus2_spawns_two_gloo_ranks():
     d = json.loads(line[0])
     assert d["dist"] == {"backend": "gloo", "world_size": 2}
     assert d["n_gpus"] == 2 and d["streams_per_rank"] == 3 and d["gathered_equals_scattered"]
+    assert d["paced_gather_equals_single_rank"]  # the overlapped schedule's asynchronous, paced gather
 
 
 def test_world_size_must_match_gpus():

@@ -55,3 +55,25 @@ def test_no_compat_layers_in_sources():
         if f.endswith((".hip", ".cpp", ".h")):
             t = open(os.path.join(src, f)).read()
             assert "__HIP_PLATFORM_AMD__" not in t and "cuda" not in t.lower().replace("accum", ""), f
+
+
+def test_error_status_names_every_set_bit(lib):
+    """Device error bits (AR word | codec word << 16) map to one status, the most specific condition
+    (index > state > capacity), with every set condition named in the message (an
+    index error set together with another one was lost). A host-only call: no GPU needed."""
+    from llmvox_amd import _lib
+    assert lib.lvx_error_status(0) == _lib.LVX_OK
+    assert lib.lvx_error_status(1) == _lib.LVX_E_CAPACITY
+    assert lib.lvx_error_status(32 | 1) == _lib.LVX_E_STATE
+    code = lib.lvx_error_status(1 | 32 | (4 << 16) | (8 << 16))
+    assert code == _lib.LVX_E_INDEX
+    msg = lib.lvx_last_error().decode()
+    for part in ("codec: a code outside", "fused MLP", "ISTFT window envelope", "KV capacity"):
+        assert part in msg, (part, msg)
+    with pytest.raises(_lib.LvxIndexError) as ei:
+        _lib.check_bits(1 | (4 << 16))
+    assert ei.value.bits == 1 | (4 << 16) and "KV capacity" in str(ei.value)
+    with pytest.raises(_lib.LvxNumericError):
+        _lib.check_bits(32)
+    with pytest.raises(_lib.LvxCapacityError):
+        _lib.check_bits(2)

@@ -151,3 +151,29 @@ def test_out_of_range_ids_raise_index_error(eng, what):
         eng.check_errors()  # cleared
     eng.decode_codes(torch.tensor([[0, 4095, 3]], dtype=torch.int32, device=eng.device))
     eng.check_errors()  # the envelope self-check holds and in-range codes raise nothing
+
+
+def test_error_words_are_split_and_every_bit_is_reported(eng):
+    """the codec keeps its own error word (it may run on a second stream beside the
+    decode), a take of one word leaves the other alone, and check_errors names every set condition."""
+    from llmvox_amd import _lib
+    dev = eng.device
+    eng.text_embed(torch.tensor([5, 400], dtype=torch.int64, device=dev))        # AR word, bit 4
+    side = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(side):                                                # codec word, bit 4
+        eng.decode_codes(torch.tensor([[1, 5000, 3]], dtype=torch.int32, device=dev))
+    side.synchronize()
+    bits = torch.zeros(1, dtype=torch.int32, device=dev)
+    eng.take_errors(_lib.ERRW_CODEC, bits)                                       # the codec word only
+    assert int(bits.item()) == 4 << 16
+    with pytest.raises(_lib.LvxIndexError) as ei:                               # the AR bit is still set
+        eng.check_errors()
+    assert ei.value.bits == 0 or "text id" in str(ei.value)
+    eng.check_errors()
+    # both words at once: one exception naming both
+    eng.text_embed(torch.tensor([-3], dtype=torch.int64, device=dev))
+    eng.decode_codes(torch.tensor([[4096]], dtype=torch.int32, device=dev))
+    with pytest.raises(_lib.LvxIndexError) as ei:
+        eng.check_errors()
+    assert "text id" in str(ei.value) and "codec: a code outside" in str(ei.value)
+    eng.check_errors()

@@ -128,28 +128,41 @@ def test_fused_multistream_batch_equals_single(handler):
         one.close_stream(st)
 
 
-def test_fused_overlap_delivers_same_items(handler):
-    """Codec on a second HIP stream (deferred delivery) == synchronous decode, item for item."""
-    texts = [WORDS, "hello there world.".split(" ")]
+@pytest.mark.parametrize("forced_eoa", [False, True])
+def test_fused_overlap_delivers_same_items(handler, forced_eoa):
+    """The service schedule (overlap: chunk c + 1's decode queued before chunk c is read back, chunk c's
+    codec on a second HIP stream, delivery by the delivery thread when its codec ends) == the serial
+    schedule, item for item, byte for byte. forced_eoa: the token the model emits at step 23 is the
+    end-of-audio id, so a segment ends mid-chunk and the run-ahead rows of that stream are rolled back
+    (VERDICT r04 item 2)."""
+    a = np.load(os.path.join(GOLDEN, "ar_golden.npz"))
+    eoa = int(a["ids"][23]) if forced_eoa else 453
+    texts = [WORDS, "hello there world.".split(" "), WORDS[:5] + ["again."], "one two three.".split(" ")]
     res = []
     for overlap in (False, True):
         sch = S.FusedScheduler(handler.engine, max_chunk=40, overlap=overlap)
         sts = []
         for i, t in enumerate(texts):
-            st = sch.open_stream(index=i % 2, dump_size=10 if i % 2 == 0 else 160)
+            st = sch.open_stream(index=i % 2, dump_size=10 if i % 2 == 0 else 160, eoa_id=eoa)
             for w in t:
                 st.feed(w)
             sts.append(st)
-        for _ in range(8):
+        for _ in range(10):
             sch.run_chunk()
         sch.flush()
-        res.append([list(st.events) for st in sts])
+        res.append([(list(st.events), list(st.tokens)) for st in sts])
+        assert sch.overlap == overlap
         for st in sts:
             sch.close_stream(st)
-    assert sch.overlap
-    for a, b in zip(*res):
-        assert len(a) == len(b) and len(a) > 0
-        for x, y in zip(a, b):
+        sch.close()
+    if forced_eoa:
+        assert any(isinstance(x, int) for ev, _ in res[0] for x in ev)  # a segment did end
+    for (a_ev, a_tok), (b_ev, b_tok) in zip(*res):
+        n = min(len(a_ev), len(b_ev))  # (the overlapped run decoded one more chunk in its 10 calls)
+        assert n > 0
+        m = min(len(a_tok), len(b_tok))
+        assert a_tok[:m] == b_tok[:m]
+        for x, y in zip(a_ev[:n], b_ev[:n]):
             assert type(x) is type(y)
             assert x == y
 

@@ -192,7 +192,7 @@ def test_row_ending_exactly_at_capacity_keeps_its_tokens():
     toks = []
     prev = 7
     for j, p in enumerate(range(60, 64)):
-        prev = ref._tok(int(sch.plan_h[0, j]), prev, p)
+        prev = ref._tok(int(sch.bufs[0]["plan_h"][0, j]), prev, p)
         toks.append(prev)
     assert a.tokens == toks
 
@@ -212,7 +212,10 @@ def test_capacity_edge_ends_only_its_request():
             # s0's replica 0 jumps to 8 positions below the capacity, past the service's own cap check
             st = s0.streams[0]
             eng.set_slot(st.slot, 392, 0)
-            st.m.gen_index = 392  # (the next chunk runs before the service's cap check sees it)
+            st.m.gen_index = 392
+            # (past the service's own stop rule too, which would keep it from being planned there)
+            rule = w.sched.stop_rule
+            w.sched.stop_rule = lambda x, n, p: False if x is st else rule(x, n, p)
         out = {}
 
         def read(name, s):
