@@ -389,6 +389,13 @@ def run_config3(args, eng, world, rank, local, dist):
     rng = np.random.default_rng(1234)  # rank 0 draws every rank's request texts
     pcm_bytes = [0]
 
+    class FirstBytes:  # a stream's sink: when its first PCM bytes were delivered
+        t = None
+
+        def put(self, item):
+            if self.t is None and isinstance(item, bytes):
+                self.t = time.perf_counter()
+
     def utterance():
         streams = []
         t0 = time.perf_counter()  # first text word enqueued (p50 first-chunk latency starts here)
@@ -397,17 +404,15 @@ def run_config3(args, eng, world, rank, local, dist):
         mine = scatter_texts(texts, S, dev, dist, rank, world)
         for s in range(S):
             g = rank * S + s
-            st = sched.open_stream(index=g % 2, dump_size=10 if g % 2 == 0 else 160)
+            st = sched.open_stream(index=g % 2, dump_size=10 if g % 2 == 0 else 160, sink=FirstBytes())
             for w in mine[s].split(" "):
                 st.feed(w)
             streams.append(st)
-        first = None
         while min(len(st.tokens) for st in streams) < N:
             if sched.run_chunk() == 0:
                 raise RuntimeError("scheduler went idle before the utterance ended")
-            if first is None and any(st.events for st in streams):
-                first = (time.perf_counter() - t0) * 1e3
         sched.flush()
+        first = (min(st.sink.t for st in streams if st.sink.t is not None) - t0) * 1e3
         tails = {}  # the tail below the current dump size: flushed as one last dump (end of audio)
         rest = [st for st in streams if st.m.speech_outputs]
         for L in sorted({len(st.m.speech_outputs) for st in rest}):
@@ -638,14 +643,35 @@ def first_chunk_latency_loaded(eng, busy=31, reps=12, max_chunk=64, seed=99, ove
     import queue
     import threading
     from llmvox_amd.streaming import FusedScheduler
-    sched = FusedScheduler(eng, max_chunk=max_chunk, to_bytes=True, overlap=overlap)
+    inbox = queue.Queue()
+
+    def admit():  # queued requests / closes, between chunks or (overlap) while the scheduler waits
+        while True:
+            try:
+                op, arg = inbox.get_nowait()
+            except queue.Empty:
+                return
+            if op == "open":
+                sink = arg[1]
+                st = sched.open_stream(index=0, dump_size=10, sink=sink)
+                for w in arg[0]:
+                    st.feed(w)
+                sink.stream = st
+            else:
+                sched.close_stream(arg)
+
+    def waiter(ev):  # as the service's waiter: admissions land while the device works
+        ev.synchronize()
+        admit()
+
+    sched = FusedScheduler(eng, max_chunk=max_chunk, to_bytes=True, overlap=overlap, waiter=waiter)
     rng = np.random.default_rng(seed)
     words = lambda n: " ".join(random_sentence(rng) for _ in range(n)).split(" ")
     for i in range(busy):  # replica streams as the service opens them (dump 10 / 160, x3 to 1280)
         st = sched.open_stream(index=i % 2, dump_size=10 if i % 2 == 0 else 160)
         for w in words(24):
             st.feed(w)
-    inbox, done = queue.Queue(), threading.Event()
+    done = threading.Event()
     errors = []
     busy_streams = list(sched.streams)
 
@@ -655,19 +681,7 @@ def first_chunk_latency_loaded(eng, busy=31, reps=12, max_chunk=64, seed=99, ove
         try:
             torch.cuda.set_stream(cur)  # the graph-replay stream of the timed run
             while not done.is_set():
-                while True:  # admit queued requests / closes between chunks
-                    try:
-                        op, arg = inbox.get_nowait()
-                    except queue.Empty:
-                        break
-                    if op == "open":
-                        sink = arg[1]
-                        st = sched.open_stream(index=0, dump_size=10, sink=sink)
-                        for w in arg[0]:
-                            st.feed(w)
-                        sink.stream = st
-                    else:
-                        sched.close_stream(arg)
+                admit()
                 for st in busy_streams:  # keep the load: top up the text of busy streams running dry
                     if st.m.next_text_id() is None:
                         for w in words(8):

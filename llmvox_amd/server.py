@@ -67,14 +67,28 @@ class _Worker:
         # the headline's schedule (FusedScheduler overlap): chunk c + 1's decode queued before chunk c
         # is read back, chunk c's codec on a second stream, items delivered when its codec ends; the
         # stop rule keeps the run-ahead from planning a stream past max_tokens / the KV capacity
-        self.sched = FusedScheduler(engine, max_chunk=max_chunk, to_bytes=True, overlap=overlap,
-                                    stop_rule=self._stop_rule)
-        self.sessions: List[_Session] = []
         self.lock = threading.Condition()
+        # the device's decode stream (a thread's default would be the legacy null stream: no graph
+        # replay, and it serialises with the codec stream); host waits on device events release the
+        # lock, so requests are admitted (and join the next chunk) while the scheduler waits
+        import torch
+        stream = torch.cuda.Stream(device=engine.device) if torch.device(engine.device).type == "cuda" else None
+        self.sched = FusedScheduler(engine, max_chunk=max_chunk, to_bytes=True, overlap=overlap,
+                                    stop_rule=self._stop_rule, waiter=self._wait, stream=stream)
+        self.sessions: List[_Session] = []
         self.running = True
         self.error: Optional[BaseException] = None
         self.thread = threading.Thread(target=self._loop, name=f"lvx-tts-scheduler-{index}", daemon=True)
         self.thread.start()
+
+    def _wait(self, ev):
+        """The scheduler's host wait on a device event, with the worker lock released meanwhile
+        (called with it held, from run_chunk)."""
+        self.lock.release()
+        try:
+            ev.synchronize()
+        finally:
+            self.lock.acquire()
 
     def _stop_rule(self, st, n_tokens: int, position: int) -> bool:
         """A fed stream stops at max_tokens, or when its segment would outgrow the KV capacity

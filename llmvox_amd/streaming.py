@@ -16,6 +16,7 @@ Two layers:
 from __future__ import annotations
 
 import asyncio
+import contextlib
 import copy
 import re
 import threading
@@ -382,8 +383,8 @@ class _Chunk:
     """One launched AR chunk: its rows, steps, buffer set and completion event; ``bad`` holds the
     streams whose rows it must not consume (rolled back by an end-of-audio of an older chunk)."""
 
-    def __init__(self, ready, n, buf, event):
-        self.ready, self.n, self.buf, self.event = ready, n, buf, event
+    def __init__(self, ready, n, buf, event, near=None):
+        self.ready, self.n, self.buf, self.event, self.near = ready, n, buf, event, near
         self.bad = set()
 
 
@@ -460,10 +461,20 @@ class FusedScheduler:
     ``stop_rule(stream, tokens, position)`` (optional): True when a stream must not be planned once it
     has consumed ``tokens`` tokens and stands at ``position`` (the service's max_tokens / capacity
     stop), applied to the speculative state too, so run-ahead never decodes past a stop.
+
+    Joining streams: a chunk longer than ``tail`` steps is queued as two calls with an event between
+    them, ``tail`` steps before its end; the next chunk is planned once that event has passed, so a
+    stream opened while a chunk runs joins the very next chunk (with run-ahead planned at the chunk's
+    start it would wait a whole extra chunk), and the tail steps cover the host's planning.
+    ``waiter(event)`` (optional) replaces every host wait on a device event: the service passes one that
+    releases its lock meanwhile, so requests are admitted while the scheduler waits for the device.
+    ``stream`` (optional): the HIP stream of the decode steps and slot updates, whatever thread calls
+    (default: the calling thread's current stream). Decode steps on the legacy null stream run
+    without graphs and serialise with every other stream, so the service gives each device one.
     """
 
     def __init__(self, engine, max_chunk: int = 64, max_rows: Optional[int] = None, to_bytes: bool = True,
-                 overlap: bool = False, stop_rule=None):
+                 overlap: bool = False, stop_rule=None, waiter=None, tail: int = 8, stream=None):
         import torch
         self.engine = engine
         self.torch = torch
@@ -473,6 +484,9 @@ class FusedScheduler:
         self.free_slots = list(range(engine.max_streams - 1, -1, -1))
         self.to_bytes = to_bytes
         self.stop_rule = stop_rule
+        self.waiter = waiter
+        self.tail = max(1, int(tail))
+        self.ar_stream = stream
         dev = engine.device
         self.cuda = torch.device(dev).type == "cuda"
         self.overlap = bool(overlap)
@@ -502,7 +516,8 @@ class FusedScheduler:
             raise RuntimeError("no free KV slot")
         slot = self.free_slots.pop()
         st = FusedStream(self, slot, SegmentMachine(index=index, dump_size=dump_size, **kw), sink)
-        self.engine.reset_slot(slot)  # (stream-ordered behind any chunk in flight on the slot)
+        with self._on_ar():
+            self.engine.reset_slot(slot)  # (stream-ordered behind any chunk in flight on the slot)
         self.streams.append(st)
         return st
 
@@ -516,6 +531,9 @@ class FusedScheduler:
             self.deliverer.wait()
             self.deliverer.close()
             self.deliverer = None
+
+    def _on_ar(self):
+        return self.torch.cuda.stream(self.ar_stream) if self.ar_stream is not None else contextlib.nullcontext()
 
     def _steps_to_dump(self, m: SegmentMachine):
         return max(1, m.dump_size - len(m.speech_outputs))
@@ -546,6 +564,9 @@ class FusedScheduler:
         """Plan and queue the next chunk (from the speculative state of the chunk in flight, if any);
         returns its steps, 0 when nothing is ready or run-ahead would cross the capacity edge."""
         torch = self.torch
+        if self.inflight and self.inflight[-1].near is not None:
+            self._wait(self.inflight[-1].near)  # `tail` steps before the chunk in flight ends
+            self.inflight[-1].near = None
         spec = self._speculative() if self.inflight else {}
         ready = []
         for st in self.streams:
@@ -566,6 +587,11 @@ class FusedScheduler:
             n = min(n, len(p))
         if self.inflight and any(m.position + n > self.engine.max_positions for _, m in ready):
             return 0  # the capacity edge: complete the chunk in flight first (no run-ahead)
+        with self._on_ar():
+            return self._launch(ready, plans, n)
+
+    def _launch(self, ready, plans, n) -> int:
+        torch = self.torch
         buf = self.bufs[self._bi]
         self._bi = (self._bi + 1) % len(self.bufs)
         buf["slots_h"].fill_(-1)
@@ -576,7 +602,15 @@ class FusedScheduler:
         buf["slots_d"].copy_(buf["slots_h"], non_blocking=True)
         buf["plan_d"].copy_(buf["plan_h"], non_blocking=True)
         buf["rowstep_d"].zero_()
-        self.engine.ar_steps(n, buf["slots_d"][:B], buf["plan_d"][:B], buf["rowstep_d"][:B], buf["tok_d"][:B])
+        args = (buf["slots_d"][:B], buf["plan_d"][:B], buf["rowstep_d"][:B], buf["tok_d"][:B])
+        near = None
+        if self.overlap and self.cuda and n > self.tail:
+            self.engine.ar_steps(n - self.tail, *args)
+            near = torch.cuda.Event()
+            near.record(torch.cuda.current_stream(self.engine.device))
+            self.engine.ar_steps(self.tail, *args)
+        else:
+            self.engine.ar_steps(n, *args)
         ev = None
         if self.cuda:
             buf["tok_h"].copy_(buf["tok_d"], non_blocking=True)
@@ -586,8 +620,14 @@ class FusedScheduler:
                 buf["err_h"].copy_(buf["err_d"], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.engine.device))
-        self.inflight.append(_Chunk([st for st, _ in ready], n, buf, ev))
+        self.inflight.append(_Chunk([st for st, _ in ready], n, buf, ev, near))
         return n
+
+    def _wait(self, ev):
+        if self.waiter is not None:
+            self.waiter(ev)
+        else:
+            ev.synchronize()
 
     # -- completion --------------------------------------------------------------------------
     def _chunk_error(self, ch):
@@ -606,7 +646,7 @@ class FusedScheduler:
     def _complete(self, ch: _Chunk) -> int:
         """Read back the chunk's tokens (waits for its event only), consume them, queue its decodes."""
         if ch.event is not None:
-            ch.event.synchronize()
+            self._wait(ch.event)
         B, n = len(ch.ready), ch.n
         toks = (ch.buf["tok_h"] if self.cuda else ch.buf["tok_d"])[:B, :n].numpy()
         err = self._chunk_error(ch)
@@ -651,7 +691,8 @@ class FusedScheduler:
                 if reset:
                     # run-ahead past end-of-audio: drop the rest, restart the slot at position 0
                     # (queued behind any newer chunk in flight, whose row of this stream is discarded)
-                    self.engine.set_slot(st.slot, 0, 0)
+                    with self._on_ar():
+                        self.engine.set_slot(st.slot, 0, 0)
                     for newer in self.inflight:
                         newer.bad.add(st)
                     ended.add(st)
