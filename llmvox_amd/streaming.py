@@ -256,6 +256,18 @@ class SegmentMachine:
         self.words.append(word)
 
     def _word_ids(self, word: str):
+        """(ids, end of speech, end of generation) of a word; memoised (plan() re-reads the words ahead
+        every chunk, and the regex tokenizer costs ~10 us a word)."""
+        cache = self.__dict__.setdefault("_ids_cache", {})
+        got = cache.get(word)
+        if got is None:
+            got = cache[word] = self._word_ids_uncached(word)
+            if len(cache) > 4096:
+                cache.clear()
+        ids, eos_flag, end_gen = got
+        return list(ids), eos_flag, end_gen
+
+    def _word_ids_uncached(self, word: str):
         eos = self.eos
         if (eos in word) or (word[-1] == "."):
             end_gen = eos in word
@@ -340,6 +352,41 @@ class SegmentMachine:
             self.speech_outputs = []
             self._grow()
         return ev
+
+    def consume_many(self, tokens) -> tuple:
+        """``consume`` over a run of tokens, stopping after a segment end: (events, tokens consumed).
+        A run without end-of-audio that stays within max_audio_length takes a batched path (the text
+        ids popped at once, the dumps cut as consecutive dump-size slices: exactly what consume does one
+        token at a time, since a dump empties the outputs whenever they reach the dump size)."""
+        n = len(tokens)
+        if self.eoa_id in tokens or len(self.speech_outputs) + n > self.max_audio_len:
+            ev: List[Event] = []
+            for j, t in enumerate(tokens):
+                e = self.consume(int(t))
+                ev += e
+                if any(x.kind == "signal" for x in e):
+                    return ev, j + 1
+            return ev, n
+        k = n
+        while k:
+            if not self.pending and self.end_of_speech:
+                break  # the rest are PAD steps: _refill would push one PAD id per step and pop it
+            if not self._refill():
+                raise RuntimeError("consume() without an available text id")
+            take = min(k, len(self.pending))
+            for _ in range(take):
+                self.pending.popleft()
+            k -= take
+        self.gen_index += n
+        buf = self.speech_outputs + [int(t) for t in tokens]  # (ints: tokens may be numpy scalars)
+        ev = []
+        pos = 0
+        while len(buf) - pos >= self.dump_size:
+            ev.append(Event("audio", tokens=buf[pos:pos + self.dump_size]))
+            pos += self.dump_size
+            self._grow()
+        self.speech_outputs = buf[pos:]
+        return ev, n
 
     @property
     def position(self):
@@ -552,11 +599,11 @@ class FusedScheduler:
                     continue
                 m = _copy_machine(m0)
                 dummy = 0 if m.eoa_id != 0 else 1
-                ends = False
-                for _ in range(ch.n):
-                    if m.next_text_id() is None or any(e.kind == "signal" for e in m.consume(dummy)):
-                        ends = True  # (a max_audio_length reset: the chunk's real tokens end the segment)
-                        break
+                try:
+                    ev, used = m.consume_many([dummy] * ch.n)
+                    ends = used < ch.n or any(e.kind == "signal" for e in ev)  # (a max_audio_length reset)
+                except RuntimeError:
+                    ends = True
                 spec[st] = (None if ends else m, ntok + ch.n)
         return spec
 
@@ -594,11 +641,11 @@ class FusedScheduler:
         torch = self.torch
         buf = self.bufs[self._bi]
         self._bi = (self._bi + 1) % len(self.bufs)
-        buf["slots_h"].fill_(-1)
-        for r, (st, m) in enumerate(ready):
-            buf["slots_h"][r] = st.slot
-            buf["plan_h"][r, :n] = torch.tensor(plans[r][:n], dtype=torch.int32)
         B = len(ready)
+        sl = buf["slots_h"].numpy()
+        sl[:] = -1
+        sl[:B] = [st.slot for st, _ in ready]
+        buf["plan_h"].numpy()[:B, :n] = np.array([p[:n] for p in plans], dtype=np.int32)
         buf["slots_d"].copy_(buf["slots_h"], non_blocking=True)
         buf["plan_d"].copy_(buf["plan_h"], non_blocking=True)
         buf["rowstep_d"].zero_()
@@ -677,26 +724,25 @@ class FusedScheduler:
         for r, st in enumerate(ch.ready):
             if st in edge or st in ch.bad or st not in self.streams:
                 continue
-            for j in range(n):
-                tok = int(toks[r, j])
-                st.tokens.append(tok)
-                reset = False
-                for e in st.m.consume(tok):
-                    if e.kind == "audio":
-                        dumps.append((st, e.tokens))
-                        order[st].append(("audio", len(dumps) - 1))
-                    else:
-                        order[st].append(("signal", e.signal))
-                        reset = True
-                if reset:
-                    # run-ahead past end-of-audio: drop the rest, restart the slot at position 0
-                    # (queued behind any newer chunk in flight, whose row of this stream is discarded)
-                    with self._on_ar():
-                        self.engine.set_slot(st.slot, 0, 0)
-                    for newer in self.inflight:
-                        newer.bad.add(st)
-                    ended.add(st)
-                    break
+            row = toks[r].tolist()
+            evs, used = st.m.consume_many(row)
+            st.tokens.extend(row[:used])
+            reset = False
+            for e in evs:
+                if e.kind == "audio":
+                    dumps.append((st, e.tokens))
+                    order[st].append(("audio", len(dumps) - 1))
+                else:
+                    order[st].append(("signal", e.signal))
+                    reset = True
+            if reset:
+                # run-ahead past end-of-audio: drop the rest, restart the slot at position 0
+                # (queued behind any newer chunk in flight, whose row of this stream is discarded)
+                with self._on_ar():
+                    self.engine.set_slot(st.slot, 0, 0)
+                for newer in self.inflight:
+                    newer.bad.add(st)
+                ended.add(st)
         # a row that reached the capacity exactly AND ended its segment in this chunk was rewound to
         # position 0 by the end of audio: it continues, as the reference would
         at_cap -= ended

@@ -66,3 +66,30 @@ def test_overlap_stop_rule_never_plans_past_a_stop():
         sch.close()
     assert len(got[0]) == 34  # chunks 8 + 2 (dump at 10) + 8 + 8 + 8: the first count >= 30
     assert got[1] == got[0]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_consume_many_equals_per_token_consume(seed):
+    """The batched consume path gives the events, state and stop point of consume() token by token."""
+    rng = np.random.default_rng(seed)
+    words = TEXTS[seed % len(TEXTS)].split(" ") * 3
+    a = S.SegmentMachine(index=seed % 2, dump_size=int(rng.choice([4, 10, 160])), eoa_id=453)
+    b = S.SegmentMachine(index=seed % 2, dump_size=a.dump_size, eoa_id=453)
+    for w in words:
+        a.feed(w)
+        b.feed(w)
+    for _ in range(60):
+        n = int(rng.integers(1, 40))
+        toks = rng.integers(0, 4096, size=n)
+        if rng.random() < 0.15:
+            toks[rng.integers(0, n)] = 453
+        if a.next_text_id() is None:
+            break
+        ev_a, used = a.consume_many(toks.tolist())
+        ev_b = []
+        for t in toks.tolist()[:used]:
+            ev_b += b.consume(t)
+        assert used == n or any(e.kind == "signal" for e in ev_a)
+        assert [(e.kind, e.tokens, e.signal) for e in ev_a] == [(e.kind, e.tokens, e.signal) for e in ev_b]
+        assert (a.speech_outputs, a.dump_size, a.gen_index, list(a.pending), list(a.words), a.end_of_speech) == \
+            (b.speech_outputs, b.dump_size, b.gen_index, list(b.pending), list(b.words), b.end_of_speech)
