@@ -814,45 +814,50 @@ class FusedScheduler:
 
     def _launch_decode(self, dumps, order, ready):
         """Queue the chunk's decodes on the codec stream (codes from the host: no wait on the AR
-        stream), PCM into pinned host memory, and a delivery job behind the codec's event."""
+        stream), one call per dump length, shortest first, each with its PCM copied into pinned host
+        memory and a delivery job behind its own event: a stream's items go out with the job of its
+        (last) dump as soon as that call ends; a 10-frame first dump does not wait for a 1,280-frame one
+        of the same chunk. Streams without a dump in the chunk are served by the first job."""
         torch = self.torch
         if not self.cuda:  # a stand-in engine: decode now, deliver in order through the same thread
             pcm = self._decode(dumps)
             self.deliverer.put(None, lambda: self._deliver(pcm, order, ready))
             return
-        if not dumps:
+        groups = sorted(self._groups(dumps), key=lambda g: g[0])
+        if not groups:
             self.deliverer.put(None, lambda: self._deliver([], order, ready))
             return
         from . import _lib
         dev = self.engine.device
-        total = 320 * sum(len(t) for _, t in dumps)
-        host = torch.empty(total, dtype=torch.float32, pin_memory=True)
-        err_h = torch.zeros((1,), dtype=torch.int32, pin_memory=True)
-        spans, off = [], 0
-        with torch.cuda.stream(self.codec_stream):
-            for L, grp in self._groups(dumps):
+        gi = {i: g for g, (_, grp) in enumerate(groups) for i in grp}
+        last = {}  # stream -> the group whose job delivers its items
+        for st in ready:
+            idx = [gi[v] for kind, v in order[st] if kind == "audio"]
+            last[st] = max(idx) if idx else 0
+        to_bytes, nd = self.to_bytes, len(dumps)
+        pcm: List[object] = [None] * nd  # filled by the jobs, in order
+        for g, (L, grp) in enumerate(groups):
+            host = torch.empty(len(grp) * 320 * L, dtype=torch.float32, pin_memory=True)
+            err_h = torch.zeros((1,), dtype=torch.int32, pin_memory=True)
+            with torch.cuda.stream(self.codec_stream):
                 codes = torch.tensor([dumps[i][1] for i in grp], dtype=torch.int32).pin_memory()
                 out = self.engine.decode_codes(codes.to(dev, non_blocking=True))
-                host[off:off + out.numel()].view(out.shape).copy_(out, non_blocking=True)
+                host.view(out.shape).copy_(out, non_blocking=True)
+                err_d = torch.zeros((1,), dtype=torch.int32, device=dev)
+                self.engine.take_errors(_lib.ERRW_CODEC, err_d)
+                err_h.copy_(err_d, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.codec_stream)
+            sts = [st for st in ready if last[st] == g]
+
+            def deliver(host=host, err_h=err_h, grp=grp, L=L, sts=sts):
+                _lib.check_bits(int(err_h[0]))
                 for k, i in enumerate(grp):
-                    spans.append((i, off + k * 320 * L, 320 * L))
-                off += out.numel()
-            err_d = torch.zeros((1,), dtype=torch.int32, device=dev)
-            self.engine.take_errors(_lib.ERRW_CODEC, err_d)
-            err_h.copy_(err_d, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(self.codec_stream)
-        to_bytes, nd = self.to_bytes, len(dumps)
+                    a = host[k * 320 * L:(k + 1) * 320 * L].numpy()
+                    pcm[i] = a.tobytes() if to_bytes else a.copy()
+                self._deliver(pcm, order, sts)
 
-        def deliver():
-            _lib.check_bits(int(err_h[0]))
-            pcm: List[object] = [None] * nd
-            for i, o, ln in spans:
-                a = host[o:o + ln].numpy()
-                pcm[i] = a.tobytes() if to_bytes else a.copy()
-            self._deliver(pcm, order, ready)
-
-        self.deliverer.put(ev, deliver)
+            self.deliverer.put(ev, deliver)
 
     def flush(self):
         """Complete every chunk in flight and deliver everything queued."""
