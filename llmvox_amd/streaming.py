@@ -651,7 +651,7 @@ class FusedScheduler:
         buf["rowstep_d"].zero_()
         args = (buf["slots_d"][:B], buf["plan_d"][:B], buf["rowstep_d"][:B], buf["tok_d"][:B])
         near = None
-        if self.overlap and self.cuda and n > self.tail:
+        if self.overlap and self.cuda and n >= 2 * self.tail:  # (a short chunk is planned behind at once)
             self.engine.ar_steps(n - self.tail, *args)
             near = torch.cuda.Event()
             near.record(torch.cuda.current_stream(self.engine.device))
