@@ -49,6 +49,7 @@ struct GemmArgs {
                              // null for the separate reduce kernel
   int asplit;                // fp32 parity mode, bf16x3 GEMM: A is a split image (split_store), not fp32
   int csplit;                // fp32 parity mode, bf16x3 GEMM (bias + GELU): C written as a split image
+  const float* ascale;       // fp8 activations (codec_dtype FP8, gemm_glds_kernel<fp8_t>): per-row scale, a = q * s
 };
 
 template <typename T> __device__ __forceinline__ void load8(const T* p, float* v);
@@ -124,6 +125,7 @@ template <typename TC>
 __device__ __forceinline__ void store_out(TC* p, float v);
 template <> __device__ __forceinline__ void store_out<float>(float* p, float v) { *p = v; }
 template <> __device__ __forceinline__ void store_out<bf16_t>(bf16_t* p, float v) { *p = f32_to_bf16(v); }
+template <> __device__ __forceinline__ void store_out<fp8_t>(fp8_t* p, float v) { *p = f32_to_fp8(v); }
 
 template <bool BF, typename TA, typename TB, int AMODE, int EPI, typename TC, bool KF>
 __global__ __launch_bounds__(256) void gemm_mfma_kernel(GemmArgs g) {
@@ -700,6 +702,7 @@ constexpr int G3_AP = G3_BM / 8 / 8, G3_BP = G3_BN / 8 / 8;  // 1-KB DMA pieces 
 static_assert(2 * 2 * G3_STAGE <= 160 * 1024 && 3 * G3_STAGE <= 160 * 1024, "LDS stages");
 __device__ __attribute__((aligned(16))) uint32_t g3_zero[4];
 typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef int i32x8f __attribute__((ext_vector_type(8)));  // 32 fp8 (e4m3fn) MFMA operand
 
 __device__ __forceinline__ void glds16(const void* src, unsigned char* lds) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
@@ -812,6 +815,53 @@ __global__ __launch_bounds__(512, NS == 2 ? 2 : 1) void gemm_glds_kernel(GemmArg
   const int kl = nkt - 1;
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p) issue(min(p, kl), p);
+  if constexpr (sizeof(TA) == 1) {
+    // fp8 x fp8 (codec_dtype FP8): a 128-B row holds 128 k; lane l's fragment is k 32 (l >> 4) .. + 31 of
+    // its row (the two 16-B segments 2 (l >> 4), 2 (l >> 4) + 1), one v_mfma_scale_f32_16x16x128_f8f6f4 per
+    // (i, j) and k-tile with unit E8M0 scales (127): the weights' per-row and the activations' per-frame
+    // fp32 scales are applied in the epilogue (tools/mx_fp8_probe.hip checks the lane maps and scales)
+    for (int kt = 0; kt < nkt; ++kt) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * (G3_AP + G3_BP)) : "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      issue(min(kt + NS - 1, kl), (kt + NS - 1) % NS);
+      const unsigned char* sa = smem + (kt % NS) * G3_STAGE;
+      const unsigned char* sb = sa + G3_ABYTES;
+      const int s0 = ((2 * fseg) ^ fsw) * 16, s1 = ((2 * fseg + 1) ^ fsw) * 16;
+      i32x8f fa8[4], fb8[3];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const unsigned char* r = sa + (wm * 64 + i * 16 + frow) * 128;
+        const u32x4 lo = *reinterpret_cast<const u32x4*>(r + s0), hi = *reinterpret_cast<const u32x4*>(r + s1);
+        fa8[i] = i32x8f{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const unsigned char* r = sb + (wn * 48 + j * 16 + frow) * 128;
+        const u32x4 lo = *reinterpret_cast<const u32x4*>(r + s0), hi = *reinterpret_cast<const u32x4*>(r + s1);
+        fb8[j] = i32x8f{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fb8[j], fa8[i], acc[i][j], 0, 0, 0, 127, 0, 127);
+    }
+    // the scales: acc[i][j][e] belongs to row m0 + wm*64 + i*16 + (lane & 15), column n0 + wn*48 + j*16 + cq + e
+    f32x4v wsc[3];
+    float asc[4];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      wsc[j] = *reinterpret_cast<const f32x4v*>(g.wscale + min(n0 + wn * 48 + j * 16 + 4 * (lane >> 4), g.N - 4));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) asc[i] = g.ascale[min(m0 + wm * 64 + i * 16 + frow, g.M - 1)];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[i][j][e] = acc[i][j][e] * wsc[j][e] * asc[i];
+  } else
   for (int kt = 0; kt < nkt; ++kt) {
     // this wave's DMAs of tile kt have landed (the NS - 2 later tiles' stay in flight); after the
     // barrier every wave's have, and every wave is done reading the stage (tile kt - 1) that tile
@@ -1148,7 +1198,9 @@ static bool skinny_launch(const GemmArgs& g, hipStream_t s) {
 template <typename TW, typename TA, int AMODE, int EPI, typename TC = float>
 static void gemm_w(const GemmArgs& g, hipStream_t s) {
   if constexpr (sizeof(TW) == 2) {
-    if (g.wscale) gemm2_launch<TA, fp8_t, AMODE, EPI, TC>(g, s);  // fp8 codec weights: any M
+    if (g.ascale) {  // fp8 activations x fp8 weights on the block-scaled fp8 MFMA (the decode's large-M pwconv1)
+      if constexpr (AMODE == A_PLAIN && EPI != E_SCALE) g3_launch<AMODE, EPI, TC, fp8_t>(g, s);
+    } else if (g.wscale) gemm2_launch<TA, fp8_t, AMODE, EPI, TC>(g, s);  // fp8 codec weights: any M
     else if (sizeof(TA) == 2 && opts().codec_skinny && g.M <= SKINNY_MAX_M && skinny_launch<AMODE, EPI, TC>(g, s))
       return;
     else if (sizeof(TA) == 2 && EPI != E_SCALE && g3_ok(g)) g3_launch<AMODE, (EPI == E_SCALE ? E_BIAS : EPI), TC>(g, s);
@@ -1160,8 +1212,12 @@ static void gemm_w(const GemmArgs& g, hipStream_t s) {
     if (EPI != E_SCALE && g3_split(g)) {
       // A / C as split images only where the orchestration asked for them (decode_impl's ConvNeXt loop)
       if constexpr (AMODE == A_PLAIN && EW == E_BIAS_GELU) {
-        if (g.asplit && g.csplit) return g3_launch<AMODE, EW, float, float, 7>(g, s);
-        if (g.csplit) return g3_launch<AMODE, EW, float, float, 5>(g, s);
+        // the split-image store lives in the vectorised epilogue only (4 consecutive columns per lane):
+        // N or ldc not a multiple of 32 would take the per-element store and write plain fp32, which
+        // the next GEMM would read as a split image -- such a C is never split
+        const bool cs = g.csplit && (g.N % 32) == 0 && (g.ldc % 32) == 0;
+        if (g.asplit && cs) return g3_launch<AMODE, EW, float, float, 7>(g, s);
+        if (cs) return g3_launch<AMODE, EW, float, float, 5>(g, s);
       }
       if (g.asplit) return g3_launch<AMODE, EW, float, float, 3>(g, s);
       g3_launch<AMODE, EW, float, float, 1>(g, s);
@@ -1412,13 +1468,16 @@ __global__ __launch_bounds__(256) void gn_adaln_kernel(const float* __restrict__
 // guarded sum's order; the LayerNorm reductions follow row_ln's order (same bits as that form).
 // FT = 16 for large M, 4 when there are few frames.
 // SPO (fp32 parity mode): y written as the split image of its rows (split_store) for pwconv1's bf16x3 GEMM
+// TO = fp8_t (codec_dtype FP8, pwconv1 on the block-scaled fp8 MFMA): y as e4m3fn with one fp32 scale per
+// frame in ys (y = q * ys[frame], ys = max |y| / 448 over the frame's 768 channels, RNE)
 template <typename TO, int FT, bool SPO = false>
 __global__ __launch_bounds__(256) void dwconv_adaln_tile_kernel(const float* __restrict__ x, int L,
                                                                 const float* __restrict__ dwt,
                                                                 const float* __restrict__ dwb,
                                                                 const float* __restrict__ scale,
-                                                                const float* __restrict__ shift, TO* __restrict__ y) {
-  __shared__ float red[2][4][FT];
+                                                                const float* __restrict__ shift, TO* __restrict__ y,
+                                                                float* __restrict__ ys = nullptr) {
+  __shared__ float red[3][4][FT];
   const int b = blockIdx.y, t0 = blockIdx.x * FT, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   float v[3][FT], sc[3], sh[3];
   // every load of the block issued before the first use, the small operands first (the compiler had
@@ -1485,6 +1544,25 @@ __global__ __launch_bounds__(256) void dwconv_adaln_tile_kernel(const float* __r
 #pragma unroll
     for (int i = 0; i < 4; ++i) r += red[1][i][f];
     const float rstd = 1.0f / sqrtf(r * (1.0f / CD) + 1e-6f);
+    if constexpr (sizeof(TO) == 1) {  // fp8: the frame's max |y| first (block max), then q = y / s
+      float o[3], m = 0.f;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        o[j] = v[j][f] * rstd * sc[j] + sh[j];
+        m = fmaxf(m, fabsf(o[j]));
+      }
+      m = wave_max(m);
+      if (lane == 0) red[2][wave][f] = m;
+      __syncthreads();
+      m = fmaxf(fmaxf(red[2][0][f], red[2][1][f]), fmaxf(red[2][2][f], red[2][3][f]));
+      const float sf = m > 0.f ? m * (1.0f / 448.f) : 1.f, inv = 1.0f / sf;
+      if (t0 + f < L) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) y[((size_t)b * L + t0 + f) * CD + tid + 256 * j] = f32_to_fp8(o[j] * inv);
+        if (tid == 0) ys[(size_t)b * L + t0 + f] = sf;
+      }
+      continue;
+    }
     if (t0 + f < L) {
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
@@ -1900,11 +1978,21 @@ static void decode_impl(const CodecWeights& w, const CodecScratch& sc, const flo
     // in-register split makes, computed once per element instead of once per reading block)
     if constexpr (sizeof(TW) == 4) {
       const bool s1 = g3_split_in(c) && dwft == 0, s2 = g3_split_in(d);
+      const bool cs = s1 && s2 && (c.N % 32) == 0 && (c.ldc % 32) == 0;  // (gemm_w's split-store condition)
       c.asplit = s1;
-      c.csplit = s1 && s2;
-      d.asplit = s1 && s2;
+      c.csplit = cs;
+      d.asplit = cs;
     }
-    if (c.asplit)
+    // codec_dtype FP8 at large M: pwconv1 as fp8 x fp8 on the block-scaled MFMA, its operand written in
+    // e4m3fn with per-frame scales by the dwconv + AdaLN kernel (option codec_exp bit 32: off, the
+    // fp8-weight bf16 GEMM)
+    const bool q8 = sizeof(TW) == 2 && c.wscale && sc.rowscale && !(opts().codec_exp & 32) && g3_ok<fp8_t>(c);
+    if (q8) {
+      c.A = t2; c.ascale = sc.rowscale;  // (t2 as bytes: [M][768] e4m3fn)
+      hipLaunchKernelGGL((dwconv_adaln_tile_kernel<fp8_t, 4>), dim3((L + 3) / 4, B), dim3(256), 0, s, x, L, w.dw_w[i],
+                         w.dw_b[i], w.cn_scale[i] + (size_t)bw * CD, w.cn_shift[i] + (size_t)bw * CD,
+                         reinterpret_cast<fp8_t*>(t2), sc.rowscale);
+    } else if (c.asplit)
       hipLaunchKernelGGL((dwconv_adaln_tile_kernel<TAct, 4, true>), dim3((L + 3) / 4, B), dim3(256), 0, s, x, L, w.dw_w[i],
                          w.dw_b[i], w.cn_scale[i] + (size_t)bw * CD, w.cn_shift[i] + (size_t)bw * CD, t2a);
     else if (M >= 2048 && dwft == 3)

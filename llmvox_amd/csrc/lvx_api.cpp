@@ -593,7 +593,8 @@ int lvx_finalize(lvx_ctx* c) {
       (r = c->dalloc(&cs.ws, (size_t)std::max(M, 256) * 2304 * 4)) ||
       (r = c->dalloc(&cs.att, (size_t)M * (std::min(M, kMaxCodecL) + 4))) ||
       (r = c->dalloc(&cs.stats, (size_t)M * 32 * 2)) || (r = c->dalloc(&cs.spec, (size_t)M * 1282)) ||
-      (r = c->dalloc(&cs.frames, (size_t)M * 1280)) || (r = c->dalloc(&cs.tick, 4096)))
+      (r = c->dalloc(&cs.frames, (size_t)M * 1280)) || (r = c->dalloc(&cs.rowscale, (size_t)M)) ||
+      (r = c->dalloc(&cs.tick, 4096)))
     return r;
   HIP_TRY(hipMemset(cs.tick, 0, 4096 * 4));
   cs.err = st.err + 1;  // the codec's own word (it may run on a second stream beside the AR)

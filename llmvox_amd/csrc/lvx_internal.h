@@ -184,6 +184,7 @@ struct CodecScratch {
   float* stats = nullptr;  // [B][32][2]
   float* spec = nullptr;   // [M][1282]
   float* frames = nullptr; // [M][1280]
+  float* rowscale = nullptr;  // [M] per-frame scale of an fp8 operand (codec_dtype FP8: pwconv1's)
   int32_t* err = nullptr;  // = ArState.err + 1, the codec's own word: bit 4 a code outside [0, 4096), bit 8 the ISTFT envelope <= 1e-11
   int max_frames = 0;
 };

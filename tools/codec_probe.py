@@ -10,7 +10,9 @@ from llmvox_amd.engine import build_engine  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 dt = sys.argv[2] if len(sys.argv) > 2 else "bf16"
-e = build_engine(0, dt, dt, max_streams=32, max_positions=64, max_codec_frames=8192)
+# dtype "fp8": bf16 context with fp8 codec weights (configs[4])
+e = build_engine(0, "bf16" if dt == "fp8" else dt, "bf16" if dt == "fp8" else dt, max_streams=32, max_positions=64,
+                 max_codec_frames=8192, codec_dtype="fp8" if dt == "fp8" else None)
 opts = sys.argv[3] if len(sys.argv) > 3 else ""
 for kv in filter(None, opts.split(",")):
     k, v = kv.split("=")
