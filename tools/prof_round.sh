@@ -7,7 +7,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 export PYTHONPATH=.
-TAG=${TAG:-r04}
+TAG=${TAG:-r05}
 O=gpurun_out/$TAG; mkdir -p $O
 # PMC passes launch the steps one by one on the null stream (--null-stream): with the default
 # side-stream HIP-graph replay, rocprofv3 --pmc segfaults in its own thread (profiles/r03/pmc_segv_graph_replay.log);
