@@ -71,7 +71,10 @@ def test_deferred_select_matches_argmax_kernel(eng, B, slots, graphs, fuse_mlp):
     finally:
         eng.set_option("fuse_mlp", 1)
     if fuse_mlp == 0 or eng.weight_dtype == "fp32":  # no arrival-order sums on this path
+        live = [b for b, s in enumerate(slots) if s >= 0]  # (an idle row's logits are not outputs)
         for a, b, name in zip(got, ref, ["tokens", "margins", "rowstep", "positions", "logits"]):
+            if name == "logits":
+                a, b = a[live], b[live]
             np.testing.assert_array_equal(np.asarray(a), np.asarray(b), err_msg=name)
     else:
         # a near-tie may flip a token, and the stream diverges from there: compare up to the
@@ -140,7 +143,10 @@ def test_batched_deferred_select_matches_argmax_kernel(eng_batched, B):
         got = run()
     finally:
         e.set_option("defer_select", 1)
+    live = [b for b in range(B) if b != B // 2]  # the idle row's logits are whatever its garbage x gives
     for a, b, name in zip(got, ref, ["tokens", "margins", "rowstep", "positions", "logits"]):
+        if name == "logits":
+            a, b = a[live], b[live]
         np.testing.assert_array_equal(np.asarray(a), np.asarray(b), err_msg=name)
     n = sum(calls)
     assert got[2][B // 2] == 0 and (got[0][B // 2] == -7).all()
