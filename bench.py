@@ -385,7 +385,9 @@ def run_config3(args, eng, world, rank, local, dist):
     # read back, chunk c's codec on a second stream, each dump delivered when its codec call ends
     # (round 4's overlap delivered a chunk late: p50 first chunk 3.9-4.0 vs 1.33-1.36 ms);
     # --serial-codec: the serial scheduler
-    sched = FusedScheduler(eng, max_chunk=256, to_bytes=True, overlap=args.codec_overlap)
+    so = dict(kv.split("=") for kv in filter(None, args.sched.split(",")))  # (A/B knobs: tail=, thread=)
+    sched = FusedScheduler(eng, max_chunk=256, to_bytes=True, overlap=args.codec_overlap,
+                           tail=int(so.get("tail", 8)), deliver_thread=so.get("thread", "1") != "0")
     rng = np.random.default_rng(1234)  # rank 0 draws every rank's request texts
     pcm_bytes = [0]
 
@@ -973,6 +975,7 @@ def main():
     ap.add_argument("--graph-stream", action="store_true", help="(default) kept for old command lines")
     ap.add_argument("--ar-priority", action="store_true",
                     help="decode stream at high HIP queue priority (codec stream at the default)")
+    ap.add_argument("--sched", default="", help="configs[3] FusedScheduler A/B knobs: tail=N,thread=0|1")
     ap.add_argument("--null-stream", action="store_true",
                     help="run on torch's default (null) stream: the decode steps are launched kernel by kernel")
     ap.add_argument("--no-graphs", action="store_true",

@@ -440,18 +440,39 @@ class _Deliverer:
     codec event (if any), then hands its items to the streams, so a dump reaches its stream as soon
     as its codec call has finished, in the reference's per-stream order."""
 
-    def __init__(self):
+    def __init__(self, thread: bool = True):
         self.q: Queue = Queue()
         self.cv = threading.Condition()
         self.pending = 0
         self.error: Optional[BaseException] = None
-        self.thread = threading.Thread(target=self._run, name="lvx-deliver", daemon=True)
-        self.thread.start()
+        self.jobs: Deque = deque()  # poll mode (thread=False): jobs delivered by poll() / wait()
+        self.thread = None
+        if thread:
+            self.thread = threading.Thread(target=self._run, name="lvx-deliver", daemon=True)
+            self.thread.start()
 
     def put(self, event, fn):
+        if self.thread is None:
+            self.jobs.append((event, fn))
+            return
         with self.cv:
             self.pending += 1
         self.q.put((event, fn))
+
+    def poll(self, block: bool = False):
+        """Poll mode: deliver the jobs whose events have completed, in order (all of them if block)."""
+        while self.jobs:
+            ev, fn = self.jobs[0]
+            if ev is not None and not block and not ev.query():
+                return
+            self.jobs.popleft()
+            if ev is not None:
+                ev.synchronize()
+            try:
+                fn()
+            except BaseException as e:
+                if self.error is None:
+                    self.error = e
 
     def _run(self):
         while True:
@@ -470,6 +491,9 @@ class _Deliverer:
                 self.cv.notify_all()
 
     def wait(self):
+        if self.thread is None:
+            self.poll(block=True)
+            return
         with self.cv:
             while self.pending:
                 self.cv.wait()
@@ -480,7 +504,8 @@ class _Deliverer:
             raise e
 
     def close(self):
-        self.q.put((None, None))
+        if self.thread is not None:
+            self.q.put((None, None))
 
 
 class FusedScheduler:
@@ -521,7 +546,8 @@ class FusedScheduler:
     """
 
     def __init__(self, engine, max_chunk: int = 64, max_rows: Optional[int] = None, to_bytes: bool = True,
-                 overlap: bool = False, stop_rule=None, waiter=None, tail: int = 8, stream=None):
+                 overlap: bool = False, stop_rule=None, waiter=None, tail: int = 8, stream=None,
+                 deliver_thread: bool = True):
         import torch
         self.engine = engine
         self.torch = torch
@@ -542,7 +568,7 @@ class FusedScheduler:
         self.bufs = [self._alloc() for _ in range(2 if self.overlap else 1)]
         self._bi = 0
         self.inflight: Deque[_Chunk] = deque()
-        self.deliverer = _Deliverer() if self.overlap else None
+        self.deliverer = _Deliverer(deliver_thread) if self.overlap else None
 
     def _alloc(self):
         torch, dev = self.torch, self.engine.device
@@ -675,6 +701,8 @@ class FusedScheduler:
             self.waiter(ev)
         else:
             ev.synchronize()
+        if self.deliverer is not None and self.deliverer.thread is None:
+            self.deliverer.poll()
 
     # -- completion --------------------------------------------------------------------------
     def _chunk_error(self, ch):
@@ -763,6 +791,8 @@ class FusedScheduler:
         next chunk, then complete the one in flight before it (its items are delivered when its codec
         call ends). Returns the steps queued or completed (0 = idle: everything delivered)."""
         if self.deliverer is not None:
+            if self.deliverer.thread is None:
+                self.deliverer.poll()
             self.deliverer.take_error()
         launched = self._launch_next()
         if self.inflight and (len(self.inflight) > 1 or not launched or not self.overlap):
