@@ -1241,4 +1241,17 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if os.environ.get("LVX_PROFILE_DIR"):  # development: a cProfile of each rank's process (host time)
+        import cProfile
+        import pstats
+        d = os.environ["LVX_PROFILE_DIR"]
+        os.makedirs(d, exist_ok=True)
+        pr = cProfile.Profile()
+        try:
+            pr.runcall(main)
+        finally:
+            out = os.path.join(d, f"rank{os.environ.get('RANK', '0')}.txt")
+            with open(out, "w") as f:
+                pstats.Stats(pr, stream=f).sort_stats("tottime").print_stats(25)
+    else:
+        main()
