@@ -547,7 +547,7 @@ class FusedScheduler:
 
     def __init__(self, engine, max_chunk: int = 64, max_rows: Optional[int] = None, to_bytes: bool = True,
                  overlap: bool = False, stop_rule=None, waiter=None, tail: int = 8, stream=None,
-                 deliver_thread: bool = True):
+                 deliver_thread: bool = True, codec_stream: bool = True):
         import torch
         self.engine = engine
         self.torch = torch
@@ -563,7 +563,8 @@ class FusedScheduler:
         dev = engine.device
         self.cuda = torch.device(dev).type == "cuda"
         self.overlap = bool(overlap)
-        self.codec_stream = torch.cuda.Stream(device=dev) if (self.overlap and self.cuda) else None
+        self.codec_stream = (torch.cuda.Stream(device=dev) if codec_stream else (stream or torch.cuda.current_stream(dev))) \
+            if (self.overlap and self.cuda) else None
         self.take = self.cuda and hasattr(engine, "take_errors")
         self.bufs = [self._alloc() for _ in range(2 if self.overlap else 1)]
         self._bi = 0
