@@ -388,7 +388,7 @@ def run_config3(args, eng, world, rank, local, dist):
     so = dict(kv.split("=") for kv in filter(None, args.sched.split(",")))  # (A/B knobs: tail=, thread=)
     sched = FusedScheduler(eng, max_chunk=256, to_bytes=True, overlap=args.codec_overlap,
                            tail=int(so.get("tail", 8)), deliver_thread=so.get("thread", "1") != "0",
-                           codec_stream=so.get("cs", "1") != "0")
+                           codec_stream=so.get("cs", "1") != "0", mapped_io=so.get("zc", "0") != "0")
     rng = np.random.default_rng(1234)  # rank 0 draws every rank's request texts
     pcm_bytes = [0]
 

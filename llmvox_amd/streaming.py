@@ -547,7 +547,7 @@ class FusedScheduler:
 
     def __init__(self, engine, max_chunk: int = 64, max_rows: Optional[int] = None, to_bytes: bool = True,
                  overlap: bool = False, stop_rule=None, waiter=None, tail: int = 8, stream=None,
-                 deliver_thread: bool = True, codec_stream: bool = True):
+                 deliver_thread: bool = True, codec_stream: bool = True, mapped_io: bool = False):
         import torch
         self.engine = engine
         self.torch = torch
@@ -570,6 +570,9 @@ class FusedScheduler:
         self._bi = 0
         self.inflight: Deque[_Chunk] = deque()
         self.deliverer = _Deliverer(deliver_thread) if self.overlap else None
+        # mapped_io: the codec reads its codes from and writes its PCM / error bits to pinned host memory
+        # directly (no copies queued on the codec stream)
+        self.mapped_io = bool(mapped_io) and hasattr(engine, "decode_codes_mapped")
 
     def _alloc(self):
         torch, dev = self.torch, self.engine.device
@@ -870,18 +873,22 @@ class FusedScheduler:
         for g, (L, grp) in enumerate(groups):
             host = torch.empty(len(grp) * 320 * L, dtype=torch.float32, pin_memory=True)
             err_h = torch.zeros((1,), dtype=torch.int32, pin_memory=True)
+            codes = torch.tensor([dumps[i][1] for i in grp], dtype=torch.int32).pin_memory()
             with torch.cuda.stream(self.codec_stream):
-                codes = torch.tensor([dumps[i][1] for i in grp], dtype=torch.int32).pin_memory()
-                out = self.engine.decode_codes(codes.to(dev, non_blocking=True))
-                host.view(out.shape).copy_(out, non_blocking=True)
-                err_d = torch.zeros((1,), dtype=torch.int32, device=dev)
-                self.engine.take_errors(_lib.ERRW_CODEC, err_d)
-                err_h.copy_(err_d, non_blocking=True)
+                if self.mapped_io:
+                    self.engine.decode_codes_mapped(codes, host.view(len(grp), 320 * L))
+                    self.engine.take_errors(_lib.ERRW_CODEC, err_h)
+                else:
+                    out = self.engine.decode_codes(codes.to(dev, non_blocking=True))
+                    host.view(out.shape).copy_(out, non_blocking=True)
+                    err_d = torch.zeros((1,), dtype=torch.int32, device=dev)
+                    self.engine.take_errors(_lib.ERRW_CODEC, err_d)
+                    err_h.copy_(err_d, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(self.codec_stream)
             sts = [st for st in ready if last[st] == g]
 
-            def deliver(host=host, err_h=err_h, grp=grp, L=L, sts=sts):
+            def deliver(host=host, err_h=err_h, grp=grp, L=L, sts=sts, codes=codes):  # (codes: kept alive)
                 _lib.check_bits(int(err_h[0]))
                 for k, i in enumerate(grp):
                     a = host[k * 320 * L:(k + 1) * 320 * L].numpy()
