@@ -974,9 +974,9 @@ def main():
     ap.add_argument("--serial-codec", action="store_true",
                     help="the codec after each chunk's AR on the same stream (no overlap)")
     ap.add_argument("--graph-stream", action="store_true", help="(default) kept for old command lines")
-    ap.add_argument("--ar-priority", action="store_true",
-                    help="decode stream at high HIP queue priority (codec stream at the default)")
-    ap.add_argument("--sched", default="", help="configs[3] FusedScheduler A/B knobs: tail=N,thread=0|1")
+    ap.add_argument("--sched", default="",
+                    help="configs[3] FusedScheduler A/B knobs: tail=N, thread=0|1 (delivery thread), cs=0|1 "
+                         "(codec on its own stream), zc=0|1 (codec I/O in mapped pinned memory)")
     ap.add_argument("--null-stream", action="store_true",
                     help="run on torch's default (null) stream: the decode steps are launched kernel by kernel")
     ap.add_argument("--no-graphs", action="store_true",
@@ -1058,9 +1058,9 @@ def main():
         # steadier (configs[2] 224.6 / 224.7k vs 218.7 / 223.7k; configs[1] 12.8 / 13.0k vs 12.2 /
         # 12.9k), and launched steps swing with host load (B = 8: 107-180 vs 99-104 us/step,
         # tools/step_sweep.py): the host no longer paces the step.
-        # --ar-priority: the decode stream at high queue priority (the codec stream keeps the default),
-        # so the dispatcher favours the latency-bound step's workgroups over the codec's beside it
-        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1 if args.ar_priority else 0))
+        # (round 5: the decode stream at high queue priority, the codec's at the default, measured the
+        # same: 234.5 / 235.6 / 235.3k vs 235.4 / 235.7 / 233.7k tok/s, profiles/r05/priority_ab.txt)
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     if args.config == 3:
         return run_config3(args, eng, world, rank, local, dist)
 

@@ -21,7 +21,7 @@ timeout -k 10 300 python bench.py --config 4 --seconds 60 --no-cpu-baseline --no
 line $O/cfg4_60s.jsonl
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu-baseline --no-probe --dist-backend gloo > $O/dist2.jsonl 2> $O/dist2.err || { tail -5 $O/dist2.err; exit 1; }
 line $O/dist2.jsonl
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --config 3 --steps 1 --warmup 1 --no-cpu-baseline --no-probe --dist-backend gloo > $O/dist2_c3.jsonl 2> $O/dist2_c3.err || { tail -5 $O/dist2_c3.err; exit 1; }
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --config 3 --steps 1 --warmup 1 --no-cpu-baseline --no-probe --dist-backend gloo --sched cs=0 > $O/dist2_c3.jsonl 2> $O/dist2_c3.err || { tail -5 $O/dist2_c3.err; exit 1; }
 line $O/dist2_c3.jsonl
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE -d $O/pmcpar -o run --output-format csv -- python3 bench.py --steps 4 --no-cpu-baseline --null-stream > $O/pmc_parity.log 2>&1
