@@ -103,7 +103,6 @@ struct GemvArgs {
                          // 2: batched step, the next step's embedding rows kernel reduces the logits
   int xmap;              // ar_mfma2_kernel launched as a 1-D grid with the XCD-aligned tile order:
                          // 1 = mlp c_proj (K slice = XCD mod 4), 2 = c_proj batch tiles (tile = XCD mod 2)
-  int nsm;               // ar_f32b_kernel IN 2: the attention's KV splits at this B (0: attn_ns_max's count)
 };
 
 // ---------------------------------------------------------------------------------
@@ -2351,7 +2350,6 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_f32b_kernel(GemvArgs a) {
     // of the sum changes no bit, and at B = 32 (one split) it cuts the block's partial reads 16-fold
     int nsm = NSPLIT;
     while (nsm > 1 && nsm * N_HEAD * B > 256) nsm >>= 1;
-    if (a.nsm) nsm = a.nsm;
     for (int q = tid; q < R * N_HEAD; q += NTH) {
       const int bb = q / N_HEAD, head = q - bb * N_HEAD, b = min(r0 + bb, B - 1);
       const int4 ri = a.st.rowinfo[b];
@@ -2706,8 +2704,6 @@ static bool use_f32b(int B) {
 // lm_head folds them into x and leaves the LayerNorm'd fp32 rows the GEMM stages (IN 6). Option exp
 // bit 512: the unsplit mlp c_proj with x final at every boundary and the LayerNorm in the GEMM prologue.
 static bool f32b_qsplit(int B) { return !(opts().exp & 512) && B <= 32 && !(opts().exp & 1024); }
-// KV splits of the fp32 attention: enough to fill the chip; option exp bit 8192 (A/B): two where that is one
-static int f32b_ns(int B) { return ((opts().exp & 8192) && attn_ns_max(B) == 1) ? 2 : attn_ns_max(B); }
 static void launch_op_f32b(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtype, int B, hipStream_t s) {
   const bool ksp = !(opts().exp & 512);
   a.layer = l;
@@ -2734,11 +2730,10 @@ static void launch_op_f32b(int op, GemvArgs& a, const ArWeights& w, int l, int k
         launch_f32b<768, 0, 0>(a, s);
       }
       break;
-    case 1: launch_attn(a.st, kvdtype, B, l, s, f32b_ns(B), f32b_ns(B) == 1 ? 3 : 0, 0, qsp); break;
+    case 1: launch_attn(a.st, kvdtype, B, l, s, attn_ns_max(B), attn_ns_max(B) == 1 ? 3 : 0, 0, qsp); break;
     case 2:
       a.W = w.w_aproj[l]; a.Wf = w.f_aproj[l]; a.N = D;
-      a.nsm = f32b_ns(B);
-      if (f32b_ns(B) == 1) launch_f32b<768, 4, 1>(a, s);  // the attention wrote the rows (direct 3)
+      if (attn_ns_max(B) == 1) launch_f32b<768, 4, 1>(a, s);  // the attention wrote the rows (direct 3)
       else launch_f32b<768, 2, 1>(a, s);
       break;
     case 3: a.W = w.w_fc[l]; a.Wf = w.f_fc[l]; a.N = DFF; a.ln_w = w.ln2[l]; launch_f32b<768, 0, 2>(a, s); break;
