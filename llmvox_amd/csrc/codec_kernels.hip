@@ -1052,10 +1052,9 @@ static void g3_launch(GemmArgs g, hipStream_t s) {
   // more tiles than CUs: two blocks per CU (2 stages, 80 KB each), else one (3 stages, 120 KB).
   // Kernel traces of the 32 x 256-frame decode: N = 2,304 (768 tiles) 52.5 vs 61 us, N = 768 (256
   // tiles) 40.4 vs 47 us; 16 x 256 frames (N = 2,304: 384 tiles) 1.57 vs 1.70 ms per decode
-  // (codec_exp bit 64, A/B: one block per CU at any tile count, 40 KB of LDS left to the decode kernels
-  // running beside the codec)
-  if (grid.x * grid.y > 256 && !(opts().codec_exp & 64))
-    hipLaunchKernelGGL((gemm_glds_kernel<AMODE, EPI, TC, 2, TA, SPLIT>), grid, dim3(512), 0, s, g);
+  // (round 5: one block per CU at any tile count, leaving 40 KB of LDS to the decode kernels beside the
+  // codec, measured the same: configs[2] 235.0 / 235.5 / 235.7k vs 235.1 / 234.4 / 235.2k tok/s)
+  if (grid.x * grid.y > 256) hipLaunchKernelGGL((gemm_glds_kernel<AMODE, EPI, TC, 2, TA, SPLIT>), grid, dim3(512), 0, s, g);
   else hipLaunchKernelGGL((gemm_glds_kernel<AMODE, EPI, TC, 3, TA, SPLIT>), grid, dim3(512), 0, s, g);
 }
 
