@@ -682,10 +682,13 @@ class FusedScheduler:
         args = (buf["slots_d"][:B], buf["plan_d"][:B], buf["rowstep_d"][:B], buf["tok_d"][:B])
         near = None
         if self.overlap and self.cuda and n >= 2 * self.tail:  # (a short chunk is planned behind at once)
-            self.engine.ar_steps(n - self.tail, *args)
+            # the head a whole number of 16-step graph replays (lvx_ar_steps replays 16-step graphs and
+            # single steps for the rest): the split adds no single-step replays
+            head = max(16, (n - self.tail) // 16 * 16) if n - self.tail >= 16 else n - self.tail
+            self.engine.ar_steps(head, *args)
             near = torch.cuda.Event()
             near.record(torch.cuda.current_stream(self.engine.device))
-            self.engine.ar_steps(self.tail, *args)
+            self.engine.ar_steps(n - head, *args)
         else:
             self.engine.ar_steps(n, *args)
         ev = None
