@@ -388,7 +388,8 @@ def run_config3(args, eng, world, rank, local, dist):
     so = dict(kv.split("=") for kv in filter(None, args.sched.split(",")))  # (A/B knobs: tail=, thread=)
     sched = FusedScheduler(eng, max_chunk=256, to_bytes=True, overlap=args.codec_overlap,
                            tail=int(so.get("tail", 8)), deliver_thread=so.get("thread", "1") != "0",
-                           codec_stream=so.get("cs", "1") != "0", mapped_io=so.get("zc", "0") != "0")
+                           codec_stream=so.get("cs", "1") != "0", mapped_io=so.get("zc", "0") != "0",
+                           stream=torch.cuda.Stream(device=dev, priority=-1) if so.get("hp") == "1" else None)
     rng = np.random.default_rng(1234)  # rank 0 draws every rank's request texts
     pcm_bytes = [0]
 
@@ -976,7 +977,7 @@ def main():
     ap.add_argument("--graph-stream", action="store_true", help="(default) kept for old command lines")
     ap.add_argument("--sched", default="",
                     help="configs[3] FusedScheduler A/B knobs: tail=N, thread=0|1 (delivery thread), cs=0|1 "
-                         "(codec on its own stream), zc=0|1 (codec I/O in mapped pinned memory)")
+                         "(codec on its own stream), zc=0|1 (codec I/O in mapped pinned memory), hp=1 (decode stream at high priority)")
     ap.add_argument("--null-stream", action="store_true",
                     help="run on torch's default (null) stream: the decode steps are launched kernel by kernel")
     ap.add_argument("--no-graphs", action="store_true",
