@@ -1063,7 +1063,10 @@ def main():
         # same: 234.5 / 235.6 / 235.3k vs 235.4 / 235.7 / 233.7k tok/s, profiles/r05/priority_ab.txt)
         torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     if args.config == 3:
-        return run_config3(args, eng, world, rank, local, dist)
+        try:
+            return run_config3(args, eng, world, rank, local, dist)
+        finally:
+            _release(eng)
 
     # ---- text plans: stream 0 of rank 0 opens with the config sentence; every other utterance is a
     # seeded random sentence; utterances back to back per stream
@@ -1240,6 +1243,15 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    _release(eng)
+
+
+def _release(eng):
+    """Free the library context (its graphs, streams, device memory) while the HIP runtime is fully
+    up: left to the garbage collector at interpreter exit, lvx_destroy can run during the runtime's own
+    teardown."""
+    torch.cuda.synchronize()
+    eng.close()
 
 
 if __name__ == "__main__":

@@ -16,10 +16,12 @@ Two layers:
 from __future__ import annotations
 
 import asyncio
+import atexit
 import contextlib
 import copy
 import re
 import threading
+import weakref
 from collections import deque
 from dataclasses import dataclass, field
 from queue import Empty, Queue
@@ -435,6 +437,18 @@ class _Chunk:
         self.bad = set()
 
 
+_LIVE_DELIVERERS: "weakref.WeakSet" = weakref.WeakSet()
+
+
+@atexit.register
+def _close_deliverers():
+    """Stop every delivery thread before the interpreter finalises: a daemon thread still inside a
+    GIL-releasing torch call (Event.synchronize) when finalisation reclaims it unwinds through a C++
+    destructor and the process aborts ("terminate called without an active exception")."""
+    for d in list(_LIVE_DELIVERERS):
+        d.close()
+
+
 class _Deliverer:
     """The overlapped scheduler's delivery thread: jobs run in submission order; each waits for its
     codec event (if any), then hands its items to the streams, so a dump reaches its stream as soon
@@ -450,6 +464,7 @@ class _Deliverer:
         if thread:
             self.thread = threading.Thread(target=self._run, name="lvx-deliver", daemon=True)
             self.thread.start()
+            _LIVE_DELIVERERS.add(self)
 
     def put(self, event, fn):
         if self.thread is None:
@@ -504,8 +519,10 @@ class _Deliverer:
             raise e
 
     def close(self):
-        if self.thread is not None:
+        if self.thread is not None and self.thread.is_alive():
             self.q.put((None, None))
+            self.thread.join(timeout=30)
+        _LIVE_DELIVERERS.discard(self)
 
 
 class FusedScheduler:
