@@ -156,19 +156,6 @@ class Engine:
                                                    self.stream_handle()))
         return pcm
 
-    def decode_codes_mapped(self, codes: torch.Tensor, pcm: torch.Tensor, bandwidth_id: int = 0):
-        """decode_codes with caller-owned operands that may live in pinned (device-mapped) host memory:
-        int32 codes [B, L] in, f32 PCM [B, 320 L] out, read / written by the kernels themselves (no copy
-        on the stream). The caller keeps both alive until the call's work on the stream is done."""
-        B, L = codes.shape
-        if codes.dtype != torch.int32 or not codes.is_contiguous() or pcm.dtype != torch.float32 or \
-                pcm.numel() != B * 320 * L or not pcm.is_contiguous():
-            raise ValueError("codes int32 [B, L] and pcm float32 [B, 320 L], contiguous")
-        if codes.device.type == "cpu" and not codes.is_pinned() or pcm.device.type == "cpu" and not pcm.is_pinned():
-            raise ValueError("host operands must be pinned (device-mapped)")
-        _lib.check(self.lib.lvx_codec_decode_codes(self.h, _ptr(codes), B, L, int(bandwidth_id), _ptr(pcm),
-                                                   self.stream_handle()))
-
     def close(self):
         if getattr(self, "h", None):
             self.lib.lvx_destroy(self.h)

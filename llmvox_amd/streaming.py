@@ -454,40 +454,19 @@ class _Deliverer:
     codec event (if any), then hands its items to the streams, so a dump reaches its stream as soon
     as its codec call has finished, in the reference's per-stream order."""
 
-    def __init__(self, thread: bool = True):
+    def __init__(self):
         self.q: Queue = Queue()
         self.cv = threading.Condition()
         self.pending = 0
         self.error: Optional[BaseException] = None
-        self.jobs: Deque = deque()  # poll mode (thread=False): jobs delivered by poll() / wait()
-        self.thread = None
-        if thread:
-            self.thread = threading.Thread(target=self._run, name="lvx-deliver", daemon=True)
-            self.thread.start()
-            _LIVE_DELIVERERS.add(self)
+        self.thread = threading.Thread(target=self._run, name="lvx-deliver", daemon=True)
+        self.thread.start()
+        _LIVE_DELIVERERS.add(self)
 
     def put(self, event, fn):
-        if self.thread is None:
-            self.jobs.append((event, fn))
-            return
         with self.cv:
             self.pending += 1
         self.q.put((event, fn))
-
-    def poll(self, block: bool = False):
-        """Poll mode: deliver the jobs whose events have completed, in order (all of them if block)."""
-        while self.jobs:
-            ev, fn = self.jobs[0]
-            if ev is not None and not block and not ev.query():
-                return
-            self.jobs.popleft()
-            if ev is not None:
-                ev.synchronize()
-            try:
-                fn()
-            except BaseException as e:
-                if self.error is None:
-                    self.error = e
 
     def _run(self):
         while True:
@@ -506,9 +485,6 @@ class _Deliverer:
                 self.cv.notify_all()
 
     def wait(self):
-        if self.thread is None:
-            self.poll(block=True)
-            return
         with self.cv:
             while self.pending:
                 self.cv.wait()
@@ -519,7 +495,7 @@ class _Deliverer:
             raise e
 
     def close(self):
-        if self.thread is not None and self.thread.is_alive():
+        if self.thread.is_alive():
             self.q.put((None, None))
             self.thread.join(timeout=30)
         _LIVE_DELIVERERS.discard(self)
@@ -564,7 +540,7 @@ class FusedScheduler:
 
     def __init__(self, engine, max_chunk: int = 64, max_rows: Optional[int] = None, to_bytes: bool = True,
                  overlap: bool = False, stop_rule=None, waiter=None, tail: int = 8, stream=None,
-                 deliver_thread: bool = True, codec_stream: bool = True, mapped_io: bool = False):
+                 codec_stream: bool = True):
         import torch
         self.engine = engine
         self.torch = torch
@@ -586,10 +562,7 @@ class FusedScheduler:
         self.bufs = [self._alloc() for _ in range(2 if self.overlap else 1)]
         self._bi = 0
         self.inflight: Deque[_Chunk] = deque()
-        self.deliverer = _Deliverer(deliver_thread) if self.overlap else None
-        # mapped_io: the codec reads its codes from and writes its PCM / error bits to pinned host memory
-        # directly (no copies queued on the codec stream)
-        self.mapped_io = bool(mapped_io) and hasattr(engine, "decode_codes_mapped")
+        self.deliverer = _Deliverer() if self.overlap else None
 
     def _alloc(self):
         torch, dev = self.torch, self.engine.device
@@ -725,8 +698,6 @@ class FusedScheduler:
             self.waiter(ev)
         else:
             ev.synchronize()
-        if self.deliverer is not None and self.deliverer.thread is None:
-            self.deliverer.poll()
 
     # -- completion --------------------------------------------------------------------------
     def _chunk_error(self, ch):
@@ -815,8 +786,6 @@ class FusedScheduler:
         next chunk, then complete the one in flight before it (its items are delivered when its codec
         call ends). Returns the steps queued or completed (0 = idle: everything delivered)."""
         if self.deliverer is not None:
-            if self.deliverer.thread is None:
-                self.deliverer.poll()
             self.deliverer.take_error()
         launched = self._launch_next()
         if self.inflight and (len(self.inflight) > 1 or not launched or not self.overlap):
@@ -895,15 +864,11 @@ class FusedScheduler:
             err_h = torch.zeros((1,), dtype=torch.int32, pin_memory=True)
             codes = torch.tensor([dumps[i][1] for i in grp], dtype=torch.int32).pin_memory()
             with torch.cuda.stream(self.codec_stream):
-                if self.mapped_io:
-                    self.engine.decode_codes_mapped(codes, host.view(len(grp), 320 * L))
-                    self.engine.take_errors(_lib.ERRW_CODEC, err_h)
-                else:
-                    out = self.engine.decode_codes(codes.to(dev, non_blocking=True))
-                    host.view(out.shape).copy_(out, non_blocking=True)
-                    err_d = torch.zeros((1,), dtype=torch.int32, device=dev)
-                    self.engine.take_errors(_lib.ERRW_CODEC, err_d)
-                    err_h.copy_(err_d, non_blocking=True)
+                out = self.engine.decode_codes(codes.to(dev, non_blocking=True))
+                host.view(out.shape).copy_(out, non_blocking=True)
+                err_d = torch.zeros((1,), dtype=torch.int32, device=dev)
+                self.engine.take_errors(_lib.ERRW_CODEC, err_d)
+                err_h.copy_(err_d, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(self.codec_stream)
             sts = [st for st in ready if last[st] == g]
