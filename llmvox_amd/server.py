@@ -152,8 +152,9 @@ class _Worker:
                 with self.lock:
                     live = [s for s in self.sessions if not s.done]
                     edge_streams = getattr(e, "streams", None) or []
-                    edge = [s for s in live if any(st in edge_streams for st in s.streams)]
-                    for s in edge or live:
+                    # the sessions of the named streams only; an error naming no stream ends them all
+                    edge = [s for s in live if any(st in edge_streams for st in s.streams)] if edge_streams else live
+                    for s in edge:
                         self.end(s, error=e)
             except BaseException as e:  # this device is out of service: its requests end with the error
                 with self.lock:

@@ -726,6 +726,7 @@ class FusedScheduler:
         # range error (B <= 2) invalidates the logits of this chunk's rows: they are named the same way
         from ._lib import LvxCapacityError, LvxNumericError
         edge, at_cap = set(), set()
+        live = [st for st in ch.ready if st in self.streams and st not in ch.bad]  # (rows still consumed)
         if err is not None:
             if isinstance(err, LvxCapacityError):
                 # a row that ran past max_positions had its last positions clamped: those tokens are
@@ -733,14 +734,17 @@ class FusedScheduler:
                 # its last step, but all n of its tokens came from positions <= max_positions - 1:
                 # they are consumed below, then the row is reported at capacity
                 P = self.engine.max_positions
-                edge = {st for st in ch.ready if st.m.position + n > P}
-                at_cap = {st for st in ch.ready if st.m.position + n == P}
-                if not edge and not at_cap:  # not a position overflow of a known row (a plan overrun)
+                bits = getattr(err, "bits", 0) or 0  # (device bits: 1 KV capacity, 2 a plan overrun)
+                if bits & 2 or not any(st.m.position + n >= P for st in ch.ready):  # not a row at the edge
                     raise err
+                edge = {st for st in live if st.m.position + n > P}
+                at_cap = {st for st in live if st.m.position + n == P}
             elif isinstance(err, LvxNumericError):
-                edge = set(ch.ready)
+                edge = set(live)
             else:
                 raise err
+            # (an error of rows already discarded -- a closed stream, a run-ahead row rolled back --
+            # concerns no live stream: nothing is raised for it below)
         dumps = []  # (stream, tokens)
         order: Dict[FusedStream, List[tuple]] = {st: [] for st in ch.ready}
         ended = set()
@@ -777,7 +781,7 @@ class FusedScheduler:
             if self.deliverer is not None:
                 self.deliverer.wait()
             err.streams = sorted(edge | at_cap, key=lambda st: st.slot)
-            if err.streams or not isinstance(err, LvxCapacityError):
+            if err.streams:
                 raise err
         return n
 

@@ -192,3 +192,33 @@ def test_tts_two_replica_order_matches_reference_consumers(handler, mode):
     got, ref = np.frombuffer(body, dtype=np.float32), np.frombuffer(want, dtype=np.float32)
     assert got.shape == ref.shape and got.size > 0
     assert np.abs(got - ref).max() < 1e-5
+
+
+@pytest.mark.gpu
+def test_numeric_error_ends_only_the_request():
+    """the B <= 2 fused MLP's range check (error bit 32: a non-finite partial) used to reach
+    the service as a device failure, taking every session on the GPU down. It is now raised as
+    LvxNumericError naming the rows of that chunk; the service ends those requests and stays in
+    service. A NaN planted in one c_fc weight row makes every step's partials non-finite."""
+    import numpy as np
+    from llmvox_amd import weights as LW
+    from llmvox_amd._lib import LvxNumericError
+    from llmvox_amd.engine import build_engine
+    from llmvox_amd.server import TTSService
+    gw, cw, tt = LW.synthetic_all(1234)
+    w = np.array(gw["transformer.h.1.mlp.c_fc.weight"], dtype=np.float32, copy=True)
+    w[7, 3] = np.nan
+    gw["transformer.h.1.mlp.c_fc.weight"] = w
+    eng = build_engine(0, "bf16", "bf16", max_streams=4, max_positions=512, max_codec_frames=1280,
+                       weights=(gw, cw, tt))
+    svc = TTSService(eng, max_chunk=16, max_tokens=64)
+    try:
+        for _ in range(2):  # the service keeps serving (and failing) requests: the device stays in service
+            s = svc.submit("Hello there.")
+            with pytest.raises(RuntimeError) as ei:
+                b"".join(svc.chunks(s, timeout=0.01))
+            assert isinstance(ei.value.__cause__, LvxNumericError), repr(ei.value.__cause__)
+            assert svc.error is None and svc.workers[0].error is None
+    finally:
+        svc.shutdown()
+        eng.close()
