@@ -212,3 +212,23 @@ def test_fp8_codec_against_reference_pcm(eng_fp8, L):
         res[name] = _golden_rel(pcm[0], g, f"pcm_{L}")
     print(f"fp8 codec vs reference PCM, L = {L} in a batch of {k}: rel RMS {res}")
     assert res["w8a8_mfma"] < 0.12 and res["w8a16"] < 0.08
+
+
+def test_bf16_codec_at_the_bench_kernels_against_reference_pcm():
+    """The bf16 codec on the kernels of the bench's batched decode (gemm_glds at two blocks per CU: >
+    256 tiles) against the REFERENCE's PCM directly (codec_large_golden.npz), not only against the HIP
+    fp32 engine: six copies of the reference's 1,280-frame dump in one call (7,680 frames,
+    720 pwconv1 tiles), every stream within 2 % relative RMS of the reference's samples."""
+    from llmvox_amd.engine import build_engine
+    g = np.load(os.path.join(GOLDEN, "codec_large_golden.npz"))
+    e16 = build_engine(0, "bf16", "bf16", max_streams=2, max_positions=64, max_codec_frames=6 * 1280)
+    try:
+        codes = torch.from_numpy(np.repeat(g["codes_1280"], 6, axis=0)).to(e16.device)
+        pcm = e16.decode_codes(codes).cpu().numpy()
+    finally:
+        e16.close()
+    for b in range(1, 6):
+        assert np.array_equal(pcm[b], pcm[0])
+    rel = _golden_rel(pcm[0], g, "pcm_1280")
+    print(f"bf16 codec (7,680-frame call) vs reference PCM: rel RMS {rel:.4f}")
+    assert rel < 0.02
