@@ -2277,10 +2277,13 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_bt_kernel(GemvArgs a) {
 // 768, each slice's partial stored to its pending copy (st.yacc), folded into x by the rows kernel
 // (ar_rows_kernel<5>) that normalises c_attn's / lm_head's operand rows (IN 6): 4x the blocks, a
 // quarter of the bytes per block.
-template <int K, int NT, int IN, int OUT, int KTOT = K>
-__global__ __launch_bounds__(K / 192 * 64) void ar_f32b_kernel(GemvArgs a) {
-  constexpr int NW = K / 192, R = NT * 16, NTH = NW * 64;
-  constexpr bool STAGE = IN != 1;  // K == 768: the operand tile in LDS
+// CT column tiles per block (CT x K / 192 waves sharing the block's operand tile): CT = 2 halves the
+// blocks of the wide ops (c_fc, lm_head, the mlp c_proj slices) so that 192-256 blocks cover the CUs
+// once instead of 384-512 blocks loading two tiles' bytes on some CUs. Same bits either way.
+template <int K, int NT, int IN, int OUT, int KTOT = K, int CT = 1>
+__global__ __launch_bounds__(K / 192 * 64 * CT) void ar_f32b_kernel(GemvArgs a) {
+  constexpr int NWK = K / 192, NW = NWK * CT, R = NT * 16, NTH = NW * 64;
+  constexpr bool STAGE = IN != 1 || CT > 1;  // K == 768: the operand tile in LDS (shared by the column tiles)
   static_assert(KTOT == K || (IN == 1 && OUT == 6 && KTOT == YCOPIES * K), "split K: mlp c_proj into the pending copies");
   // IN 4 (c_proj after a one-split attention, direct == 3): the normalised rows are split 0 of part_o
   // IN 6 (c_attn / lm_head after ar_rows_kernel<5>): the LayerNorm'd fp32 rows in st.h
@@ -2290,11 +2293,13 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_f32b_kernel(GemvArgs a) {
   __shared__ float red[NW][16 * R];
   __shared__ float cf_s[IN == 2 ? R * N_HEAD * NSPLIT : 1];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int n0 = blockIdx.x * 16, r0 = blockIdx.y * R, ks = KTOT > K ? blockIdx.z : 0;
+  const int kw = wave % NWK;  // the wave's 192-wide K slice; wave / NWK its column tile
+  const int nb = blockIdx.x * CT * 16, r0 = blockIdx.y * R, ks = KTOT > K ? blockIdx.z : 0;
+  const int n0 = min(nb + (wave / NWK) * 16, a.N - 16);  // (a tile past N: the last one's weights, never stored)
   const int B = a.B;
   // weights (fragment-packed, the wave's 12 contiguous KB), issued first for IN 1 / IN 2; behind the
   // first row inputs for the LayerNorm modes (their statistics then overlap the weight stream)
-  const float4* wsrc = reinterpret_cast<const float4*>(a.Wf) + ((size_t)(n0 >> 4) * (KTOT / 16) + ks * (K / 16) + wave * 12) * 64 + lane;
+  const float4* wsrc = reinterpret_cast<const float4*>(a.Wf) + ((size_t)(n0 >> 4) * (KTOT / 16) + ks * (K / 16) + kw * 12) * 64 + lane;
   float4 wf[12];
   if constexpr (IN == 1 || IN == 2 || IN == 4 || IN == 6) {
 #pragma unroll
@@ -2415,16 +2420,16 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_f32b_kernel(GemvArgs a) {
       const int e = (tid + i * NTH) * 4, bb = e / D, c = e - bb * D;
       *reinterpret_cast<float4*>(xs + bb * LDX + c) = rv[i];
     }
-  } else if constexpr (IN == 6) {
-    // the rows kernel's LayerNorm'd rows, 16 B per thread and load, all in flight (padded rows:
-    // row B-1, never stored)
+  } else if constexpr (IN == 6 || (IN == 1 && STAGE)) {
+    // the rows kernel's LayerNorm'd rows (IN 6), or the K slice of the h rows (IN 1, two column
+    // tiles), 16 B per thread and load, all in flight (padded rows: row B-1, never stored)
     constexpr int NL = R * D / 4 / NTH;
     static_assert(R * D / 4 % NTH == 0, "whole float4 loads per thread");
     float4 rv[NL];
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int e = (tid + i * NTH) * 4, bb = e / D, c = e - bb * D;
-      rv[i] = *reinterpret_cast<const float4*>(a.st.h + (size_t)min(r0 + bb, B - 1) * D + c);
+      rv[i] = *reinterpret_cast<const float4*>(a.st.h + (size_t)min(r0 + bb, B - 1) * (IN == 1 ? KTOT : D) + (IN == 1 ? ks * K : 0) + c);
     }
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
@@ -2441,12 +2446,12 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_f32b_kernel(GemvArgs a) {
   for (int t = 0; t < NT; ++t) {
     float4 xf[12];
     if constexpr (STAGE) {
-      const float* xr = xs + (t * 16 + (lane & 15)) * LDX + wave * 192 + kq;
+      const float* xr = xs + (t * 16 + (lane & 15)) * LDX + kw * 192 + kq;
 #pragma unroll
       for (int j = 0; j < 12; ++j) xf[j] = *reinterpret_cast<const float4*>(xr + 16 * j);
     } else {
       const int b = min(r0 + t * 16 + (lane & 15), B - 1);  // padded columns recompute row B-1, never stored
-      const float* xr = a.st.h + (size_t)b * KTOT + ks * K + wave * 192 + kq;
+      const float* xr = a.st.h + (size_t)b * KTOT + ks * K + kw * 192 + kq;
 #pragma unroll
       for (int j = 0; j < 12; ++j) xf[j] = *reinterpret_cast<const float4*>(xr + 16 * j);
     }
@@ -2465,12 +2470,13 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_f32b_kernel(GemvArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) red[wave][(4 * (lane >> 4) + i) * R + t * 16 + (lane & 15)] = acc[t][i];
   __syncthreads();
-  for (int e = tid; e < 16 * R; e += NTH) {
-    const int r = e / R, c = e - r * R, n = n0 + r, b = r0 + c;
+  for (int e = tid; e < CT * 16 * R; e += NTH) {
+    const int ct = e / (16 * R), el = e - ct * (16 * R);
+    const int r = el / R, c = el - r * R, n = nb + ct * 16 + r, b = r0 + c;
     if (b >= B || n >= a.N) continue;
     float v = 0.f;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) v += red[w][e];
+    for (int w = 0; w < NWK; ++w) v += red[ct * NWK + w][el];
     if constexpr (OUT == 6) a.yacc[((size_t)b * YCOPIES + ks) * D + n] = v;  // K slice ks -> its pending copy
     else gemv_store<OUT>(a, n, b, v);
   }
@@ -2542,9 +2548,25 @@ __global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_qkv_ksplit_f32_kernel(
 template <int K, int IN, int OUT, int KTOT = K>
 static void launch_f32b(const GemvArgs& a, hipStream_t s) {
   const bool nt1 = a.B <= 16 || !(opts().exp & 8);
-  dim3 grid((a.N + 15) / 16, nt1 ? (a.B + 15) / 16 : (a.B + 31) / 32, KTOT / K), block(K / 192 * 64);
-  if (nt1) hipLaunchKernelGGL((ar_f32b_kernel<K, 1, IN, OUT, KTOT>), grid, block, 0, s, a);
-  else hipLaunchKernelGGL((ar_f32b_kernel<K, 2, IN, OUT, KTOT>), grid, block, 0, s, a);
+  const int nbr = nt1 ? (a.B + 15) / 16 : (a.B + 31) / 32;
+  // two column tiles per block when one per block would put more than 256 blocks on the chip
+  // (round 5, B = 32 t = 384-639: 200.9 vs 210.9 us/step, c_fc 7.58 -> 6.37 us, lm_head 7.27 -> 6.40,
+  // mlp c_proj with its h slice staged once per block; option exp bit 8192: one tile per block)
+  const bool ct2 = nt1 && K == 768 && (a.N / 16) * nbr * (KTOT / K) > 256 && !(opts().exp & 8192);
+  dim3 grid((a.N + 15) / 16, nbr, KTOT / K), block(K / 192 * 64);
+  if constexpr (K == 768) {
+    if (ct2) {
+      grid.x = (a.N + 31) / 32;
+      block.x *= 2;
+      hipLaunchKernelGGL((ar_f32b_kernel<K, 1, IN, OUT, KTOT, 2>), grid, block, 0, s, a);
+      return;
+    }
+  }
+  if (nt1) {
+    hipLaunchKernelGGL((ar_f32b_kernel<K, 1, IN, OUT, KTOT>), grid, block, 0, s, a);
+  } else {
+    hipLaunchKernelGGL((ar_f32b_kernel<K, 2, IN, OUT, KTOT>), grid, block, 0, s, a);
+  }
 }
 
 // Measured (round-1 sweep, us per step at positions 256-511): v3 saves kernels but every block

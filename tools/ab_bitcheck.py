@@ -1,13 +1,15 @@
 """Development check: an option A/B (lvx_set_option) must leave the decode bit-identical: tokens,
 margins and final logits of N steps from position 0, bf16 weights + bf16 KV.
-usage: python tools/ab_bitcheck.py OPT VALUE [B ...]"""
+usage: python tools/ab_bitcheck.py OPT VALUE [B ...]   (LVX_AB_W=fp32: fp32 weights + fp32 KV, the parity mode)"""
+import os
 import sys
 import torch
 from llmvox_amd.engine import build_engine
 
 opt, val = sys.argv[1], int(sys.argv[2])
 Bs = [int(x) for x in sys.argv[3:]] or [4, 16, 17, 24, 32]
-e = build_engine(0, "bf16", "bf16", max_streams=max(Bs), max_positions=1024, max_codec_frames=256)
+W = os.environ.get("LVX_AB_W", "bf16")
+e = build_engine(0, W, W, max_streams=max(Bs), max_positions=1024, max_codec_frames=256)
 e.set_option("fuse_mlp", 0)  # the fused MLP (B <= 2) adds with fp32 atomics: run-to-run noise
 dev = e.device
 n = 320
