@@ -2605,6 +2605,8 @@ static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_
   // t = 384-639 fp8 KV 103.9 vs 98.3 us/step, bf16 KV 109.6 vs 100.1)
   if (nw8 && !qkv && kvdtype == LVX_DTYPE_BF16)  // 8 waves, 128-key tiles: twice the KV bytes in flight per block
     hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2, 8>), grid, dim3(512), 0, s, st, l, ns_max, direct, selcopy);
+  // (round 5, measured slower: 3 / 4 fp8 KV tiles in flight per wave at B = 8, t = 384-639 99.2 / 100.1
+  // vs 98.0 us/step)
   else if (nw8 && !qkv && kvdtype == LVX_DTYPE_FP8)
     hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t, 2, 8>), grid, dim3(512), 0, s, st, l, ns_max, direct, selcopy);
   // (round 4, fp32 KV at B = 32, measured slower: 8 waves with 128-key tiles 212.6, 3 tiles in flight
