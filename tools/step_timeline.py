@@ -28,7 +28,7 @@ lib = _lib.load()
 lib.lvx_debug_timeline.restype = ctypes.c_int
 lib.lvx_debug_timeline.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
 
-e = build_engine(0, "bf16", "bf16", max_streams=B, max_positions=P0 + 512, max_codec_frames=256)
+e = build_engine(0, "bf16", os.environ.get("LVX_TL_KV", "bf16"), max_streams=B, max_positions=P0 + 512, max_codec_frames=256)  # LVX_TL_KV=fp8: configs[4]
 dev = e.device
 for kv in (sys.argv[4].split(",") if len(sys.argv) > 4 else []):
     k, v = kv.split("=")
