@@ -386,7 +386,7 @@ def run_config3(args, eng, world, rank, local, dist):
     # (round 4's overlap delivered a chunk late: p50 first chunk 3.9-4.0 vs 1.33-1.36 ms);
     # --serial-codec: the serial scheduler
     so = dict(kv.split("=") for kv in filter(None, args.sched.split(",")))
-    sched = FusedScheduler(eng, max_chunk=256, to_bytes=True, overlap=args.codec_overlap,
+    sched = FusedScheduler(eng, max_chunk=int(so.get("mc", 256)), to_bytes=True, overlap=args.codec_overlap,
                            tail=int(so.get("tail", 8)), codec_stream=so.get("cs", "1") != "0")
     rng = np.random.default_rng(1234)  # rank 0 draws every rank's request texts
     pcm_bytes = [0]
@@ -982,7 +982,7 @@ def main():
                     help="the codec after each chunk's AR on the same stream (no overlap)")
     ap.add_argument("--graph-stream", action="store_true", help="(default) kept for old command lines")
     ap.add_argument("--sched", default="",
-                    help="configs[3] FusedScheduler knobs: tail=N (steps after the planning event), cs=0 "
+                    help="configs[3] FusedScheduler knobs: tail=N (steps after the planning event), mc=N (max chunk), cs=0 "
                          "(the codec on the decode stream: 2 processes sharing one card, DESIGN 4)")
     ap.add_argument("--null-stream", action="store_true",
                     help="run on torch's default (null) stream: the decode steps are launched kernel by kernel")
