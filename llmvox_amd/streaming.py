@@ -672,9 +672,11 @@ class FusedScheduler:
         args = (buf["slots_d"][:B], buf["plan_d"][:B], buf["rowstep_d"][:B], buf["tok_d"][:B])
         near = None
         if self.overlap and self.cuda and n >= 2 * self.tail:  # (a short chunk is planned behind at once)
-            # the head a whole number of 16-step graph replays (lvx_ar_steps replays 16-step graphs and
-            # single steps for the rest): the split adds no single-step replays
-            head = max(16, (n - self.tail) // 16 * 16) if n - self.tail >= 16 else n - self.tail
+            # (round 5, measured worse: the head rounded down to whole 16-step graph replays moved the
+            # planning point up to 16 steps before the chunk's end, and a request arriving in that window
+            # waits for the whole next chunk: loaded first chunk p50 11.2 / 13.8 vs 9.0 / 10.2 ms,
+            # tools/latency_ab.py 32)
+            head = n - self.tail
             self.engine.ar_steps(head, *args)
             near = torch.cuda.Event()
             near.record(torch.cuda.current_stream(self.engine.device))
