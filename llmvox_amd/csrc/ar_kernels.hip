@@ -2487,7 +2487,9 @@ __global__ __launch_bounds__(K / 192 * 64 * CT) void ar_f32b_kernel(GemvArgs a) 
 // fragment-packed fp32 weights) and stages the slice of the rows kernel's LayerNorm'd fp32 rows (st.h,
 // NT * 16 x 192) once in LDS for its 4 waves; each wave stores its 16 x (NT * 16) partial to
 // st.qkvp[slice]; the attention (ar_attn_v2_kernel<float, ..., QKV>) sums the four slices in slice
-// order and appends the new key. 144 blocks of 48 + 24 KB instead of 144 of 48 + 96 KB.
+// order and appends the new key. 144 blocks of 48 + 24 KB instead of 144 of 48 + 96 KB. (Round 5,
+// measured slower: 8-wave blocks whose two wave groups each multiply one of the two 16-row tiles, a
+// 48-MFMA chain per wave instead of 96: B = 32 fp32 203.8 vs 201.4 us/step, bit-identical.)
 template <int NT>
 __global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_qkv_ksplit_f32_kernel(GemvArgs a) {
   constexpr int XR = NT * 16, XS = 196;  // rows, fp32 row stride (784 B: 16 rows 4 banks apart)
