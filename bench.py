@@ -1275,5 +1275,6 @@ if __name__ == "__main__":
             out = os.path.join(d, f"rank{os.environ.get('RANK', '0')}.txt")
             with open(out, "w") as f:
                 pstats.Stats(pr, stream=f).sort_stats("tottime").print_stats(25)
+                pstats.Stats(pr, stream=f).sort_stats("cumulative").print_stats(45)
     else:
         main()
