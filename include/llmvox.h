@@ -161,9 +161,10 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
  * an option set on one context never changes another context's kernels; each call binds a snapshot
  * of its context's options, and the context drops its captured graphs on its next call after a
  * change). Defaults are the measured-faster variants:
- *   "defer_select" 1: the greedy select is committed by the next step's first kernel (B <= 2: c_attn
- *                     layer 0 reduces lm_head's granules; B >= 4: ar_embed_select); 0: ar_argmax_kernel
- *                     after every lm_head (bit-identical results: tests/test_gpu_select.py);
+ *   "defer_select" 1: the greedy select is committed by the next step's first kernel (B <= 2 and
+ *                     4 <= B <= 8: c_attn layer 0 reduces lm_head's granules; larger B: ar_embed_select);
+ *                     2: as 1 but 4 <= B <= 8 through ar_embed_select; 0: ar_argmax_kernel after every
+ *                     lm_head (bit-identical results: tests/test_gpu_select.py);
  *   "fuse_mlp"     1: bf16, B <= 2: c_fc + gelu + mlp c_proj in one kernel (2^-32 fixed-point int64
  *                     atomics: exact sums, reproducible run to run); 0: the two GEMV kernels;
  *   "bt"           1: batched path v3 for 32 < B <= 64; 2: v3 for every batched B; 0: never;

@@ -217,6 +217,33 @@ __device__ __forceinline__ Best lmg_reduce(const LmGran& q) {
   return best_wave(r);
 }
 
+// Batched deferred select at 4 <= B <= 8 (defer_sel 3): lm_head (ar_mfma_ln_kernel OUT 3, 16 vocabulary
+// rows per block) leaves one granule per (block, row) in st.lmbest laid out [256 blocks][8 rows]; the
+// next step's c_attn layer 0 (ar_mfma_ln_kernel MODE 7) reduces a row's 256 granules with one wave
+constexpr int LM8_BLOCKS = VOCAB / 16, LM8_ROWS = 8;
+struct LmGran8 {
+  u64x2_t g[LM8_BLOCKS / 64];
+};
+__device__ __forceinline__ void lmg8_issue(const ArState& st, int b, int lane, LmGran8& q) {
+  const u64x2_t* base = reinterpret_cast<const u64x2_t*>(st.lmbest);
+#pragma unroll
+  for (int k = 0; k < LM8_BLOCKS / 64; ++k) q.g[k] = base[(size_t)(lane + 64 * k) * LM8_ROWS + b];
+}
+__device__ __forceinline__ Best lmg8_reduce(const LmGran8& q) {
+  Best r{-INFINITY, -INFINITY, 0x7fffffff};
+#pragma unroll
+  for (int k = 0; k < LM8_BLOCKS / 64; ++k)
+    r = best_merge(r, Best{__uint_as_float((unsigned)q.g[k].x), __uint_as_float((unsigned)q.g[k].y),
+                           (int)(q.g[k].x >> 32)});
+  return best_wave(r);
+}
+__device__ __forceinline__ u64x2_t lm_granule(Best r) {
+  u64x2_t g;
+  g.x = ((unsigned long long)(unsigned)r.i << 32) | __float_as_uint(r.v);
+  g.y = (unsigned long long)__float_as_uint(r.v2);
+  return g;
+}
+
 // one K (which 0) or V (which 1) element of the KV cache in its dtype
 __device__ __forceinline__ void store_kv(const GemvArgs& a, int which, size_t idx, float v) {
   void* base = which ? a.st.vc : a.st.kc;
@@ -2037,12 +2064,21 @@ static void launch_mproj_split(const GemvArgs& a, hipStream_t s) {
 // an LDS bf16 tile, then runs the MFMA 16 x (NT*16) tile of its 16 weight rows from it. The rows
 // are recomputed by every block (B x 3 KB of x from L2) instead of paying a separate rows kernel
 // and its launch boundary; the weight fragments are in flight while the rows are normalised.
+// MODE 7 (c_attn layer 0 of the deferred select at 4 <= B <= 8, defer_sel 3): MODE 3 after committing
+// the previous step's greedy select from lm_head's granules (block 0 writes the state and the shadow
+// records, attention layer 0 copies them back, as the B <= 2 GEMV step's IN 5); every block builds the
+// rows from the new records, which the KV append of the epilogue uses too. OUT 3 with defer_sel 3:
+// the block's top-1 / top-2 per row as one granule, the pending flag set by block 0.
 template <int NT, int OUT, int MODE>
 __global__ __launch_bounds__(256) void ar_mfma_ln_kernel(GemvArgs a) {
   constexpr int K = 768, NW = 4, R = NT * 16, RW = R / NW;  // rows per wave
   constexpr int LDX = K + 8;                                 // bf16 row stride (16-B pad)
+  static_assert(MODE != 7 || (NT == 1 && OUT == 0), "the deferred select's c_attn: B <= 8");
+  constexpr int SR = MODE == 7 ? LM8_ROWS / NW : 1;          // rows per wave that can be live (B <= 8)
   __shared__ __attribute__((aligned(16))) bf16_t xs[R * LDX];
   __shared__ float red[NW][NT * 256];
+  __shared__ float lgs[OUT == 3 && NT == 1 ? 16 * 17 : 1];
+  __shared__ int4 ri_s[MODE == 7 ? LM8_ROWS : 1];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int n0 = blockIdx.x * 16;
   const int B = a.B;
@@ -2052,13 +2088,26 @@ __global__ __launch_bounds__(256) void ar_mfma_ln_kernel(GemvArgs a) {
   constexpr int YR = MODE == 4 ? (RW < 2 ? RW : 2) : 0;
   float4 xv[RW][3], ya[YR > 0 ? YR : 1][YCOPIES][3];
   int4 ri[RW];
+  // MODE 7: the select's inputs with the control records (clamped rows, unconditional loads)
+  LmGran8 lmg[SR];
+  int2 rxp[SR];
+  unsigned selpend = 0u;
+  if constexpr (MODE == 7) {
+    selpend = *a.st.selp;
+#pragma unroll
+    for (int i = 0; i < SR; ++i) {
+      const int b = min(wave + NW * i, B - 1);
+      rxp[i] = a.st.rowx[b];
+      lmg8_issue(a.st, b, lane, lmg[i]);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < RW; ++i) {
     const int b = min(wave + NW * i, B - 1);
     if (MODE == 0 || MODE == 4) {
 #pragma unroll
       for (int j = 0; j < 3; ++j) xv[i][j] = *reinterpret_cast<const float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4);
-    } else {
+    } else if (MODE != 7 || i < SR) {
       ri[i] = a.st.rowinfo[b];
     }
     if (i < YR)
@@ -2081,13 +2130,42 @@ __global__ __launch_bounds__(256) void ar_mfma_ln_kernel(GemvArgs a) {
     wf[kk] = *reinterpret_cast<const uint4*>(
         a.Wf ? reinterpret_cast<const bf16_t*>(a.Wf) + (((size_t)(n0 >> 4) * (K / 32) + wave * 6 + kk) * 64 + lane) * 8
              : W + (size_t)wrow * K + k0 + kk * 32);
+  if constexpr (MODE == 7) {
+    // commit the previous step's select (ar_embed_select_kernel's argmax_commit, B <= 2 IN 5's shadow
+    // records); reduction and record select unconditional so that the granule loads stay up front
+#pragma unroll
+    for (int i = 0; i < SR; ++i) {
+      const int b = wave + NW * i, bc = min(b, B - 1);
+      const Best r = softmax_ties(a.st.logits + (size_t)bc * VOCAB, lmg8_reduce(lmg[i]), lane);
+      const int4 r0 = ri[i];
+      const int s = r0.x, j = rxp[i].x, p = r0.y + 1;
+      const bool take = selpend && s >= 0;
+      const int4 rn = take ? make_int4(s, min(p, a.st.max_pos - 1), rxp[i].y, min(max(r.i, 0), VOCAB - 1)) : r0;
+      if (b < B && blockIdx.x == 0 && lane == 0) {
+        if (take) {
+          if (p >= a.st.max_pos) atomicOr(a.st.err, 1);
+          if (j < a.st.plan_stride) {
+            a.st.tok_plan[(size_t)b * a.st.plan_stride + j] = r.i;
+            if (a.st.margin_plan) a.st.margin_plan[(size_t)b * a.st.plan_stride + j] = r.v - r.v2;
+          }
+          a.st.prev[s] = r.i;
+          a.st.pos[s] = p;
+          a.st.rowstep[b] = j + 1;
+        }
+        a.st.rowx_n[b] = make_int2(take ? j + 1 : j, 0);  // attention layer 0 looks up the next text id
+        a.st.rowinfo_n[b] = rn;
+      }
+      ri[i] = rn;
+      if (b < LM8_ROWS && lane == 0) ri_s[b] = rn;
+    }
+  }
   // 2. rows -> LayerNorm -> bf16 tile (rows >= B are zero: padded columns, never stored)
 #pragma unroll
   for (int i = 0; i < RW; ++i) {
     const int b = wave + NW * i;
     uint2* dst = reinterpret_cast<uint2*>(xs + b * LDX);
-    if (b < B) {
-      if (MODE == 3) {
+    if (b < B && (MODE != 7 || i < SR)) {
+      if (MODE == 3 || MODE == 7) {
         embed_row(a, ri[i], lane, xv[i]);
         if (blockIdx.x == 0)
 #pragma unroll
@@ -2134,16 +2212,49 @@ __global__ __launch_bounds__(256) void ar_mfma_ln_kernel(GemvArgs a) {
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) v += red[w][e];
-    if (OUT == 5) a.st.hb[(size_t)b * DFF + n] = f32_to_bf16(gelu_tanh(v));
-    else gemv_store<OUT>(a, n, b, v);
+    if constexpr (OUT == 3 && NT == 1) lgs[r * 17 + b] = v;
+    if constexpr (MODE == 7) {  // c_attn's store with this step's new record (gemv_store<0> reads rowinfo)
+      if (n < D) {
+        a.st.q[(size_t)b * D + n] = v;
+      } else {
+        const int c = (n - D) % D, which = (n - D) / D;
+        const int head = c / HD, d = c - head * HD;
+        const int4 rr = ri_s[b];
+        if (rr.x >= 0) store_kv(a, which, kv_at(a.layer, a.st.kv_chunks, a.st.max_streams, rr.x, head, rr.y) + d, v);
+      }
+    } else if (OUT == 5) {
+      a.st.hb[(size_t)b * DFF + n] = f32_to_bf16(gelu_tanh(v));
+    } else {
+      gemv_store<OUT>(a, n, b, v);
+    }
+  }
+  if constexpr (OUT == 3 && NT == 1) {
+    if (a.defer_sel == 3) {  // (kernel argument: uniform) this block's granule per row, pending flag
+      // raw barrier after the LDS writes: __syncthreads() would also wait for the logits stores
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (tid < B) {
+        Best r{-INFINITY, -INFINITY, 0x7fffffff};
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr)
+          if (n0 + rr < a.N) r = best_merge(r, Best{lgs[rr * 17 + tid], -INFINITY, n0 + rr});
+        reinterpret_cast<u64x2_t*>(a.st.lmbest)[(size_t)blockIdx.x * LM8_ROWS + tid] = lm_granule(r);
+      }
+      if (blockIdx.x == 0 && tid == 0) *a.st.selp = 1u;
+    }
   }
 }
 
 template <int OUT, int MODE>
 static void launch_mfma_ln(const GemvArgs& a, hipStream_t s) {
   dim3 grid((a.N + 15) / 16), block(256);
-  if (a.B <= 16) hipLaunchKernelGGL((ar_mfma_ln_kernel<1, OUT, MODE>), grid, block, 0, s, a);
-  else hipLaunchKernelGGL((ar_mfma_ln_kernel<2, OUT, MODE>), grid, block, 0, s, a);
+  if constexpr (MODE == 7) {  // (B <= 8 by defer_select_ln)
+    hipLaunchKernelGGL((ar_mfma_ln_kernel<1, OUT, MODE>), grid, block, 0, s, a);
+  } else {
+    if (a.B <= 16) hipLaunchKernelGGL((ar_mfma_ln_kernel<1, OUT, MODE>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((ar_mfma_ln_kernel<2, OUT, MODE>), grid, block, 0, s, a);
+  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -2682,6 +2793,13 @@ static bool defer_select(int B) {
 template <typename TW>
 static bool use_f32b(int B);
 static bool f32b_qsplit(int B);
+// 4 <= B <= 8 on the LayerNorm-prologue GEMMs (ar_mfma_ln_kernel): the select folded into c_attn layer
+// 0's prologue from lm_head's granules (defer_sel 3) instead of ar_embed_select_kernel + the c_attn
+// launch (option defer_select 2: the embedding + select kernel at these B too, the cross-check)
+template <typename TW>
+static bool defer_select_ln(int B) {
+  return opts().defer_select == 1 && use_mfma<TW>(B) && B >= 4 && B <= MFMA_LN_MAX && B <= LM8_ROWS;
+}
 template <typename TW>
 static bool defer_select_batched(int B) {
   // us/step (tools/step_sweep.py, t = 256+) argmax kernel / deferred: B = 3: 112.9 / 114.7 (B = 3
@@ -2821,7 +2939,9 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
   switch (op) {
     case 0:
       a.W = w.w_attn[l]; a.Wf = pk ? w.f_attn[l] : nullptr; a.N = 3 * D; a.ln_w = w.ln1[l];
-      if (mf && l == 0 && a.defer_sel == 2) {  // embedding + the previous step's select, then c_attn
+      if (mf && l == 0 && a.defer_sel == 3) {  // the previous step's select + embedding in c_attn's prologue
+        launch_mfma_ln<0, 7>(a, s);
+      } else if (mf && l == 0 && a.defer_sel == 2) {  // embedding + the previous step's select, then c_attn
         hipLaunchKernelGGL(ar_embed_select_kernel<>, dim3(B), dim3(256), 0, s, a);
         if (qkv_ksplit<TW>(B, kvdtype)) launch_qkv_ksplit(a, s);
         else launch_mfma2<768, 0>(a, s);
@@ -2844,7 +2964,7 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       }
       break;
     case 1:
-      launch_attn(a.st, kvdtype, B, l, s, nsm, (mf && nsm == 1) ? 1 + a.xpk : 0, a.defer_sel == 1 && l == 0,
+      launch_attn(a.st, kvdtype, B, l, s, nsm, (mf && nsm == 1) ? 1 + a.xpk : 0, (a.defer_sel == 1 || a.defer_sel == 3) && l == 0,
                   qkv_ksplit<TW>(B, kvdtype), a8);
       break;
     case 2:
@@ -2922,7 +3042,7 @@ template <typename TW>
 static bool ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B, const float* emb_row, int slot,
                       int pos, float* logits_dst, bool select, hipStream_t s) {
   GemvArgs a = make_args<TW>(w, st, kvdtype, B, emb_row);
-  a.defer_sel = (select && !emb_row) ? (defer_select<TW>(B) ? 1 : defer_select_batched<TW>(B) ? 2 : 0) : 0;
+  a.defer_sel = (select && !emb_row) ? (defer_select<TW>(B) ? 1 : defer_select_batched<TW>(B) ? (defer_select_ln<TW>(B) ? 3 : 2) : 0) : 0;
   if (emb_row) hipLaunchKernelGGL(ar_row_state_kernel, dim3(1), dim3(1), 0, s, st, slot, pos);
   for (int l = 0; l < N_LAYER; ++l)
     for (int op = 0; op < 5; ++op) launch_op<TW>(op, a, w, l, kvdtype, B, s);
@@ -2962,6 +3082,17 @@ void ar_launch_step(const ArWeights& w, const ArState& st, int wdtype, int kvdty
   if (mode == 0 && !deferred) hipLaunchKernelGGL(ar_argmax_kernel, dim3(B), dim3(256), 0, s, st);
 }
 
+// test hook (select probe path 3): the 4 <= B <= 8 granule select as c_attn layer 0 (MODE 7) runs it
+// (lmg8_reduce + softmax_ties), committed with argmax_commit
+__global__ __launch_bounds__(64) void ar_select8_probe_kernel(ArState st) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int4 ri = st.rowinfo[b];
+  LmGran8 q;
+  lmg8_issue(st, b, lane, q);
+  const Best r = softmax_ties(st.logits + (size_t)b * VOCAB, lmg8_reduce(q), lane);
+  if (lane == 0 && ri.x >= 0) argmax_commit(st, b, ri, r);
+}
+
 // deferred select: the last step's lm_head granules are committed here (argmax_commit), once per
 // lvx_ar_steps call, after the steps
 __global__ __launch_bounds__(64) void ar_select_final_kernel(ArState st) {
@@ -2988,6 +3119,11 @@ __global__ __launch_bounds__(64) void ar_select_final_kernel(ArState st) {
 __global__ void ar_select_probe_prep_kernel(ArState st, int B, int path) {
   const int blk = blockIdx.x, b = threadIdx.x;
   if (b >= B) return;
+  if (path == 3 && blk < LM8_BLOCKS) {  // as ar_mfma_ln_kernel OUT 3 forms them: 16 vocabulary rows per block
+    Best r{-INFINITY, -INFINITY, 0x7fffffff};
+    for (int n = blk * 16; n < blk * 16 + 16; ++n) r = best_merge(r, Best{st.logits[(size_t)b * VOCAB + n], -INFINITY, n});
+    reinterpret_cast<u64x2_t*>(st.lmbest)[(size_t)blk * LM8_ROWS + b] = lm_granule(r);
+  }
   if (path == 1) {
     Best r{-INFINITY, -INFINITY, 0x7fffffff};
     for (int n = blk * 8; n < blk * 8 + 8; ++n) r = best_merge(r, Best{st.logits[(size_t)b * VOCAB + n], -INFINITY, n});
@@ -3003,13 +3139,15 @@ __global__ void ar_select_probe_prep_kernel(ArState st, int B, int path) {
 }
 
 int ar_select_probe(const ArWeights& w, const ArState& st, int B, int path, hipStream_t s) {
-  if (path < 0 || path > 2 || B < 1 || (path == 1 && B > 4)) return -1;
+  if (path < 0 || path > 3 || B < 1 || (path == 1 && B > 4) || (path == 3 && B > LM8_ROWS)) return -1;
   hipLaunchKernelGGL(ar_rowinfo_init_kernel, dim3((B + 63) / 64), dim3(64), 0, s, st, B);
   hipLaunchKernelGGL(ar_select_probe_prep_kernel, dim3(LM_SEL_BLOCKS), dim3(64), 0, s, st, B, path);
   if (path == 0) {
     hipLaunchKernelGGL(ar_argmax_kernel, dim3(B), dim3(256), 0, s, st);
   } else if (path == 1) {
     hipLaunchKernelGGL(ar_select_final_kernel, dim3(B), dim3(64), 0, s, st);
+  } else if (path == 3) {
+    hipLaunchKernelGGL(ar_select8_probe_kernel, dim3(B), dim3(64), 0, s, st);
   } else {
     GemvArgs a = make_args<float>(w, st, LVX_DTYPE_F32, B, nullptr);
     a.ln_w = w.ln1[0];

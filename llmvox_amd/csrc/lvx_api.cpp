@@ -665,7 +665,7 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   std::string n(name);
   std::lock_guard<std::mutex> lk(c->mu);
   Opts& o = c->opts;  // this context only (round 4: the switches were process-wide globals)
-  if (n == "defer_select") o.defer_select = value != 0;
+  if (n == "defer_select") o.defer_select = value;
   else if (n == "fuse_mlp") o.fuse_mlp = value != 0;
   else if (n == "bt") o.bt = std::min(std::max(value, 0), 2);
   else if (n == "codec_g2") o.codec_g2 = value != 0;
@@ -876,8 +876,9 @@ int lvx_select_probe(lvx_ctx* c, int path, int B, const int32_t* slots, const fl
                      const int32_t* text_plan, int plan_stride, int32_t* rowstep, int32_t* tok_plan,
                      float* margin_plan, void* stream) {
   NEED_FINAL(c);
-  if (B < 1 || B > c->cfg.max_streams || (path == 1 && B > 4)) return fail(LVX_E_ARG, "B out of range for this path");
-  if (path < 0 || path > 2) return fail(LVX_E_ARG, "path must be 0, 1 or 2");
+  if (B < 1 || B > c->cfg.max_streams || (path == 1 && B > 4) || (path == 3 && B > 8))
+    return fail(LVX_E_ARG, "B out of range for this path");
+  if (path < 0 || path > 3) return fail(LVX_E_ARG, "path must be 0, 1, 2 or 3");
   if (!slots || !logits || !text_plan || !rowstep || !tok_plan || plan_stride < 2)
     return fail(LVX_E_ARG, "null argument or plan_stride < 2");
   HIP_TRY(hipSetDevice(c->cfg.device));

@@ -30,7 +30,8 @@ constexpr int LM_MAX_BLOCKS = 1024;  // lm_head blocks of the fused argmax tail 
 // opts(). Options set on one context therefore never change another context's kernels, and a
 // launch never reads an option while another thread writes it.
 struct Opts {
-  int defer_select = 1;  // greedy select deferred into the next step's first kernel; 0: argmax kernel
+  int defer_select = 1;  // greedy select deferred into the next step's first kernel; 0: argmax kernel;
+                         // 2: as 1 but 4 <= B <= 8 through ar_embed_select_kernel (cross-check)
   int fuse_mlp = 1;      // bf16, B <= 2: c_fc + gelu + mlp c_proj in one kernel; 0: two GEMV kernels
   int bt = 1;            // 1: batched v3 for 32 < B <= 64; 2: v3 for every batched B (cross-check); 0: off
   int codec_g2 = 1, codec_skinny = 1, codec_g3 = 1, codec_g3f = 2;  // codec GEMM kernels (cross-checks)

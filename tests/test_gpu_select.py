@@ -109,11 +109,13 @@ def eng_batched():
     e.close()
 
 
-@pytest.mark.parametrize("B", [4, 8, 32, 48])
-def test_batched_deferred_select_matches_argmax_kernel(eng_batched, B):
-    """Batched steps (MFMA / v3 paths): the select runs in the next step's embedding rows kernel
-    (ar_argmax_kernel after the last step). These paths have no arrival-order sums: bit-equal,
-    with one idle row."""
+@pytest.mark.parametrize("B,ref_mode", [(4, 0), (8, 0), (32, 0), (48, 0), (4, 2), (5, 2), (8, 2)])
+def test_batched_deferred_select_matches_argmax_kernel(eng_batched, B, ref_mode):
+    """Batched steps (MFMA / v3 paths): the select runs in the next step's first kernel (4 <= B <= 8:
+    c_attn layer 0 reduces lm_head's granules; larger B: the embedding rows kernel), ar_argmax_kernel
+    after the last step. Against the argmax kernel after every lm_head (ref_mode 0) and, at B <= 8,
+    against the embedding + select kernel (option defer_select 2). These paths have no arrival-order
+    sums: bit-equal, with one idle row."""
     e = eng_batched
     slots = list(range(B))
     slots[B // 2] = -1
@@ -136,7 +138,7 @@ def test_batched_deferred_select_matches_argmax_kernel(eng_batched, B):
         pos = [e.slot_position(s) for s in slots if s >= 0]
         return tok.cpu().numpy(), margin.cpu().numpy(), rowstep.cpu().numpy(), pos, e.last_logits(B).cpu().numpy()
 
-    e.set_option("defer_select", 0)
+    e.set_option("defer_select", ref_mode)
     try:
         ref = run()
         e.set_option("defer_select", 1)
@@ -193,9 +195,9 @@ def test_kernel_probe_graphs(eng, B):
         eng.probe_kernel(6, slots, 20)
 
 
-@pytest.mark.parametrize("path,B", [(0, 1), (0, 8), (1, 1), (1, 2), (1, 4), (2, 4), (2, 16)],
+@pytest.mark.parametrize("path,B", [(0, 1), (0, 8), (1, 1), (1, 2), (1, 4), (2, 4), (2, 16), (3, 4), (3, 8)],
                          ids=["argmax-B1", "argmax-B8", "granules-B1", "granules-B2", "granules-B4",
-                              "batched-B4", "batched-B16"])
+                              "batched-B4", "batched-B16", "granules16-B4", "granules16-B8"])
 def test_select_paths_reproduce_softmax_argmax(eng_batched, path, B):
     """Every production select path over constructed near-tie logits (rivals 0..6 ulps and up to
     3 x 2^-25 below the maximum, before and after it) picks what the reference's
@@ -227,3 +229,55 @@ def test_select_paths_reproduce_softmax_argmax(eng_batched, path, B):
             assert rs[b] == 2 and t[b, 0] == -7 and t[b, 2] == -7
         assert [e.slot_position(s) for s in range(B)] == [6] * B
     assert picked == want
+
+
+@pytest.mark.parametrize("B", [4, 8])
+def test_granule_select_fp8_kv_matches_embed_select(B):
+    """configs[4]'s path (bf16 weights, fp8 KV, one 8-wave attention split): the 4 <= B <= 8 select
+    folded into c_attn layer 0 (defer_select 1) against the embedding + select kernel (defer_select 2)
+    and the argmax kernel after lm_head (0), across several lvx_ar_steps calls and graph replays on a
+    side stream, with an idle row: tokens, margins, plan steps, positions and the live rows' logits
+    bit-equal."""
+    from llmvox_amd.engine import build_engine
+    e = build_engine(0, "bf16", "fp8", max_streams=8, max_positions=512, max_codec_frames=64)
+    dev = e.device
+    slots = list(range(B))
+    slots[1] = -1
+    calls = [5, 16, 1, 33]
+    n = sum(calls)
+
+    def run():
+        rng = np.random.default_rng(7 * B)
+        plan = torch.from_numpy(rng.integers(3, 384, size=(B, n)).astype(np.int32)).to(dev)
+        for s in range(8):
+            e.reset_slot(s)
+        st = torch.tensor(slots, dtype=torch.int32, device=dev)
+        rowstep = torch.zeros(B, dtype=torch.int32, device=dev)
+        tok = torch.full((B, n), -7, dtype=torch.int32, device=dev)
+        margin = torch.zeros(B, n, dtype=torch.float32, device=dev)
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for c in calls:
+                e.ar_steps(c, st, plan, rowstep, tok, margin)
+            e.check_errors()
+            pos = [e.slot_position(s) for s in slots if s >= 0]
+            logits = e.last_logits(B)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        return tok.cpu().numpy(), margin.cpu().numpy(), rowstep.cpu().numpy(), pos, logits.cpu().numpy()
+
+    try:
+        res = {}
+        for mode in (2, 0, 1):
+            e.set_option("defer_select", mode)
+            res[mode] = run()
+    finally:
+        e.close()
+    live = [b for b in range(B) if slots[b] >= 0]
+    for ref in (2, 0):
+        for a, b, name in zip(res[1], res[ref], ["tokens", "margins", "rowstep", "positions", "logits"]):
+            if name == "logits":
+                a, b = a[live], b[live]
+            np.testing.assert_array_equal(np.asarray(a), np.asarray(b), err_msg=f"{name} vs defer_select {ref}")
+    assert res[1][2][1] == 0 and (res[1][0][1] == -7).all()
+    assert all(res[1][2][b] == n for b in live)
