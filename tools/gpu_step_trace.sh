@@ -1,6 +1,6 @@
 #!/bin/bash
-# Per-kernel times of the fp32 parity-mode step (B = 32, positions 384..639) and of the bf16 step
-# at the same positions: rocprofv3 kernel-trace stats of tools/step_sweep.py (null stream: each
+# Per-kernel times of the decode step (default: the fp32 parity mode and the bf16 step at B = 32,
+# positions 384..639; B / P0 / SPEC / WS / LVX_SWEEP_KV select others): rocprofv3 kernel-trace stats of tools/step_sweep.py (null stream: each
 # kernel a dispatch of its own). Outputs under gpurun_out/fp32t.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
