@@ -8,7 +8,8 @@ usage: python tools/interference_probe.py [P0] [mask ...]   mask: all | first:K 
   | lowprio (a low-priority plain stream, the steps' stream high) | opt=name=value (an option for the
   codec calls, on a plain stream) | copy:MB (a torch copy of MB megabytes instead
   of the codec) | mm:N (a torch bf16 N x N x N matmul instead of the codec) | mm:MxNxK (an M x K by K x N
-  matmul)"""
+  matmul) | split:K (the 32 streams' codec as K calls of 32 / K streams each)
+Also printed: the step time lost per codec call (lost per ms x the call's ms beside the steps)."""
 import ctypes
 import sys
 import time
@@ -28,7 +29,7 @@ n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
 
 
 def masked_stream(spec):
-    if spec == "all" or spec.startswith("opt=") or spec.startswith("copy:") or spec.startswith("mm:"):
+    if spec == "all" or spec.split(":")[0] in ("opt=", "copy", "mm", "split") or spec.startswith("opt="):
         return torch.cuda.Stream(device=dev)
     if spec == "lowprio":
         return torch.cuda.Stream(device=dev, priority=0)
@@ -96,6 +97,13 @@ def codec_run(C, n, spec="all"):
             c0.record(C)
             for _ in range(n * reps):
                 torch.mm(a, b)
+        elif spec.startswith("split:"):
+            k = int(spec.split(":")[1])
+            g = B // k
+            c0.record(C)
+            for _ in range(n):
+                for j in range(k):
+                    e.decode_codes(codes[j * g:(j + 1) * g], 0, out=pcm[j * g:(j + 1) * g])
         else:
             c0.record(C)
             for _ in range(n):
@@ -133,6 +141,7 @@ for spec in MASKS:
     res.sort(key=lambda r: r[2])
     a, ca, b, cb, per = res[1]
     print(f"codec stream {spec:10s}: steps alone {a:6.1f} us, beside the codec {b:6.1f} us; codec alone "
-          f"{ca:5.2f} ms, beside the steps {cb:5.2f} ms; step time lost per ms of codec {per:5.2f}", flush=True)
+          f"{ca:5.2f} ms, beside the steps {cb:5.2f} ms; step time lost per ms of codec {per:5.2f} "
+          f"(per call {per * cb:5.2f} ms)", flush=True)
     if spec.startswith("opt="):
         e.set_option(k, 0)
