@@ -37,6 +37,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import statistics
 import sys
@@ -492,8 +493,9 @@ def run_config3(args, eng, world, rank, local, dist):
                                           "its codec ends" if args.codec_overlap else "serial FusedScheduler"),
                        "streams_per_gpu": S, "utterance_tokens": N, "dump_schedule_replica0": dump_schedule(N, 10),
                        "dump_schedule_replica1": dump_schedule(N, 160),
-                       "parallelism": f"streams sharded over {world} GPU(s); rank 0 scatters the request texts and "
-                                      "gathers every stream's PCM bytes (sizes first) over RCCL"},
+                       "parallelism": (f"streams sharded over {world} GPU(s); rank 0 scatters the request texts and "
+                                       f"gathers every stream's PCM bytes (sizes first) over {dist.get_backend()}"
+                                       if dist is not None else "one GPU, no process group (no collective runs)")},
             "pcm_bytes_gathered_rank0": pcm_bytes[0],
             "audio_samples_per_s": round(320 * value, 1),
             "realtime_factor_per_stream": round(value / (world * S) / 75.0, 1),
@@ -632,7 +634,7 @@ def first_chunk_latency(eng, reps=12, overlap=True):
     return statistics.median(lat)
 
 
-def first_chunk_latency_loaded(eng, busy=31, reps=12, max_chunk=64, seed=99, overlap=True):
+def first_chunk_latency_loaded(eng, busy=31, reps=34, max_chunk=64, seed=99, overlap=True):
     """p50 first-chunk latency UNDER LOAD (reference: a replica's first chunk is
     produced while the other replica decodes, streaming_server.py:357-376): a fresh stream joins a
     FusedScheduler that is already decoding `busy` streams (continuous batching, chunks of up to
@@ -641,7 +643,8 @@ def first_chunk_latency_loaded(eng, busy=31, reps=12, max_chunk=64, seed=99, ove
     at a random moment of the chunk in flight. Timed from the enqueue of the sentence's words to its
     first 3,200-sample dump as f32le bytes on the host (the in-flight chunk's remainder, the 10-step
     chunk it joins at B = busy + 1, that chunk's codec calls and the PCM copy included); the first
-    two of `reps` dropped (graph capture at the new batch sizes)."""
+    two of `reps` dropped (graph capture at the new batch sizes). Returns (p50, p90, max, joins) in ms
+    (the tail over >= 30 joins, not the median alone)."""
     import queue
     import threading
     from llmvox_amd.streaming import FusedScheduler
@@ -726,11 +729,13 @@ def first_chunk_latency_loaded(eng, busy=31, reps=12, max_chunk=64, seed=99, ove
     for st in list(sched.streams):
         sched.close_stream(st)
     sched.close()
-    return statistics.median(lat), max(lat)
+    q = sorted(lat)
+    p90 = q[min(len(q) - 1, int(math.ceil(0.9 * len(q))) - 1)]  # nearest-rank
+    return statistics.median(lat), p90, max(lat), len(lat)
 
 
 def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, world=1, codec_overlap=False,
-               seconds=0.0, window_s=10.0, record=None):
+               seconds=0.0, window_s=10.0, record=None, gathered=None):
     """W untimed then K timed bench steps (one step = `chunk` fused decode steps for the S streams,
     the batched codec decode of their codes, the PCM to the host; the PCM gathered to rank 0 when
     distributed). With reset_every R, step c is chunk c % R of utterance c // R: the streams' KV
@@ -740,7 +745,9 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
     passed instead of K (the plans are cycled), with a device sync every window_s seconds to record
     the rate of each window (run_chunks.windows, run_chunks.k_done). record (a list, tests only): every
     chunk's tokens and PCM, copied on the codec stream before its buffers are reused
-    (tests/test_gpu_bench_schedule.py holds the overlapped schedule to the serial one with it)."""
+    (tests/test_gpu_bench_schedule.py holds the overlapped schedule to the serial one with it).
+    gathered (a list, tests only): on rank 0, what the async gather delivered for each timed chunk, as
+    [rank][S, samples] host tensors in issue order (tests/test_gpu_rccl.py)."""
     from llmvox_amd.parallel import ChunkGather, gather_pcm
     n_plan_chunks = mine.shape[1] // chunk
     dev = eng.device
@@ -774,7 +781,7 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
     # and waited for (host poll) before the PCM buffer is written again: neither the decode nor the
     # codec queue ever holds the collective (round 4 put it on the codec stream, and N > 1 fell back
     # to the serial schedule)
-    gather = (ChunkGather(dist, rank, world, torch.cuda.Stream(device=dev))
+    gather = (ChunkGather(dist, rank, world, torch.cuda.Stream(device=dev), keep=gathered is not None)
               if (dist is not None and codec_overlap) else None)
     gpending = [False, False]
 
@@ -862,6 +869,8 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
     eng.check_errors()
     reset_all()
     torch.cuda.synchronize()
+    if gather is not None:
+        gather.gathered.clear()  # (tests) the warm-up chunks' gathers
 
     # timed region: K chunks, barrier + synchronize on both sides
     if dist is not None:
@@ -918,6 +927,8 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
         dist.barrier()
     dt = time.perf_counter() - t0
     eng.check_errors()
+    if gathered is not None and gather is not None:
+        gathered.extend(gather.gathered)
     run_chunks.ar_ms = [a.elapsed_time(b) for a, b in ar_t]
     return dt, tok_bufs[(K - 1) & 1], codec_stream, tok_bufs, pcm_bufs
 
@@ -990,6 +1001,10 @@ def main():
                     help="never replay graphs (steps and kernel probes launched kernel by kernel)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the multi-rank path on one GPU (collectives on host copies)")
+    ap.add_argument("--no-dist-world1", dest="dist_world1", action="store_false",
+                    help="at N = 1, no process group (by default N = 1 creates a one-rank RCCL group and runs the "
+                         "scatter / async gather path of N > 1: the same code the N-GPU lines time)")
+    ap.add_argument("--dist-world1", dest="dist_world1", action="store_true", help="(default) kept for old command lines")
     ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4],
                     help="BASELINE.json workload (2: default, 32 streams; 1: one stream; 3: scheduler replicas; 4: fp8)")
     ap.add_argument("--codec-dtype", default=None, choices=["fp8"], help="fp8 codec weights (configs[4])")
@@ -1004,6 +1019,7 @@ def main():
                     help="library options for A/B runs, name=value[,name=value] (lvx_set_option; default: production)")
     ap.add_argument("--rehearse", action="store_true",
                     help="CPU-only rehearsal of the multi-rank skeleton (gloo; tests/test_bench_launcher.py)")
+    ap.set_defaults(dist_world1=True)
     args = ap.parse_args()
     args.codec_overlap = not args.serial_codec
     if args.streams == 0:
@@ -1027,9 +1043,22 @@ def main():
     if args.rehearse:
         return rehearse(args, world, rank)
     dist, dist_info = None, None
-    if world > 1:
+    if world > 1 or args.dist_world1:
         import torch.distributed as tdist
-        if args.dist_backend == "gloo":  # rehearsal: every rank may share one GPU
+        if world == 1:
+            # a one-rank RCCL group (in-process store, no rendezvous), so that the N = 1 run takes the
+            # N > 1 code path: the RCCL text scatter, the async PCM gather on its communicator stream and
+            # its completion polls. Round 6, one box: 233.0k / 231.4k tok/s with it,
+            # 234.0k without (profiles/r06/dist_world1_ab.txt)
+            torch.cuda.set_device(local)
+            try:
+                tdist.init_process_group("nccl", store=tdist.HashStore(), rank=0, world_size=1,
+                                         device_id=torch.device(f"cuda:{local}"))
+                dist = tdist
+            except Exception as e:  # (reported in the line: dist backend null)
+                sys.stderr.write(f"bench.py: no one-rank RCCL group ({e!r}); N = 1 runs without collectives\n")
+                dist = None
+        elif args.dist_backend == "gloo":  # rehearsal: every rank may share one GPU
             local = local % max(1, torch.cuda.device_count())
             torch.cuda.set_device(local)
             tdist.init_process_group("gloo")
@@ -1038,7 +1067,8 @@ def main():
             torch.cuda.set_device(local)
             tdist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
             dist = tdist
-        dist_info = {"backend": tdist.get_backend(), "world_size": tdist.get_world_size()}
+        if dist is not None:
+            dist_info = {"backend": tdist.get_backend(), "world_size": tdist.get_world_size()}
 
     from llmvox_amd.engine import build_engine
     S, chunk, K, Wm = args.streams, args.chunk, args.steps, args.warmup
@@ -1217,7 +1247,9 @@ def main():
                                       if reset_every else f", one {K * chunk}-token utterance per stream"),
                        "streams_per_gpu": S, "chunk_tokens": chunk, "utterance_tokens": utt,
                        "kv_positions": f"0..{min(K * chunk, utt) - 1}",
-                       "parallelism": f"streams sharded over {world} GPU(s), RCCL scatter text / gather PCM",
+                       "parallelism": (f"streams sharded over {world} GPU(s), {dist_info['backend']} scatter text / "
+                                       "async gather PCM" if dist_info else
+                                       "one GPU, no process group (no collective runs)"),
                        "codec_schedule": ("chunk c's codec on a second stream beside chunk c + 1's AR (host-paced)"
                                           if args.codec_overlap else "codec after each chunk's AR, one stream")},
             "dist": dist_info or {"backend": None, "world_size": 1},
@@ -1225,7 +1257,8 @@ def main():
             "realtime_factor_per_stream": round(value / (world * S) / 75.0, 1),
             "p50_first_chunk_latency_ms": round(p50, 3),
             "p50_first_chunk_latency_loaded_ms": round(p50_loaded[0], 3) if p50_loaded else None,
-            "first_chunk_latency_loaded": ({"p50_ms": round(p50_loaded[0], 3), "max_ms": round(p50_loaded[1], 3),
+            "first_chunk_latency_loaded": ({"p50_ms": round(p50_loaded[0], 3), "p90_ms": round(p50_loaded[1], 3),
+                                            "max_ms": round(p50_loaded[2], 3), "joins": p50_loaded[3],
                                             "busy_streams": min(31, eng.max_streams - 1), "max_chunk": 64,
                                             "note": "a fresh stream joining a FusedScheduler already decoding the "
                                                     "busy streams; enqueue -> first 3,200-sample dump on the host"}

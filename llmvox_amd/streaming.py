@@ -478,8 +478,12 @@ class _Deliverer:
                     ev.synchronize()
                 fn()
             except BaseException as e:  # surfaced on the scheduler thread (take_error)
+                from ._lib import LvxStreamError
                 if self.error is None:
                     self.error = e
+                elif isinstance(self.error, LvxStreamError) and isinstance(e, LvxStreamError):
+                    # two groups' codec errors before the scheduler took the first: one error naming both
+                    self.error.streams = sorted(set(self.error.streams) | set(e.streams), key=lambda st: st.slot)
             with self.cv:
                 self.pending -= 1
                 self.cv.notify_all()
@@ -559,10 +563,15 @@ class FusedScheduler:
         self.codec_stream = (torch.cuda.Stream(device=dev) if codec_stream else (stream or torch.cuda.current_stream(dev))) \
             if (self.overlap and self.cuda) else None
         self.take = self.cuda and hasattr(engine, "take_errors")
+        self.codec_take = hasattr(engine, "take_errors")  # (host-synchronous decodes: any engine with the words)
         self.bufs = [self._alloc() for _ in range(2 if self.overlap else 1)]
         self._bi = 0
         self.inflight: Deque[_Chunk] = deque()
         self.deliverer = _Deliverer() if self.overlap else None
+        # streams whose dump failed in the codec (its error word): nothing more is delivered to them,
+        # so a client never receives audio after a hole (the error names them; the caller closes them;
+        # weak: kept past close_stream, for the jobs of chunks still queued behind the failure)
+        self.failed = weakref.WeakSet()
 
     def _alloc(self):
         torch, dev = self.torch, self.engine.device
@@ -737,14 +746,26 @@ class FusedScheduler:
                 # they are consumed below, then the row is reported at capacity
                 P = self.engine.max_positions
                 bits = getattr(err, "bits", 0) or 0  # (device bits: 1 KV capacity, 2 a plan overrun)
-                if bits & 2 or not any(st.m.position + n >= P for st in ch.ready):  # not a row at the edge
+                if bits & 2:
                     raise err
-                edge = {st for st in live if st.m.position + n > P}
-                at_cap = {st for st in live if st.m.position + n == P}
+                # the rows at the edge among the live ones (a discarded row's machine was rewound by its
+                # end of audio: its host position no longer says where its device row ran)
+                if not any(st.m.position + n >= P for st in live):
+                    if len(live) == len(ch.ready):
+                        raise err  # no row can have reached the edge: not a capacity condition of ours
+                    err = None  # only discarded rows can have run into it: their tokens are dropped anyway
+                else:
+                    edge = {st for st in live if st.m.position + n > P}
+                    at_cap = {st for st in live if st.m.position + n == P}
             elif isinstance(err, LvxNumericError):
                 edge = set(live)
             else:
                 raise err
+            # the named streams' rows in newer chunks (planned assuming this chunk was consumed) are not
+            # consumed either: the caller ends those streams
+            for st in edge | at_cap:
+                for newer in self.inflight:
+                    newer.bad.add(st)
             # (an error of rows already discarded -- a closed stream, a run-ahead row rolled back --
             # concerns no live stream: nothing is raised for it below)
         dumps = []  # (stream, tokens)
@@ -775,16 +796,20 @@ class FusedScheduler:
         # a row that reached the capacity exactly AND ended its segment in this chunk was rewound to
         # position 0 by the end of audio: it continues, as the reference would
         at_cap -= ended
+        codec_err = None
         if self.overlap:
             self._launch_decode(dumps, order, ch.ready)
         else:
-            self._deliver(self._decode(dumps), order, ch.ready)
+            pcm, codec_err = self._decode(dumps)
+            self._deliver(pcm, order, ch.ready)
         if err is not None:
             if self.deliverer is not None:
                 self.deliverer.wait()
-            err.streams = sorted(edge | at_cap, key=lambda st: st.slot)
+            err.streams = sorted(edge | at_cap | set(codec_err.streams if codec_err else ()), key=lambda st: st.slot)
             if err.streams:
                 raise err
+        if codec_err is not None:
+            raise codec_err
         return n
 
     def run_chunk(self) -> int:
@@ -803,8 +828,25 @@ class FusedScheduler:
 
     def _deliver(self, pcm, order, ready):
         for st in ready:
+            if st in self.failed:
+                continue
             for kind, v in order[st]:
                 st._out(pcm[v] if kind == "audio" else v)
+
+    def _codec_failure(self, exc, streams):
+        """A codec call's error word was set: the streams of its dumps get nothing more (``failed``) and
+        the error is re-raised as an LvxStreamError naming them (the service ends only their requests);
+        an error of a call that carries no stream's dump (decode_now) is returned as it was."""
+        from ._lib import LvxStreamError
+        streams = [st for st in streams if st is not None]
+        if not streams:
+            return exc
+        for st in streams:
+            self.failed.add(st)
+        se = LvxStreamError(getattr(exc, "code", -2), f"codec error word: {exc}")
+        se.bits = getattr(exc, "bits", 0)
+        se.streams = sorted(set(streams), key=lambda st: st.slot)
+        return se
 
     def _groups(self, dumps):
         """Dump indices batched by length (one codec call per group, within max_codec_frames)."""
@@ -817,29 +859,53 @@ class FusedScheduler:
                 yield L, idx[s:s + cap]
 
     def _decode(self, dumps):
+        """Every dump decoded now (one call per length group), host-synchronous. Returns (PCM per dump,
+        None or the LvxStreamError naming the streams of the groups whose codec error word was set:
+        the other groups' PCM is valid and delivered)."""
         torch = self.torch
         res: List[object] = [None] * len(dumps)
+        first, bad = None, []
         for L, grp in self._groups(dumps):
             codes = torch.tensor([dumps[i][1] for i in grp], dtype=torch.int32, device=self.engine.device)
             out = self.engine.decode_codes(codes).cpu().numpy()
             for k, i in enumerate(grp):
                 res[i] = out[k].astype("float32").tobytes() if self.to_bytes else out[k]
-        if dumps and self.take:  # the codec's own error word (host-synchronous here)
-            from . import _lib
-            e = torch.zeros((1,), dtype=torch.int32, device=self.engine.device)
-            self.engine.take_errors(_lib.ERRW_CODEC, e)
-            _lib.check_bits(int(e.item()))
-        return res
+            if self.codec_take:  # the codec's own error word, per group
+                from . import _lib
+                e = torch.zeros((1,), dtype=torch.int32, device=self.engine.device)
+                self.engine.take_errors(_lib.ERRW_CODEC, e)
+                try:
+                    _lib.check_bits(int(e.item()))
+                except _lib.LvxError as exc:
+                    first = first or exc
+                    bad += [dumps[i][0] for i in grp]
+        return res, (self._codec_failure(first, bad) if first is not None else None)
 
     def decode_now(self, tokens: List[int]):
-        """One dump decoded and returned at once (the service's end-of-request tails): on the codec
-        stream when overlapping, so it does not queue behind the decode chunk in flight."""
+        """One dump decoded and returned at once, on the codec stream when overlapping, so it does not
+        queue behind the decode chunk in flight (raises for the codec's error word)."""
         torch = self.torch
-        if self.codec_stream is None:
-            return self._decode([(None, tokens)])[0]
-        with torch.cuda.stream(self.codec_stream):
-            out = self._decode([(None, tokens)])[0]
-        return out
+        with (torch.cuda.stream(self.codec_stream) if self.codec_stream is not None else contextlib.nullcontext()):
+            res, err = self._decode([(None, tokens)])
+        if err is not None:
+            raise err
+        return res[0]
+
+    def queue_tail(self, st: FusedStream, tokens: List[int]):
+        """The stream's undumped tail decoded as one last dump and delivered AFTER every item already
+        queued for it (the service's end of a request). Overlap: queued on the codec stream, delivered by
+        the delivery thread behind its event (the caller never waits for the device); serial: now."""
+        if self.deliverer is None:
+            st._out(self.decode_now(tokens))
+            return
+        self._launch_decode([(st, tokens)], {st: [("audio", 0)]}, [st])
+
+    def after_delivered(self, fn):
+        """fn() once every item queued so far has been delivered (in the delivery order)."""
+        if self.deliverer is None:
+            fn()
+        else:
+            self.deliverer.put(None, fn)
 
     def _launch_decode(self, dumps, order, ready):
         """Queue the chunk's decodes on the codec stream (codes from the host: no wait on the AR
@@ -849,8 +915,13 @@ class FusedScheduler:
         of the same chunk. Streams without a dump in the chunk are served by the first job."""
         torch = self.torch
         if not self.cuda:  # a stand-in engine: decode now, deliver in order through the same thread
-            pcm = self._decode(dumps)
-            self.deliverer.put(None, lambda: self._deliver(pcm, order, ready))
+            pcm, err = self._decode(dumps)
+
+            def job():
+                self._deliver(pcm, order, ready)
+                if err is not None:
+                    raise err
+            self.deliverer.put(None, job)
             return
         groups = sorted(self._groups(dumps), key=lambda g: g[0])
         if not groups:
@@ -880,11 +951,20 @@ class FusedScheduler:
             sts = [st for st in ready if last[st] == g]
 
             def deliver(host=host, err_h=err_h, grp=grp, L=L, sts=sts, codes=codes):  # (codes: kept alive)
-                _lib.check_bits(int(err_h[0]))
-                for k, i in enumerate(grp):
-                    a = host[k * 320 * L:(k + 1) * 320 * L].numpy()
-                    pcm[i] = a.tobytes() if to_bytes else a.copy()
+                # a set codec error word fails this group's streams only: the
+                # other streams of the job, and the other groups' jobs, are still delivered
+                exc = None
+                try:
+                    _lib.check_bits(int(err_h[0]))
+                except _lib.LvxError as e:
+                    exc = self._codec_failure(e, [dumps[i][0] for i in grp])
+                if exc is None:
+                    for k, i in enumerate(grp):
+                        a = host[k * 320 * L:(k + 1) * 320 * L].numpy()
+                        pcm[i] = a.tobytes() if to_bytes else a.copy()
                 self._deliver(pcm, order, sts)
+                if exc is not None:
+                    raise exc
 
             self.deliverer.put(ev, deliver)
 

@@ -140,16 +140,18 @@ def test_fused_overlap_delivers_same_items(handler, forced_eoa):
     texts = [WORDS, "hello there world.".split(" "), WORDS[:5] + ["again."], "one two three.".split(" ")]
     res = []
     for overlap in (False, True):
-        sch = S.FusedScheduler(handler.engine, max_chunk=40, overlap=overlap)
+        # both schedules run to idle, each stream stopped at 200 tokens by the stop rule, so the whole
+        # event lists compare (a common prefix would pass a run that drops trailing items)
+        sch = S.FusedScheduler(handler.engine, max_chunk=40, overlap=overlap,
+                               stop_rule=lambda st, ntok, pos: ntok >= 200)
         sts = []
         for i, t in enumerate(texts):
             st = sch.open_stream(index=i % 2, dump_size=10 if i % 2 == 0 else 160, eoa_id=eoa)
             for w in t:
                 st.feed(w)
             sts.append(st)
-        for _ in range(10):
-            sch.run_chunk()
-        sch.flush()
+        assert sch.run_until_idle(max_chunks=200) > 0
+        assert sch.run_chunk() == 0 and not sch.inflight
         res.append([(list(st.events), list(st.tokens)) for st in sts])
         assert sch.overlap == overlap
         for st in sts:
@@ -158,11 +160,9 @@ def test_fused_overlap_delivers_same_items(handler, forced_eoa):
     if forced_eoa:
         assert any(isinstance(x, int) for ev, _ in res[0] for x in ev)  # a segment did end
     for (a_ev, a_tok), (b_ev, b_tok) in zip(*res):
-        n = min(len(a_ev), len(b_ev))  # (the overlapped run decoded one more chunk in its 10 calls)
-        assert n > 0
-        m = min(len(a_tok), len(b_tok))
-        assert a_tok[:m] == b_tok[:m]
-        for x, y in zip(a_ev[:n], b_ev[:n]):
+        assert len(a_ev) > 0 and len(a_ev) == len(b_ev)
+        assert a_tok == b_tok
+        for x, y in zip(a_ev, b_ev):
             assert type(x) is type(y)
             assert x == y
 
@@ -207,3 +207,45 @@ def test_checkpoint_block_size_bounds_positions(tmp_path_factory):
     with pytest.raises(AssertionError, match="block size is only 64"):
         h.model(torch.cat([hist, x], dim=1), kvcache=kv)
     h.engine.close()
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+def test_codec_error_word_fails_only_its_group(handler, overlap):
+    """a codec call whose error word is set (here: a code outside the codebook in
+    one stream's dump) fails only the streams of that call, as an LvxStreamError naming them; the other
+    call's stream gets its PCM (equal to a clean decode of the same codes), and nothing is delivered to
+    the failed stream afterwards (no audio after a hole)."""
+    from llmvox_amd._lib import LvxStreamError
+    eng = handler.engine
+    sch = S.FusedScheduler(eng, max_chunk=32, overlap=overlap)
+    a = sch.open_stream(index=0, dump_size=10)
+    b = sch.open_stream(index=1, dump_size=160)
+    good = [(7 * i + 3) % 4096 for i in range(10)]
+    bad = [1, 5000] + [(11 * i) % 4096 for i in range(18)]  # 20 frames: a call of its own
+    dumps, order = [(a, good), (b, bad)], {a: [("audio", 0)], b: [("audio", 1), ("signal", 1)]}
+    if overlap:
+        sch._launch_decode(dumps, order, [a, b])
+        with pytest.raises(LvxStreamError) as ei:
+            sch.flush()
+        err = ei.value
+    else:
+        pcm, err = sch._decode(dumps)
+        sch._deliver(pcm, order, [a, b])
+    assert isinstance(err, LvxStreamError) and err.streams == [b]
+    assert b.events == []
+    assert len(a.events) == 1
+    ref = eng.decode_codes(torch.tensor([good], dtype=torch.int32, device=eng.device)).cpu().numpy()[0]
+    assert np.frombuffer(a.events[0], dtype=np.float32).tobytes() == ref.astype(np.float32).tobytes()
+    # a later dump of the failed stream is not delivered; the other stream's still is
+    if overlap:
+        sch._launch_decode([(b, good), (a, good)], {b: [("audio", 0)], a: [("audio", 1)]}, [b, a])
+        sch.flush()
+    else:
+        pcm, err2 = sch._decode([(b, good), (a, good)])
+        assert err2 is None
+        sch._deliver(pcm, {b: [("audio", 0)], a: [("audio", 1)]}, [b, a])
+    assert b.events == [] and len(a.events) == 2
+    eng.check_errors()  # both words were taken
+    for st in (a, b):
+        sch.close_stream(st)
+    sch.close()

@@ -14,6 +14,6 @@ reps = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 e = build_engine(0, "bf16", "bf16", max_streams=32, max_positions=8192, max_codec_frames=32 * 256)
 torch.cuda.set_stream(torch.cuda.Stream(device=e.device))
 for rep in range(2):
-    p50, mx = bench.first_chunk_latency_loaded(e, busy=31, reps=reps, seed=99 + rep)
+    p50, _, mx, _ = bench.first_chunk_latency_loaded(e, busy=31, reps=reps, seed=99 + rep)
     print(f"loaded first chunk p50 {p50:.2f} ms max {mx:.2f} ms", flush=True)
 e.close()
