@@ -96,20 +96,14 @@ def attn_splits(B, wbytes):
     return ns
 
 
-KSPLIT = False  # library option "ksplit" (bench.py --opt ksplit=1)
-
-
 def kernel_bytes(which, B, t, wbytes, kvbytes):
     """Algorithmic HBM bytes of one launch of op `which` (weights streamed once + KV + the
-    activations it must read and write), as the batched path at this B moves them. With option
-    ksplit = 1 (off by default since round 3), at 9 <= B <= 32 with bf16 weights, c_attn hands its
-    output to the attention as four K-slice partials (ar_qkv_ksplit_kernel: 4 x 2,304 fp32 per row
-    written, read back by the attention, which also appends the new key). Split-KV partials (8 heads x ns x (96 + 2) fp32 per row) are
-    charged only when the attention runs more than one split (attn_splits)."""
+    activations it must read and write), as the batched path at this B moves them. Split-KV partials
+    (8 heads x ns x (96 + 2) fp32 per row) are charged only when the attention runs more than one
+    split (attn_splits)."""
     D, F, V = 768, 3072, 4096
     act = 4 * B
     mfma = wbytes == 2 and 3 <= B <= 64
-    ksplit = KSPLIT and mfma and kvbytes <= 2 and 9 <= B <= 32
     ns = attn_splits(B, wbytes)
     parts = act * 8 * ns * 98 if ns > 1 else 0           # split-KV partials written / read once
     rows_bf16 = 2 * D * B                                  # one bf16 operand row set
@@ -119,13 +113,9 @@ def kernel_bytes(which, B, t, wbytes, kvbytes):
     # prologue reads x and the partials itself (nothing written)
     fold = (6 * act * D + rows_bf16 if B > 8 else 5 * act * D) if mfma else 0
     if which == 0:
-        if ksplit:  # operand rows in, 4 K-slice partials out (the KV append happens in the attention)
-            return 3 * D * D * wbytes + rows_bf16 + act * 4 * 3 * D + fold
         return 3 * D * D * wbytes + (rows_bf16 if mfma else act * D) + act * D + 2 * D * kvbytes * B + fold
     if which == 1:
         kv = 2 * t * D * kvbytes * B
-        if ksplit:  # partials in, new key appended, head outputs (bf16 rows or split partials) out
-            return kv + act * 4 * 3 * D + 2 * D * kvbytes * B + (rows_bf16 if ns == 1 else parts)
         return kv + act * D + (rows_bf16 if (mfma and ns == 1) else parts)
     if which == 2:  # (+ the merge kernel when ns > 1) x read + written, bf16 copy for c_fc
         merge = (parts + 2 * rows_bf16) if (mfma and ns > 1) else parts
@@ -1080,12 +1070,9 @@ def main():
                        codec_dtype=args.codec_dtype)
     dev = eng.device
     torch.cuda.set_device(dev)
-    global KSPLIT
     for kv in filter(None, args.opt.split(",")):
         k, v = kv.split("=")
         eng.set_option(k, int(v))
-        if k == "ksplit":
-            KSPLIT = int(v) != 0
     if args.no_graphs:
         eng.set_graphs(False)
     if not args.null_stream:

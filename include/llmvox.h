@@ -173,28 +173,21 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
  *                     (no split-K combine); 0: the tile kernels;
  *   "codec_g3f"    fp32 (parity mode) codec GEMMs with >= 192 tiles of 128 x 192: 2 (default): the
  *                     LDS-DMA kernel with fp32 operands split into bf16 hi + lo, hi.hi + lo.hi + hi.lo
- *                     on v_mfma_f32_16x16x32_bf16 (fp32 accumulation); 1: the LDS-DMA kernel with
- *                     exact-fp32 v_mfma_f32_16x16x4_f32; 0: the 64 x 64 register-staged exact one;
+ *                     on v_mfma_f32_16x16x32_bf16 (fp32 accumulation); 1: the same kernel with exact-fp32
+ *                     v_mfma_f32_16x16x4_f32 (slower; the tests' exact-fp32 oracle for the split form);
  *   "codec_exp"    codec development bits, 0 = production kernels; bit 0: the general GroupNorm
  *                     kernel at every L (same bits); bits 1-2: dwconv+AdaLN frames per block at
  *                     >= 2,048 frames (0: 4, 1: 16, 2: 32, 3: 8; same bits); bit 3: library
  *                     exp / sin / cos in the bf16 iSTFT; bit 4: fp32 bf16x3 GEMMs split their
  *                     operands in registers, no split-image producers (same bits);
- *   "exp"          development bits, 0 = production kernels; bit 1: the one-launch c_attn even with
- *                     option ksplit = 1 (bit-identical: tests/test_gpu_batched.py); bit 2: the
- *                     batched MFMA GEMMs read the row-major weights instead of the fragment-packed
- *                     copy (bit-identical); bit 4: at 9 <= B <= 32 the bf16 operand rows (xn, xb,
- *                     hb) row-major instead of fragment-packed (bit-identical); bit 8: fp32 batched
- *                     c_proj / mlp c_proj in 32-row instead of 16-row batch tiles (bit-identical);
- *                     bit 16: batched bf16 c_proj / mlp c_proj in the 2-D grid order instead of the
- *                     XCD-aligned 1-D order (bit-identical);
+ *   "exp"          cross-check bits, 0 = production kernels (fp32 parity mode, each bit-identical or
+ *                     within fp32 summation noise: tests/test_gpu_f32b.py); bit 8: fp32 batched GEMMs
+ *                     in 32-row instead of 16-row batch tiles (bit-identical); bit 512: fp32 mlp c_proj
+ *                     unsplit, bit 1024: fp32 c_attn in one launch (another summation order);
  *   "f32b"         1: fp32 weights, 3 <= B <= 64: batched steps on exact-fp32 MFMA (ar_f32b_kernel);
  *                     0: the fp32 GEMV family (same ids against the reference: tests/test_gpu_f32b.py);
-  *   "ksplit"       (default 0) c_attn as four K-slice partials summed by the attention (9 <= B <= 32):
- *                  bit-identical to the one-launch c_attn; faster only when steps are launched one
- *                  by one (the null stream), slower under graph replay.
  *   "ln_max"       (2..8, default 8) largest B whose batched GEMMs normalise in their own prologue;
- *                  larger B run the rows kernel + K-split c_attn structure. */
+ *                  larger B run the rows kernel + batched GEMM structure. */
 int lvx_set_option(lvx_ctx* ctx, const char* name, int value);
 /* Enable/disable HIP-graph replay of lvx_ar_step for a given B (default on). */
 int lvx_set_graphs(lvx_ctx* ctx, int enable);

@@ -97,7 +97,6 @@ struct GemvArgs {
                             // accumulators in 2^-32 fixed point (int64 atomics: order-independent sums)
   const float* gsum;     // batched c_fc (ar_mfma2_kernel XM 1): ArWeights::fc_gsum of the layer
   int add_y;             // c_proj: fold the accumulators into x (layers >= 1; 0 at layer 0 = just clear)
-  int epi_late;          // ar_mfma2_kernel OUT 1: x and the copies loaded in the epilogue (option exp bit 4096, A/B)
   int defer_sel;         // deferred greedy select (option "defer_select"). 1: B <= 2 GEMV step, lm_head
                          // publishes per-block granules, the next step's c_attn layer 0 reduces them;
                          // 2: batched step, the next step's embedding rows kernel reduces the logits
@@ -1056,11 +1055,10 @@ template <> struct KvPiece<fp8_t> {
 // direct = 1 (batched path with one split per (row, head)): the normalised head output goes
 // straight to the bf16 operand row xn, as the merge kernel would write it (o * (1 / l)), and the
 // merge kernel is skipped.
-// QKV (bf16 KV, 9 <= B <= 32): c_attn left its output as four K-slice partials
-// (ar_qkv_ksplit_kernel, st.qkvp); threads 0-287 sum them in the K-slice order the one-launch GEMM
-// summed its waves (bit-identical), q goes through LDS, and the split holding key t - 1 appends the
-// new key's K / V to the cache and takes them from LDS in its last tile (its own store is not read
-// back).
+// QKV (fp32 KV: the parity mode, 3 <= B <= 32): c_attn left its output as four K-slice partials
+// (ar_qkv_ksplit_f32_kernel, st.qkvp); threads 0-287 sum them in K-slice order, q goes through LDS,
+// and the split holding key t - 1 appends the new key's K / V to the cache and takes them from LDS in
+// its last tile (its own store is not read back).
 // Online softmax kept PER KEY SLOT (bf16 / fp8 KV; round 3): each lane quad owns one key slot of the
 // tile (4 lanes x 24 dims) and keeps its own (m, l, o[24]) over the keys it sees, so a tile needs no
 // wave-wide reduction (the wave-uniform form spent two DPP + readlane reductions and a 24-deep FMA
@@ -1170,7 +1168,7 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
   // block for long splits (batched steps)
   constexpr int TK = NW * 16;
   constexpr bool SLOT = sizeof(TKV) < 4;  // per-key-slot online softmax (bf16 / fp8 KV)
-  static_assert(!QKV || NW == 4 || NW == 8, "the K-split c_attn path: 4 or 8 waves");
+  static_assert(!QKV || (NW == 4 && sizeof(TKV) == 4), "the K-split c_attn: the fp32 parity mode's 4-wave blocks");
   constexpr int QH = QKV ? (3 * HD + NW * 64 - 1) / (NW * 64) : 1;  // q / k / v elements per thread (2 at 4 waves, 1 at 8)
   __shared__ float wm_s[NW], wl_s[NW];
   __shared__ float wo_s[NW][4][HD];  // [wave][16-lane row][part * 24 + i]
@@ -1283,17 +1281,6 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
       uint4 ku[3], vu[3];
 #pragma unroll
       for (int i = 0; i < 3; ++i) { ku[i] = reinterpret_cast<const uint4&>(kp[i]); vu[i] = reinterpret_cast<const uint4&>(vp[i]); }
-      if constexpr (QKV) {  // the tile holding key t - 1 (wave-uniform test): that lane takes it from LDS
-        if (kb + TK >= k1) {
-          if (kb + kq == t - 1) {
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-              ku[i] = reinterpret_cast<const uint4*>(kvh_s[0])[part * 3 + i];
-              vu[i] = reinterpret_cast<const uint4*>(kvh_s[1])[part * 3 + i];
-            }
-          }
-        }
-      }
       slot_softmax_step_bf16(m, l, o2, qsp, ku, vu, valid);
       return;
     }
@@ -1769,9 +1756,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   const int B = a.B;
   TS_DECL;
   TS_MARK(0);
-  const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(a.W);
   const bf16_t* __restrict__ X = XM == 1 ? a.st.xb : ((KTOT == 768) ? a.st.xn : a.st.hb);
-  const int wrow = min(n0 + (lane & 15), a.N - 1);
   const int k0 = by * K + wave * 192 + 8 * (lane >> 4);
   // epilogue operands first (a load in the epilogue is one more dependent round trip): thread tid
   // stores elements e = tid + k * NW * 64, all of batch row tid % (NT * 16) (NW * 64 is a multiple
@@ -1826,12 +1811,10 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
   }
   uint4 wf[6], xf[NT][6];
   // fragment-packed weights (a.Wf): the wave's 6 loads are 6 contiguous KB
-  const bf16_t* wsrc = a.Wf ? reinterpret_cast<const bf16_t*>(a.Wf) +
-                                  (((size_t)(n0 >> 4) * (KTOT / 32) + (by * K + wave * 192) / 32) * 64 + lane) * 8
-                            : W + (size_t)wrow * KTOT + k0;
-  const int wstep = a.Wf ? 512 : 32;
+  const bf16_t* wsrc = reinterpret_cast<const bf16_t*>(a.Wf) +
+                       (((size_t)(n0 >> 4) * (KTOT / 32) + (by * K + wave * 192) / 32) * 64 + lane) * 8;
 #pragma unroll
-  for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(wsrc + kk * wstep);
+  for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(wsrc + kk * 512);
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int b = min(r0 + t * 16 + (lane & 15), B - 1);  // padded columns recompute row B-1, never stored
@@ -1914,7 +1897,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
       xo[e] = xn;
     } else if (OUT == 6) {  // split-K partial of mlp c_proj (K slice by) -> pending copy
       a.yacc[((size_t)b * YCOPIES + by) * D + n] = v;
-    } else if (OUT == 1 && !a.epi_late) {  // x (+ the folded copies, prefetched) + v
+    } else if (OUT == 1) {  // x (+ the folded copies, prefetched) + v
       a.st.x[(size_t)b * D + n] = xpre[k] + v;
     } else {
       gemv_store<OUT>(a, n, b, v);
@@ -1949,7 +1932,7 @@ static void launch_mfma2(const GemvArgs& a, hipStream_t s, bool btile = false) {
   dim3 grid((a.N + 15) / 16), block((K / 192) * 64);
   if (btile && a.B > 16) {  // 16-row batch tiles in grid.z: half the operand bytes per block
     grid.z = (a.B + 15) / 16;
-    if (grid.z == 2 && grid.x % 8 == 0 && !(opts().exp & 16)) {  // XCD-aligned order (xmap 2)
+    if (grid.z == 2 && grid.x % 8 == 0) {  // XCD-aligned order (xmap 2)
       GemvArgs b = a;
       b.xmap = 2;
       hipLaunchKernelGGL((ar_mfma2_kernel<K, 1, OUT, K, XM>), dim3(grid.x * 2), block, 0, s, b);
@@ -1961,85 +1944,12 @@ static void launch_mfma2(const GemvArgs& a, hipStream_t s, bool btile = false) {
   else hipLaunchKernelGGL((ar_mfma2_kernel<K, 4, OUT, K, XM>), grid, block, 0, s, a);
 }
 
-// c_attn of the batched v2 steps with the rows kernel before it (9 <= B <= 32, bf16 KV):
-// the K = 768 reduction split over the grid instead of over a block's waves. A block is 4 waves x 16
-// output rows (64 rows) of one 192-wide K slice: 24.6 KB of weights + 12.3 KB of operand rows per
-// block instead of 24.6 + 49 KB. Each wave stores its 16 x 32 partial (one 16-B store per
-// lane and batch tile) to st.qkvp[slice]; the attention sums the four slices in the order the
-// one-launch kernel summed its waves and appends the new key (bit-identical to ar_mfma2_kernel OUT 0).
-template <int NT>
-__global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_qkv_ksplit_kernel(GemvArgs a) {
-  // The batched GEMM launches are bound by the bytes each CU loads (~30 GB/s per CU from entry to
-  // operands landed, tools/step_timeline.py: 72 KB per CU 2.8 us, 36 KB 1.5 us, nothing 0.5 us), so
-  // the block's operand slice (NT * 16 rows x 192 columns), which all four waves multiply, is loaded
-  // once and shared through LDS: four waves each loading it measured as slow as the one-launch layout.
-  // B = 32, t = 512: c_attn 3.9 -> 2.0 us per launch, 154.3 -> 149.6 us per step.
-  constexpr int XR = NT * 16, XS = 200;  // rows, bf16 row stride (400 B: 16 rows hit distinct bank groups)
-  __shared__ __attribute__((aligned(16))) bf16_t xs[XR * XS];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int n0 = (blockIdx.x * 4 + wave) * 16, ks = blockIdx.y;
-  const int B = a.B;
-  TS_DECL;
-  TS_MARK(0);
-  const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(a.W);
-  const bf16_t* __restrict__ X = a.st.xn;
-  // operand slice first (vmcnt retires in issue order: the LDS fill then waits for it alone): the
-  // XR x 24 16-B chunks spread over the block, chunk c = tid + 256 j -> row c / 24, chunk c % 24
-  constexpr int XC = (XR * 24 + 255) / 256;
-  constexpr bool EXACT = XR * 24 % 256 == 0;  // NT = 2: three chunks per thread; NT = 1: 1.5 (clamped)
-  uint4 xv[XC];
-#pragma unroll
-  for (int j = 0; j < XC; ++j) {
-    const int c = EXACT ? tid + 256 * j : min(tid + 256 * j, XR * 24 - 1), r = c / 24, q = c - r * 24;
-    // a.xpk: the slice is NT x 6 fragments (chunk c = fragment c / 64, lane c % 64), else rows of 384 B
-    // (rows past B: row B-1 / whatever the tile holds, never stored)
-    const bf16_t* src = a.xpk ? X + ((((size_t)(c / 384) * (D / 32) + ks * 6 + (c % 384) / 64) * 64 + (c & 63)) << 3)
-                              : X + (size_t)min(r, B - 1) * D + ks * 192 + q * 8;
-    xv[j] = *reinterpret_cast<const uint4*>(src);
-  }
-  const int k0 = ks * 192 + 8 * (lane >> 4);
-  uint4 wf[6], xf[NT][6];
-  const bf16_t* wsrc = a.Wf ? reinterpret_cast<const bf16_t*>(a.Wf) + (((size_t)(n0 >> 4) * (D / 32) + ks * 6) * 64 + lane) * 8
-                            : W + (size_t)(n0 + (lane & 15)) * D + k0;
-  const int wstep = a.Wf ? 512 : 32;
-#pragma unroll
-  for (int kk = 0; kk < 6; ++kk) wf[kk] = *reinterpret_cast<const uint4*>(wsrc + kk * wstep);
-#pragma unroll
-  for (int j = 0; j < XC; ++j) {
-    const int c = tid + 256 * j, r = c / 24, q = c - r * 24;
-    if (EXACT || c < XR * 24) *reinterpret_cast<uint4*>(xs + (a.xpk ? c * 8 : r * XS + q * 8)) = xv[j];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int kk = 0; kk < 6; ++kk)
-      xf[t][kk] = *reinterpret_cast<const uint4*>(
-          xs + (a.xpk ? ((t * 6 + kk) * 64 + lane) * 8 : (t * 16 + (lane & 15)) * XS + 8 * (lane >> 4) + kk * 32));
-  __builtin_amdgcn_sched_barrier(0);
-  f32x4_t acc[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int kk = 0; kk < 6; ++kk)
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[kk]),
-                                                       __builtin_bit_cast(bf16x8_t, xf[t][kk]), acc[t], 0, 0, 0);
-  TS_MARK(1);
-  // lane: C[n0 + 4 (lane >> 4) + i][t * 16 + (lane & 15)], i = 0..3
-  float* dst = a.st.qkvp + (size_t)ks * a.st.max_streams * (3 * D) + n0 + 4 * (lane >> 4);
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int b = t * 16 + (lane & 15);
-    if (b < B) *reinterpret_cast<float4*>(dst + (size_t)b * (3 * D)) = make_float4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
-  }
-  TS_SAVE(1, a.layer, blockIdx.x + gridDim.x * blockIdx.y);
-}
-static_assert(3 * D == 4 * 16 * 36, "qkv_ksplit: 36 blocks of 64 rows");
-
-template <typename TW>
-static bool qkv_ksplit(int B, int kvdtype);  // defined with the B-dependent kernel choice below
+// (round 2-5: c_attn at 9 <= B <= 32 as four K-slice partials summed by the attention, the block's
+// operand slice shared through LDS -- faster launched kernel by kernel on the null stream (B = 32
+// 149.6 vs 154.3 us/step), slower under the HIP-graph replay every production path uses (B = 32
+// t = 0 / 384 / 768: 103.8 / 130.5 / 160.6 vs 101.5 / 127.3 / 155.5 us/step); option "ksplit",
+// off since round 3, removed in round 6 with its kernel. The fp32 parity mode keeps its K split:
+// ar_qkv_ksplit_f32_kernel.)
 
 // mlp c_proj (K = 3072) split into YCOPIES K slices of 768: 4x the blocks of the unsplit GEMM;
 // each slice's partial goes to its pending copy (plain stores, deterministic), folded into x by
@@ -2049,7 +1959,7 @@ static void launch_mproj_split(const GemvArgs& a, hipStream_t s) {
   static_assert(DFF == YCOPIES * 768, "one pending copy per K slice");
   dim3 grid((a.N + 15) / 16, YCOPIES), block(256);
   GemvArgs b = a;
-  if (YCOPIES == 4 && grid.x % 2 == 0 && !(opts().exp & 16)) {  // XCD-aligned order (xmap 1): 1-D grid
+  if (YCOPIES == 4 && grid.x % 2 == 0) {  // XCD-aligned order (xmap 1): 1-D grid
     b.xmap = 1;
     grid = dim3(grid.x * 4);
   }
@@ -2117,8 +2027,6 @@ __global__ __launch_bounds__(256) void ar_mfma_ln_kernel(GemvArgs a) {
         for (int j = 0; j < 3; ++j)
           ya[i < YR ? i : 0][c][j] = *reinterpret_cast<const float4*>(a.yacc + ((size_t)b * YCOPIES + c) * D + j * 256 + lane * 4);
   }
-  const bf16_t* __restrict__ W = reinterpret_cast<const bf16_t*>(a.W);
-  const int wrow = min(n0 + (lane & 15), a.N - 1);
   const int k0 = wave * 192 + 8 * (lane >> 4);
   float4 g[3];  // gamma ahead of the weights (the first LayerNorm waits for it)
 #pragma unroll
@@ -2128,8 +2036,7 @@ __global__ __launch_bounds__(256) void ar_mfma_ln_kernel(GemvArgs a) {
 #pragma unroll
   for (int kk = 0; kk < 6; ++kk)  // fragment-packed weights (a.Wf): 6 contiguous KB per wave
     wf[kk] = *reinterpret_cast<const uint4*>(
-        a.Wf ? reinterpret_cast<const bf16_t*>(a.Wf) + (((size_t)(n0 >> 4) * (K / 32) + wave * 6 + kk) * 64 + lane) * 8
-             : W + (size_t)wrow * K + k0 + kk * 32);
+        reinterpret_cast<const bf16_t*>(a.Wf) + (((size_t)(n0 >> 4) * (K / 32) + wave * 6 + kk) * 64 + lane) * 8);
   if constexpr (MODE == 7) {
     // commit the previous step's select (ar_embed_select_kernel's argmax_commit, B <= 2 IN 5's shadow
     // records); reduction and record select unconditional so that the granule loads stay up front
@@ -2665,7 +2572,7 @@ static void launch_f32b(const GemvArgs& a, hipStream_t s) {
   // two column tiles per block when one per block would put more than 256 blocks on the chip
   // (round 5, B = 32 t = 384-639: 200.9 vs 210.9 us/step, c_fc 7.58 -> 6.37 us, lm_head 7.27 -> 6.40,
   // mlp c_proj with its h slice staged once per block; option exp bit 8192: one tile per block)
-  const bool ct2 = nt1 && K == 768 && (a.N / 16) * nbr * (KTOT / K) > 256 && !(opts().exp & 8192);
+  const bool ct2 = nt1 && K == 768 && (a.N / 16) * nbr * (KTOT / K) > 256;
   dim3 grid((a.N + 15) / 16, nbr, KTOT / K), block(K / 192 * 64);
   if constexpr (K == 768) {
     if (ct2) {
@@ -2716,24 +2623,17 @@ static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_
   dim3 grid(ns_max, N_HEAD, B);
   // (round 4, measured slower: 16 waves and 256-key tiles for the one-split blocks at B <= 8, B = 8
   // t = 384-639 fp8 KV 103.9 vs 98.3 us/step, bf16 KV 109.6 vs 100.1)
-  if (nw8 && !qkv && kvdtype == LVX_DTYPE_BF16)  // 8 waves, 128-key tiles: twice the KV bytes in flight per block
+  if (qkv && kvdtype != LVX_DTYPE_F32) return;  // (no such path: the K split is the fp32 parity mode's)
+  if (nw8 && kvdtype == LVX_DTYPE_BF16)  // 8 waves, 128-key tiles: twice the KV bytes in flight per block
     hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2, 8>), grid, dim3(512), 0, s, st, l, ns_max, direct, selcopy);
   // (round 5, measured slower: 3 / 4 fp8 KV tiles in flight per wave at B = 8, t = 384-639 99.2 / 100.1
   // vs 98.0 us/step)
-  else if (nw8 && !qkv && kvdtype == LVX_DTYPE_FP8)
+  else if (nw8 && kvdtype == LVX_DTYPE_FP8)
     hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t, 2, 8>), grid, dim3(512), 0, s, st, l, ns_max, direct, selcopy);
   // (round 4, fp32 KV at B = 32, measured slower: 8 waves with 128-key tiles 212.6, 3 tiles in flight
   // per wave 218.0 vs 211.7 us/step)
-  else if (qkv && kvdtype == LVX_DTYPE_F32)  // fp32 parity mode: ar_qkv_ksplit_f32_kernel's partials
+  else if (qkv)  // fp32 parity mode: ar_qkv_ksplit_f32_kernel's partials (the only K-split c_attn)
     hipLaunchKernelGGL((ar_attn_v2_kernel<float, 2, 4, true>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
-  else if (qkv && kvdtype == LVX_DTYPE_BF16 && nw8)  // (ksplit with ln_max < B <= 8: the same 8-wave blocks)
-    hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2, 8, true>), grid, dim3(512), 0, s, st, l, ns_max, direct, selcopy);
-  else if (qkv && kvdtype == LVX_DTYPE_FP8 && nw8)  // K-slice partials, the 8-wave blocks of fp8 KV at B <= 16
-    hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t, 2, 8, true>), grid, dim3(512), 0, s, st, l, ns_max, direct, selcopy);
-  else if (qkv && kvdtype == LVX_DTYPE_FP8)  // c_attn left K-slice partials (qkv_ksplit)
-    hipLaunchKernelGGL((ar_attn_v2_kernel<fp8_t, 2, 4, true>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
-  else if (qkv)
-    hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2, 4, true>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
   else if (kvdtype == LVX_DTYPE_BF16)
     hipLaunchKernelGGL((ar_attn_v2_kernel<bf16_t, 2, 4>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
   else if (kvdtype == LVX_DTYPE_FP8)
@@ -2817,25 +2717,6 @@ static bool fused_mlp(int B) {
   return sizeof(TW) == 2 && opts().fuse_mlp && B <= 2 && !use_mfma<TW>(B);
 }
 
-// c_attn as K-slice partials summed by the attention: batched bf16 steps on the v2 kernels with the
-// rows kernel before c_attn (9 <= B <= 32), bf16 or fp8 KV. Option "ksplit", off by default since
-// round 3: with the steps replayed as HIP graphs (bench.py's default stream since round 3) the
-// one-launch c_attn is faster at every B and position measured (tools/step_sweep.py, graph replay,
-// us/step: B = 32 t = 0 / 384 / 768: 101.5 / 127.3 / 155.5 vs 103.8 / 130.5 / 160.6; B = 24 115.8 vs
-// 119.1; B = 16 110.8 vs 112.2; fp8 KV B = 12 / 16 / 32 103.6 / 105.4 / 110.1 vs 105.3 / 107.3 / 111.8);
-// launched one by one on the null stream it had measured faster (B = 16 123.4 vs 126.3, B = 32
-// 149.6 vs 154.3): the K split pays only against launch gaps. Bit-identical either way.
-// option ksplit (default 0, Opts in lvx_internal.h):
-template <typename TW>
-static bool qkv_ksplit(int B, int kvdtype) {
-  return opts().ksplit && use_mfma<TW>(B) && !use_bt<TW>(B) && B > MFMA_LN_MAX && B <= 32 &&
-         (kvdtype == LVX_DTYPE_BF16 || kvdtype == LVX_DTYPE_FP8) && !(opts().exp & 1);
-}
-static void launch_qkv_ksplit(const GemvArgs& a, hipStream_t s) {
-  if (a.B <= 16) hipLaunchKernelGGL(ar_qkv_ksplit_kernel<1>, dim3(36, 4), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(ar_qkv_ksplit_kernel<2>, dim3(36, 4), dim3(256), 0, s, a);
-}
-
 template <typename TW>
 static bool use_f32b(int B) {
   return sizeof(TW) == 4 && opts().f32b && B >= MFMA_BATCH_MIN && B <= 64;
@@ -2916,43 +2797,40 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
   // step at t = 128 / 640): bf16 KV B = 12 104.3 / 113.0 -> 95.4 / 107.7, B = 16 107.1 / 126.7 ->
   // 97.4 / 119.0; fp8 KV B = 12 103.2 / 110.3 -> 95.4 / 108.4, B = 16 104.2 / 111.5 -> 96.1 / 109.2.
   // At B = 8 (64 blocks) one split loses at long histories (fp8 KV 102.4 -> 105.7 at t = 640 while
-  // 98.1 -> 92.5 at t = 128): B <= 8 keeps the split-KV attention + merge. Option exp bit 32 restores
-  // the two splits at 9 <= B <= 16 (A/B).
+  // 98.1 -> 92.5 at t = 128): B <= 8 keeps the split-KV attention + merge.
   // 5 <= B <= 8: one split too, in 8-wave blocks (128-key tiles: twice the KV bytes in flight per
   // block, 40-64 blocks); tools/step_sweep.py, fp8 KV, B = 8, t = 128 / 640 / 896: 98.0 / 102.3 / 104.2
   // -> 92.6 / 102.8 / 106.5 us (bf16 KV 98.7 / 105.9 / 108.5 -> 95.1 / 105.3 / 108.8): ~1 % over a
-  // 1,024-token utterance; at B = 4 it loses (91.9 / 94.5 / 95.5 -> 87.6 / 96.3 / 100.8). Option exp
-  // bit 64 restores the split-KV attention + merge kernel at 5 <= B <= 8. fp8 KV (half the bytes per
+  // 1,024-token utterance; at B = 4 it loses (91.9 / 94.5 / 95.5 -> 87.6 / 96.3 / 100.8). fp8 KV (half the bytes per
   // key) keeps the 8-wave blocks up to B = 16: B = 12 / 16, t = 128 / 640 / 896: 95.8 / 108.3 / 114.8 ->
   // 97.0 / 105.5 / 109.6 and 95.8 / 109.6 / 115.5 -> 97.0 / 106.8 / 110.2 us; bf16 KV there loses
-  // (B = 16: 97.0 / 109.9 / 128.1 -> 100.8 / 112.5 / 130.5).
-  const bool a8 = mf && B >= 5 && (B <= 8 || (kvdtype == LVX_DTYPE_FP8 && (B <= 16 || ((opts().exp & 128) && B <= 32)))) && !(opts().exp & 64);
-  const int nsm = mf ? (((B > 8 && !(opts().exp & 32)) || a8) ? 1 : attn_ns_max(B)) : NSPLIT;
-  const bool pk = mf && !(opts().exp & 2);  // fragment-packed weights for the MFMA GEMMs (exp bit 2: row-major)
-  // fragment-packed operand rows on the v2 steps with the rows kernel (9 <= B <= 32; exp bit 4: row-major)
-  a.xpk = (mf && B > MFMA_LN_MAX && B <= 32 && !(opts().exp & 4)) ? 1 : 0;
+  // (B = 16: 97.0 / 109.9 / 128.1 -> 100.8 / 112.5 / 130.5). (The switches restoring the older forms,
+  // option exp bits 32 / 64 / 128, were removed in round 6.)
+  const bool a8 = mf && B >= 5 && (B <= 8 || (kvdtype == LVX_DTYPE_FP8 && B <= 16));
+  const int nsm = mf ? ((B > 8 || a8) ? 1 : attn_ns_max(B)) : NSPLIT;
+  // the MFMA GEMMs read the fragment-packed weight copies (a.Wf; round 6: the row-major reads of option
+  // exp bit 2, bit-identical and slower, removed)
+  // fragment-packed operand rows on the v2 steps with the rows kernel (9 <= B <= 32)
+  a.xpk = (mf && B > MFMA_LN_MAX && B <= 32) ? 1 : 0;
   a.layer = l;
-  a.epi_late = (opts().exp & 4096) ? 1 : 0;
   a.yacc = mf ? a.st.yacc : nullptr;
   a.yfx = fm ? a.st.yfx : nullptr;
   a.add_y = l > 0;
   switch (op) {
     case 0:
-      a.W = w.w_attn[l]; a.Wf = pk ? w.f_attn[l] : nullptr; a.N = 3 * D; a.ln_w = w.ln1[l];
+      a.W = w.w_attn[l]; a.Wf = w.f_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
       if (mf && l == 0 && a.defer_sel == 3) {  // the previous step's select + embedding in c_attn's prologue
         launch_mfma_ln<0, 7>(a, s);
       } else if (mf && l == 0 && a.defer_sel == 2) {  // embedding + the previous step's select, then c_attn
         hipLaunchKernelGGL(ar_embed_select_kernel<>, dim3(B), dim3(256), 0, s, a);
-        if (qkv_ksplit<TW>(B, kvdtype)) launch_qkv_ksplit(a, s);
-        else launch_mfma2<768, 0>(a, s);
+        launch_mfma2<768, 0>(a, s);
       } else if (mf && B <= MFMA_LN_MAX) {
         if (l == 0) launch_mfma_ln<0, 3>(a, s);
         else launch_mfma_ln<0, 4>(a, s);
       } else if (mf) {  // rows kernel: LayerNorm (layer 0: of the embedding; else of x + the MLP copies)
         if (l == 0) hipLaunchKernelGGL((ar_rows_kernel<3>), dim3(B), dim3(64), 0, s, a);
         else hipLaunchKernelGGL((ar_rows_kernel<4>), dim3(B), dim3(64), 0, s, a);
-        if (qkv_ksplit<TW>(B, kvdtype)) launch_qkv_ksplit(a, s);
-        else launch_mfma2<768, 0>(a, s);
+        launch_mfma2<768, 0>(a, s);
       } else if (l == 0 && a.defer_sel) {
         launch_gemv<TW, 768, 1, 2, 5, 0>(a, s);  // + the previous step's select
       } else if (l == 0) {
@@ -2965,10 +2843,10 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       break;
     case 1:
       launch_attn(a.st, kvdtype, B, l, s, nsm, (mf && nsm == 1) ? 1 + a.xpk : 0, (a.defer_sel == 1 || a.defer_sel == 3) && l == 0,
-                  qkv_ksplit<TW>(B, kvdtype), a8);
+                  false, a8);
       break;
     case 2:
-      a.W = w.w_aproj[l]; a.Wf = pk ? w.f_aproj[l] : nullptr; a.N = D;
+      a.W = w.w_aproj[l]; a.Wf = w.f_aproj[l]; a.N = D;
       if (mf) {
         if (B > MFMA_LN_MAX) a.add_y = 0;  // ar_rows_kernel<4> of this layer's c_attn folded them
         if (nsm > 1) launch_merge_bf16(a.st, B, nsm, s, a.xpk);  // nsm == 1: the attention wrote xn itself
@@ -2982,7 +2860,7 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       }
       break;
     case 3:
-      a.W = w.w_fc[l]; a.Wf = pk ? w.f_fc[l] : nullptr; a.N = DFF; a.ln_w = w.ln2[l];
+      a.W = w.w_fc[l]; a.Wf = w.f_fc[l]; a.N = DFF; a.ln_w = w.ln2[l];
       if (fm) {  // 16 h rows per block (192 blocks)
         const bf16_t* wfc = reinterpret_cast<const bf16_t*>(w.w_fc[l]);
         const bf16_t* wpk = reinterpret_cast<const bf16_t*>(w.w_mproj_pk[l]);
@@ -2998,13 +2876,13 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       }
       break;
     case 4:
-      a.W = w.w_mproj[l]; a.Wf = pk ? w.f_mproj[l] : nullptr; a.N = D;
+      a.W = w.w_mproj[l]; a.Wf = w.f_mproj[l]; a.N = D;
       if (fm) return false;
       if (mf) launch_mproj_split<6>(a, s);
       else launch_gemv<TW, 3072, 4, 2, 1, 1>(a, s);
       break;
     case 5:
-      a.W = w.w_lm; a.Wf = pk ? w.f_lm : nullptr; a.N = VOCAB; a.ln_w = w.lnf;
+      a.W = w.w_lm; a.Wf = w.f_lm; a.N = VOCAB; a.ln_w = w.lnf;
       if (mf && B <= MFMA_LN_MAX) {
         launch_mfma_ln<3, 4>(a, s);
       } else if (mf) {

@@ -671,11 +671,10 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   else if (n == "codec_g2") o.codec_g2 = value != 0;
   else if (n == "codec_skinny") o.codec_skinny = value != 0;
   else if (n == "codec_g3") o.codec_g3 = value != 0;
-  else if (n == "codec_g3f") o.codec_g3f = std::min(std::max(value, 0), 2);
+  else if (n == "codec_g3f") o.codec_g3f = value == 1 ? 1 : 2;  // 1: the exact-fp32 kernel (a test oracle)
   else if (n == "codec_exp") o.codec_exp = value;
   else if (n == "exp") o.exp = value;
   else if (n == "f32b") o.f32b = value != 0;
-  else if (n == "ksplit") o.ksplit = value != 0;
   else if (n == "ln_max") o.ln_max = std::min(std::max(value, 2), 8);
   else return fail(LVX_E_NAME, "unknown option " + n);
   ++c->opt_epoch;  // this context's captured kernels change (checked in cached_graph)

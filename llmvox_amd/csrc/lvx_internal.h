@@ -36,9 +36,8 @@ struct Opts {
   int bt = 1;            // 1: batched v3 for 32 < B <= 64; 2: v3 for every batched B (cross-check); 0: off
   int codec_g2 = 1, codec_skinny = 1, codec_g3 = 1, codec_g3f = 2;  // codec GEMM kernels (cross-checks)
   int codec_exp = 0;     // codec A/B bits (bit-identical variants)
-  int exp = 0;           // AR A/B bits (bit-identical variants, tests/test_gpu_batched.py, test_gpu_f32b.py)
+  int exp = 0;           // AR cross-check bits (fp32 tiles / one-launch forms: tests/test_gpu_f32b.py)
   int f32b = 1;          // fp32 batched steps on exact-fp32 MFMA; 0: the GEMV family
-  int ksplit = 0;        // batched bf16 c_attn as K-slice partials summed by the attention
   int ln_max = 8;        // batched steps with the LayerNorm fused into the GEMM prologue for B <= ln_max
 };
 const Opts& opts();  // the calling thread's bound options (the defaults when none is bound)

@@ -132,32 +132,10 @@ def test_v3_path_agrees_with_v2(eng, B):
     assert np.abs(got - ref).max() < 0.02 * np.abs(ref).max()
 
 
-@pytest.mark.parametrize("B,kv", [(9, "bf16"), (16, "bf16"), (17, "bf16"), (32, "bf16"), (12, "fp8"), (32, "fp8")])
-def test_qkv_ksplit_matches_one_launch_cattn(B, kv):
-    """9 <= B <= 32 (bf16 or fp8 KV): c_attn runs as K-slice partials summed by the attention, which
-    also appends the new key in the cache's dtype (ar_qkv_ksplit_kernel, option ksplit = 1) against
-    the one-launch c_attn with the KV append in its epilogue (the default). Same K-slice order and the
-    same conversion: tokens, margins and logits bit for bit, with permuted slots and ragged positions."""
-    from llmvox_amd.engine import build_engine
-    e = build_engine(0, "bf16", kv, max_streams=64, max_positions=512, max_codec_frames=256)
-    try:
-        texts = _texts(B, 96, seed=11)
-        order = list(np.random.default_rng(B).permutation(B))
-        prefix = set(range(0, B, 3))
-        res = []
-        for ks in (1, 0):
-            e.set_option("ksplit", ks)
-            res.append(_run(e, order, texts, prefix, 40, 56))
-        np.testing.assert_array_equal(res[0][0], res[1][0])
-        np.testing.assert_array_equal(res[0][1], res[1][1])
-    finally:
-        e.close()
-
-
 @pytest.mark.parametrize("B,kv", [(8, "bf16"), (8, "fp8"), (6, "bf16")])
 def test_rows_structure_at_small_b(B, kv):
-    """Option ln_max below B runs a small batch on the rows-kernel structure (rows kernel + K-split
-    c_attn + 16-row-tile GEMMs) instead of the GEMMs that normalise in their own prologue: another
+    """Option ln_max below B runs a small batch on the rows-kernel structure (rows kernel + c_attn
+    + 16-row-tile GEMMs) instead of the GEMMs that normalise in their own prologue: another
     summation order, so the logits agree to bf16 rounding and the tokens where the margin allows."""
     from llmvox_amd.engine import build_engine
     e = build_engine(0, "bf16", kv, max_streams=64, max_positions=512, max_codec_frames=256)
@@ -177,71 +155,23 @@ def test_rows_structure_at_small_b(B, kv):
         e.close()
 
 
-@pytest.mark.parametrize("B,bit", [(8, 2), (32, 2), (12, 4), (32, 4)])
-def test_fragment_packed_weights_match_row_major(B, bit):
-    """The batched MFMA GEMMs read an MFMA-fragment-packed copy of the bf16 weights (option exp bit 2
-    reads the row-major matrices) and, at 9 <= B <= 32, operand rows their producers store
-    fragment-packed (exp bit 4: row-major rows): the same products in the same order, bit for bit."""
-    from llmvox_amd.engine import build_engine
-    e = build_engine(0, "bf16", "bf16", max_streams=64, max_positions=512, max_codec_frames=256)
-    try:
-        e.set_option("fuse_mlp", 0)  # the ragged prefix may run B <= 2 rows: no fp32 atomics there
-        texts = _texts(B, 64, seed=5)
-        order = list(np.random.default_rng(B + 1).permutation(B))
-        res = []
-        for exp in (0, bit):
-            e.set_option("exp", exp)
-            res.append(_run(e, order, texts, set(range(0, B, 4)), 24, 40))
-        e.set_option("exp", 0)
-        e.set_option("fuse_mlp", 1)
-        np.testing.assert_array_equal(res[0][0], res[1][0])
-        np.testing.assert_array_equal(res[0][1], res[1][1])
-    finally:
-        e.close()
-
-
 @pytest.mark.parametrize("S", [12, 20])
 def test_fragment_packed_rows_with_odd_engine_size(S):
     """max_streams not a multiple of 16: the fragment-packed operand rows (xn, xb, hb) are
-    written and read in whole 16-row tiles, so the engine allocates them rounded up to 16 rows. B = S
-    with packed rows must equal row-major rows (exp bit 4) bit for bit, and nothing may fault."""
+    written and read in whole 16-row tiles, so the engine allocates them rounded up to 16 rows. The S
+    streams of an S-slot engine must decode bit for bit as the same streams in a 32-slot engine (rows
+    are independent of the engine's size and of their batch position), and nothing may fault. (Round 6:
+    the row-major operand rows this was compared with, option exp bit 4, were removed.)"""
     from llmvox_amd.engine import build_engine
-    e = build_engine(0, "bf16", "bf16", max_streams=S, max_positions=256, max_codec_frames=256)
-    try:
-        e.set_option("fuse_mlp", 0)
-        texts = _texts(S, 64, seed=S)
-        order = list(np.random.default_rng(S).permutation(S))
-        res = []
-        for exp in (0, 4):
-            e.set_option("exp", exp)
+    texts = _texts(S, 64, seed=S)
+    order = list(np.random.default_rng(S).permutation(S))
+    res = []
+    for slots in (S, 32):
+        e = build_engine(0, "bf16", "bf16", max_streams=slots, max_positions=256, max_codec_frames=256)
+        try:
+            e.set_option("fuse_mlp", 0)
             res.append(_run(e, order, texts, set(range(0, S, 3)), 20, 36))
-        e.set_option("exp", 0)
-        e.set_option("fuse_mlp", 1)
-        np.testing.assert_array_equal(res[0][0], res[1][0])
-        np.testing.assert_array_equal(res[0][1], res[1][1])
-    finally:
-        e.close()
-
-
-@pytest.mark.parametrize("B", [4, 17, 32])
-def test_xcd_aligned_tile_order_matches_grid_order(B):
-    """Round 3: c_proj (16-row batch tiles, B > 16) and mlp c_proj (four K slices) launch as 1-D grids
-    ordered so that each XCD runs one batch tile / K slice (its L2 fetches only that part of the
-    operand rows); option exp bit 16 restores the 2-D grid order. Same tiles, same arithmetic: bit for
-    bit, ragged batch, permuted slots."""
-    from llmvox_amd.engine import build_engine
-    e = build_engine(0, "bf16", "bf16", max_streams=64, max_positions=512, max_codec_frames=256)
-    try:
-        e.set_option("fuse_mlp", 0)
-        texts = _texts(B, 64, seed=11)
-        order = list(np.random.default_rng(B + 3).permutation(B))
-        res = []
-        for exp in (0, 16):
-            e.set_option("exp", exp)
-            res.append(_run(e, order, texts, set(range(0, B, 4)), 24, 40))
-        e.set_option("exp", 0)
-        e.set_option("fuse_mlp", 1)
-        np.testing.assert_array_equal(res[0][0], res[1][0])
-        np.testing.assert_array_equal(res[0][1], res[1][1])
-    finally:
-        e.close()
+        finally:
+            e.close()
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    np.testing.assert_array_equal(res[0][1], res[1][1])

@@ -6,7 +6,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 export PYTHONPATH=.
 O=gpurun_out/fp32t; mkdir -p $O
-SPEC=${SPEC:-}  # an option set for step_sweep (e.g. exp=8192)
+SPEC=${SPEC:-}  # an option set for step_sweep (e.g. exp=8)
 for w in ${WS:-fp32 bf16}; do
   LVX_SWEEP_W=$w timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d $O/$w -o run --output-format csv -- python3 tools/step_sweep.py ${B:-32} ${P0:-384} $SPEC > $O/$w.log 2>&1 || { echo FAIL $w; tail -20 $O/$w.log; exit 1; }
   find $O/$w -name "*kernel_stats.csv" -exec cp {} $O/${w}_stats.csv \;
