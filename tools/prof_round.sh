@@ -1,19 +1,21 @@
 #!/bin/bash
 # Round measurement refresh (round 2+; TAG defaults to the current round): PMC passes over the driver's default bench command
 # (configs[2], --steps 20: the roofline probe at KV position 2,560), kernel-trace stats of it, and
-# the bench line itself. Outputs under gpurun_out/$TAG; copy the summaries to profiles/.
+# the bench line itself (BENCH_ARGS; configs[4]: ARGS="--config 4 ..." KEY=bf16/kvfp8/B8/P512
+# CKEY=fp8/F2048/L256 BENCH_ARGS="--config 4 --steps 20 --warmup 5"). Outputs under gpurun_out/$TAG;
+# copy the summaries to profiles/.
 #   FETCH_SIZE and WRITE_SIZE passes  -> tools/pmc_traffic.py  -> pmc_traffic.json
 #   SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE pass -> tools/pmc_codec.py -> pmc_codec.json
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 export PYTHONPATH=.
-TAG=${TAG:-r05}
+TAG=${TAG:-r06}
 O=gpurun_out/$TAG; mkdir -p $O
 # PMC passes launch the steps one by one on the null stream (--null-stream): with the default
 # side-stream HIP-graph replay, rocprofv3 --pmc segfaults in its own thread (profiles/r03/pmc_segv_graph_replay.log);
 # per-dispatch counters do not depend on how the dispatch was submitted
 ARGS=${ARGS:-"--steps 20 --warmup 0 --no-cpu-baseline --no-parity-line"}
-PARGS=${PARGS:-"$ARGS --null-stream"}
+PARGS=${PARGS:-"$ARGS --null-stream --no-dist-world1"}
 KEY=${KEY:-bf16/kvbf16/B32/P512}
 CKEY=${CKEY:-bf16/F8192/L256}
 run() { # tag, timeout, rocprof args..., -- cmd
@@ -34,6 +36,6 @@ find $O/kt -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
 python3 tools/probe_trace.py $(find $O/kt -name "*kernel_trace.csv" | head -1) > $O/probe_trace.txt || exit 1
 cat $O/probe_trace.txt
 rm -rf $O/kt
-timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.jsonl 2> $O/bench.err || { echo BENCH_FAIL; tail -20 $O/bench.err; exit 1; }
+timeout -k 10 400 python bench.py ${BENCH_ARGS:---gpus 1 --steps 20 --warmup 5} > $O/bench.jsonl 2> $O/bench.err || { echo BENCH_FAIL; tail -20 $O/bench.err; exit 1; }
 tail -c 600 $O/bench.jsonl
 echo PROF_OK
