@@ -33,6 +33,12 @@ for B in Bs:
         res.append((tok.cpu(), mar.cpu(), lg.cpu()))
     e.set_option(opt, 0)
     same = all(torch.equal(a, b) for a, b in zip(*res))
-    print(f"B={B:2d} {opt}={val}: {'bit-identical' if same else 'DIFFERENT'}", flush=True)
+    extra = ""
+    if not same:  # how far apart: token agreement and the final logits
+        (t0, _, l0), (t1, _, l1) = res
+        extra = (f" (tokens equal {float((t0 == t1).float().mean()):.4f}, first differing step "
+                 f"{int((t0 != t1).any(0).float().argmax()) if (t0 != t1).any() else -1}, "
+                 f"max |dlogit| {float((l0 - l1).abs().max()):.3g} of max |logit| {float(l0.abs().max()):.3g})")
+    print(f"B={B:2d} {opt}={val}: {'bit-identical' if same else 'DIFFERENT'}{extra}", flush=True)
     bad += not same
 sys.exit(1 if bad else 0)

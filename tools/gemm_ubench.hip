@@ -171,15 +171,19 @@ int main() {
   for (size_t i = 0; i < h.size(); ++i) h[i] = 0x3c00 + (unsigned short)((i * 2654435761u >> 7) & 0xff);  // ~[0.0078, 0.016)
   CK(hipMemcpy(A, h.data(), h.size() * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(W, h.data(), (size_t)2304 * 3584 * 2, hipMemcpyHostToDevice));
-  {
-    const int N = 2304, K = 768;  // pwconv1: bias + GELU (erf), bf16 output
-    run<128, 192, 2, 32, 8, 2>("fp32 out", A, W, C, M, N, K);
-    run<128, 192, 2, 32 | 64, 8, 2>("bf16 2-B stores", A, W, C, M, N, K);
-    run<128, 192, 2, 32 | 64 | 128, 8, 2>("GELU + bf16 2-B", A, W, C, M, N, K);
-    run<128, 192, 2, 32 | 64 | 512, 8, 2>("fast act + bf16 2-B", A, W, C, M, N, K);
-    run<128, 192, 2, 32 | 256, 8, 2>("bf16 via LDS 16-B", A, W, C, M, N, K);
-    run<128, 192, 2, 32 | 256 | 128, 8, 2>("GELU + bf16 LDS 16-B", A, W, C, M, N, K);
-    run<128, 192, 2, 32 | 256 | 512, 8, 2>("fast act + LDS 16-B", A, W, C, M, N, K);
+  // round 6: tile shapes for the 1.5-round quantisation of pwconv1 (768 tiles of 128 x 192 on 512 slots
+  // of 2 blocks per CU) and pwconv2 (256 tiles, one block per CU), fp32 output, both k32 sub-steps' reads first
+  for (int which = 0; which < 2; ++which) {
+    const int N = which ? 768 : 2304, K = which ? 2304 : 768;
+    run<128, 192, 2, 32, 8, 2>("128x192 (current)", A, W, C, M, N, K);
+    run<128, 192, 3, 32, 8, 1>("128x192 3-stage 1/CU", A, W, C, M, N, K);
+    run<64, 192, 2, 32, 8, 2>("64x192", A, W, C, M, N, K);
+    run<64, 192, 3, 32, 8, 2>("64x192 3-stage", A, W, C, M, N, K);
+    run<128, 96, 2, 32, 4, 2>("128x96 4 waves", A, W, C, M, N, K);
+    run<128, 96, 2, 32, 4, 3>("128x96 4 waves occ3", A, W, C, M, N, K);
+    run<256, 192, 2, 32, 8, 1>("256x192", A, W, C, M, N, K);
+    run<128, 384, 2, 32, 8, 1>("128x384", A, W, C, M, N, K);
+    run<64, 384, 2, 32, 8, 2>("64x384", A, W, C, M, N, K);
   }
   return 0;
 }
