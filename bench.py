@@ -739,6 +739,7 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
     gathered (a list, tests only): on rank 0, what the async gather delivered for each timed chunk, as
     [rank][S, samples] host tensors in issue order (tests/test_gpu_rccl.py)."""
     from llmvox_amd.parallel import ChunkGather, gather_pcm
+    from llmvox_amd.streams import side_stream
     n_plan_chunks = mine.shape[1] // chunk
     dev = eng.device
     slots = torch.arange(S, dtype=torch.int32, device=dev)
@@ -755,7 +756,8 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
     # 228.1-228.3k, configs[1] 13.40-13.44k vs 12.90-12.96k, configs[4] 79.4k vs 76.7-77.0k, the
     # fp32 parity line 143.8k vs 142.6k (profiles/r04/codec_overlap_ab.txt). --serial-codec: the
     # codec after the AR on one stream. tok_plan / pcm are double-buffered for the overlap.
-    codec_stream = torch.cuda.Stream(device=dev) if codec_overlap else torch.cuda.current_stream(dev)
+    # (a side stream checked to run beside the decode stream: llmvox_amd/streams.py)
+    codec_stream = side_stream(dev, [None]) if codec_overlap else torch.cuda.current_stream(dev)
     tok_bufs = [tok_plan, torch.zeros_like(tok_plan)]
     pcm_bufs = [pcm, torch.empty_like(pcm)]
     ev_ar = [torch.cuda.Event(), torch.cuda.Event()]
@@ -771,7 +773,7 @@ def run_chunks(eng, mine, S, chunk, K, Wm, reset_every=0, dist=None, rank=0, wor
     # and waited for (host poll) before the PCM buffer is written again: neither the decode nor the
     # codec queue ever holds the collective (round 4 put it on the codec stream, and N > 1 fell back
     # to the serial schedule)
-    gather = (ChunkGather(dist, rank, world, torch.cuda.Stream(device=dev), keep=gathered is not None)
+    gather = (ChunkGather(dist, rank, world, side_stream(dev, [None, codec_stream]), keep=gathered is not None)
               if (dist is not None and codec_overlap) else None)
     gpending = [False, False]
 

@@ -30,6 +30,7 @@ from typing import Callable, Deque, Dict, List, Optional
 import numpy as np
 
 from . import config as C
+from .streams import side_stream
 
 
 def _cfg(config, key, default):
@@ -560,7 +561,9 @@ class FusedScheduler:
         dev = engine.device
         self.cuda = torch.device(dev).type == "cuda"
         self.overlap = bool(overlap)
-        self.codec_stream = (torch.cuda.Stream(device=dev) if codec_stream else (stream or torch.cuda.current_stream(dev))) \
+        # the codec's stream is checked to run beside the decode stream (streams.side_stream: two streams
+        # on one hardware queue run in order, and the overlap would be silently lost)
+        self.codec_stream = (side_stream(dev, [stream]) if codec_stream else (stream or torch.cuda.current_stream(dev))) \
             if (self.overlap and self.cuda) else None
         self.take = self.cuda and hasattr(engine, "take_errors")
         self.codec_take = hasattr(engine, "take_errors")  # (host-synchronous decodes: any engine with the words)

@@ -249,3 +249,25 @@ def test_codec_error_word_fails_only_its_group(handler, overlap):
     for st in (a, b):
         sch.close_stream(st)
     sch.close()
+
+
+def test_side_stream_runs_beside_the_decode_stream():
+    """streams.side_stream: the codec / gather streams are pool streams checked to run concurrently with
+    the decode stream (with GPU_MAX_HW_QUEUES hardware queues, torch's pool streams share queues round
+    robin and two streams on one queue run in order: a codec stream there lost the overlap, the idle
+    first chunk taking 3.6 instead of 1.4 ms). The probe's negative control: a stream is never beside
+    itself (its event queues behind the spin kernel)."""
+    from llmvox_amd.streams import runs_beside, side_stream
+    base = torch.cuda.Stream()
+    assert not runs_beside(base, base)
+    s = side_stream(base.device, [base])
+    assert s != base and runs_beside(s, base)
+
+
+def test_scheduler_codec_stream_runs_beside_its_decode_stream(handler):
+    from llmvox_amd.streams import runs_beside
+    dec = torch.cuda.Stream()
+    for _ in range(4):  # fresh schedulers draw fresh pool streams; none may share the decode stream's queue
+        sch = S.FusedScheduler(handler.engine, max_chunk=32, overlap=True, stream=dec)
+        assert runs_beside(sch.codec_stream, dec)
+        sch.close()
