@@ -8,6 +8,6 @@ mkdir -p gpurun_out
 export PYTHONPATH=.
 timeout -k 10 600 python -u -m pytest tests/ -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/tests.log 2>&1
 rc=$?; tail -2 gpurun_out/tests.log; [ $rc = 0 ] || exit $rc
-TAG=${TAG:-r05} bash tools/prof_round.sh || exit 1
+TAG=${TAG:-r06} bash tools/prof_round.sh || exit 1
 bash tools/gpu_round_lines.sh || exit 1
 echo FINAL_OK
