@@ -624,7 +624,7 @@ def first_chunk_latency(eng, reps=12, overlap=True):
     return statistics.median(lat)
 
 
-def first_chunk_latency_loaded(eng, busy=31, reps=34, max_chunk=64, seed=99, overlap=True):
+def first_chunk_latency_loaded(eng, busy=31, reps=34, max_chunk=32, seed=99, overlap=True):
     """p50 first-chunk latency UNDER LOAD (reference: a replica's first chunk is
     produced while the other replica decodes, streaming_server.py:357-376): a fresh stream joins a
     FusedScheduler that is already decoding `busy` streams (continuous batching, chunks of up to
@@ -1259,7 +1259,7 @@ def main():
             "p50_first_chunk_latency_loaded_ms": round(p50_loaded[0], 3) if p50_loaded else None,
             "first_chunk_latency_loaded": ({"p50_ms": round(p50_loaded[0], 3), "p90_ms": round(p50_loaded[1], 3),
                                             "max_ms": round(p50_loaded[2], 3), "joins": p50_loaded[3],
-                                            "busy_streams": min(31, eng.max_streams - 1), "max_chunk": 64,
+                                            "busy_streams": min(31, eng.max_streams - 1), "max_chunk": 32,
                                             "note": "a fresh stream joining a FusedScheduler already decoding the "
                                                     "busy streams; enqueue -> first 3,200-sample dump on the host"}
                                            if p50_loaded else None),

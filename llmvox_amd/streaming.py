@@ -543,7 +543,7 @@ class FusedScheduler:
     without graphs and serialise with every other stream, so the service gives each device one.
     """
 
-    def __init__(self, engine, max_chunk: int = 64, max_rows: Optional[int] = None, to_bytes: bool = True,
+    def __init__(self, engine, max_chunk: int = 32, max_rows: Optional[int] = None, to_bytes: bool = True,
                  overlap: bool = False, stop_rule=None, waiter=None, tail: int = 8, stream=None,
                  codec_stream: bool = True):
         import torch
