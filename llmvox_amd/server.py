@@ -332,8 +332,12 @@ class TTSService:
                 w.sched.close()
 
 
-def create_app(service):
-    """FastAPI app with the reference's /tts contract (TTSRequest {text} -> octet-stream)."""
+def create_app(service, cors: bool = True):
+    """FastAPI app with the reference's /tts contract (TTSRequest {text} -> octet-stream), its root
+    info endpoint and its CORS policy (every origin, streaming_server.py:97-104, so a browser client
+    on another origin can stream; ``cors=False`` leaves it off). The reference's /voicechat,
+    /multimodalchat and /vlmschat differ from /tts only in the producer (ASR / multimodal LLM,
+    out of scope): their speech path is this one."""
     from fastapi import FastAPI, HTTPException
     from fastapi.responses import StreamingResponse
     from pydantic import BaseModel
@@ -342,6 +346,15 @@ def create_app(service):
         text: str
 
     app = FastAPI(title="llmvox_amd streaming TTS")
+    if cors:
+        from fastapi.middleware.cors import CORSMiddleware
+        app.add_middleware(CORSMiddleware, allow_origins=["*"], allow_credentials=True,
+                           allow_methods=["*"], allow_headers=["*"])
+
+    @app.get("/")
+    def root():  # streaming_server.py:665-672
+        return {"message": "Streaming TTS API", "usage": 'POST /tts with {"text": "Your question or prompt here"}',
+                "version": "1.0.0"}
 
     @app.post("/tts")
     def tts(request: TTSRequest):

@@ -32,6 +32,12 @@ def test_tts_endpoint_streams_f32le_chunks():
     assert svc.texts == ["hello world."]
     assert client.post("/tts", json={}).status_code == 422  # TTSRequest requires text
     assert client.get("/health").json()["ok"] is True
+    root = client.get("/").json()  # the reference's info endpoint (streaming_server.py:665-672)
+    assert root["message"] == "Streaming TTS API" and root["usage"].startswith("POST /tts")
+    r = client.options("/tts", headers={"Origin": "http://example.org", "Access-Control-Request-Method": "POST"})
+    assert r.status_code == 200 and r.headers["access-control-allow-origin"] in ("*", "http://example.org")
+    assert "access-control-allow-origin" not in TestClient(create_app(svc, cors=False)).get(
+        "/", headers={"Origin": "http://example.org"}).headers
 
 
 @pytest.mark.gpu
