@@ -164,7 +164,7 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
  *   "defer_select" 1: the greedy select is committed by the next step's first kernel (B <= 2 and
  *                     4 <= B <= 8: c_attn layer 0 reduces lm_head's granules; larger B: ar_embed_select);
  *                     2: as 1 but 4 <= B <= 8 through ar_embed_select; 0: ar_argmax_kernel after every
- *                     lm_head (bit-identical results: tests/test_gpu_select.py);
+ *                     lm_head (bit-identical results with "l0q" 0: tests/test_gpu_select.py);
  *   "fuse_mlp"     1: bf16, B <= 2: c_fc + gelu + mlp c_proj in one kernel (2^-32 fixed-point int64
  *                     atomics: exact sums, reproducible run to run); 0: the two GEMV kernels;
  *   "bt"           1: batched path v3 for 32 < B <= 64; 2: v3 for every batched B; 0: never;
@@ -187,7 +187,12 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
  *   "f32b"         1: fp32 weights, 3 <= B <= 64: batched steps on exact-fp32 MFMA (ar_f32b_kernel);
  *                     0: the fp32 GEMV family (same ids against the reference: tests/test_gpu_f32b.py);
  *   "ln_max"       (2..8, default 8) largest B whose batched GEMMs normalise in their own prologue;
- *                  larger B run the rows kernel + batched GEMM structure. */
+ *                  larger B run the rows kernel + batched GEMM structure;
+ *   "l0q"          1: bf16 weights, ln_max < B <= 32 with the deferred select: layer 0's c_attn from
+ *                     table rows precomputed at lvx_finalize (text / codebook / position x ln_1 x W),
+ *                     inside the embedding + select kernel (one launch less per step; the operand is
+ *                     not rounded to bf16, so the sums differ from the GEMM's in the last bits:
+ *                     tests/test_gpu_batched.py); 0: the embedding + select kernel, then the GEMM. */
 int lvx_set_option(lvx_ctx* ctx, const char* name, int value);
 /* Enable/disable HIP-graph replay of lvx_ar_step for a given B (default on). */
 int lvx_set_graphs(lvx_ctx* ctx, int enable);

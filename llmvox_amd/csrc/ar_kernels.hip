@@ -102,6 +102,11 @@ struct GemvArgs {
                          // 2: batched step, the next step's embedding rows kernel reduces the logits
   int xmap;              // ar_mfma2_kernel launched as a 1-D grid with the XCD-aligned tile order:
                          // 1 = mlp c_proj (K slice = XCD mod 4), 2 = c_proj batch tiles (tile = XCD mod 2)
+  // layer 0's c_attn as table rows (ArWeights q0_*; ar_embed_select_kernel QKV)
+  const float* q0_text;
+  const float* q0_code;
+  const float* q0_pos;
+  const float* q0_g;
 };
 
 // ---------------------------------------------------------------------------------
@@ -1510,7 +1515,7 @@ constexpr int MFMA_BATCH_MIN = 3;  // smallest B on the batched MFMA path (measu
 // ---------------------------------------------------------------------------------
 // x row of the embedding (a2-a4) for control record ri, lane layout k = j * 256 + lane * 4:
 // normalize(cat(text_table[id], codebook[prev] | 0 at position 0), eps 1e-8) + wpe[pos]
-__device__ __forceinline__ void embed_row(const GemvArgs& a, int4 ri, int lane, float4 (&v)[3]) {
+__device__ __forceinline__ void embed_row(const GemvArgs& a, int4 ri, int lane, float4 (&v)[3], float* rden = nullptr) {
   if (ri.x < 0) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1538,6 +1543,7 @@ __device__ __forceinline__ void embed_row(const GemvArgs& a, int4 ri, int lane, 
     ss += (v[j].x * v[j].x + v[j].y * v[j].y) + (v[j].z * v[j].z + v[j].w * v[j].w);
   }
   const float den = fmaxf(sqrtf(wave_sum(ss)), 1e-8f);
+  if (rden) *rden = 1.0f / den;
 #pragma unroll
   for (int j = 0; j < 3; ++j)
     v[j] = make_float4(v[j].x / den + pe[j].x, v[j].y / den + pe[j].y, v[j].z / den + pe[j].z, v[j].w / den + pe[j].w);
@@ -1595,10 +1601,17 @@ __global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_rows_kernel(GemvArgs a
 // row's control records), wave 0 commits and builds the operand row.
 // F32OUT (the batched fp32 parity mode): the LayerNorm'd row in fp32 into st.h (ar_rows_kernel<6>'s
 // output, read by ar_qkv_ksplit_f32_kernel)
-template <bool F32OUT = false>
+// QKV (bf16, B > ln_max, option l0q): layer 0's c_attn is done here from the table rows of ArWeights
+// q0_* (src/model.py:47-50 on the input of :222-226): q / k / v[n] = rstd * ((Tt[t][n] + Tc[c][n]) / den
+// + Tp[p][n] - mean * G[n]). Tt[t] and Tp[p] (t, p follow from the control records, not from the select)
+// are loaded with the logits, Tc[c] of the token just selected by all four waves while wave 0 loads the
+// embedding rows for (den, mean, rstd): the c_attn GEMM launch and its boundary go (the operand is
+// never rounded to bf16, so the sums differ from the GEMM's in the last bits)
+template <bool F32OUT = false, bool QKV = false>
 __global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_embed_select_kernel(GemvArgs a) {
   __shared__ float sv[4], sv2[4];
   __shared__ int si[4];
+  __shared__ float4 sst;  // QKV: {1 / den, mean, rstd} of the row, wave 0 -> all
   const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   TS_DECL;
   TS_MARK(0);
@@ -1606,12 +1619,29 @@ __global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_embed_select_kernel(Ge
   const int2 rx = a.st.rowx[b];  // {plan step j, text id of step j + 1}
   const unsigned pend = a.st.selrow[b];
   float4 g[3];  // LN gamma first: the reduction's wait for the logits then covers it too
+  if constexpr (!QKV) {
 #pragma unroll
-  for (int j = 0; j < 3; ++j) g[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
+    for (int j = 0; j < 3; ++j) g[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
+  }
   const float4* lg = reinterpret_cast<const float4*>(a.st.logits + (size_t)b * VOCAB);
   float4 lv[VOCAB / 1024];
 #pragma unroll
   for (int k = 0; k < VOCAB / 1024; ++k) lv[k] = lg[k * 256 + tid];
+  constexpr int NQ = QKV ? 3 * D / 256 : 1;  // outputs n = tid + 256 i of the row
+  float tq[NQ], tpo[NQ], gq[NQ];
+  if constexpr (QKV) {  // this step's (text id, position) as the commit below sets them
+    const bool tk = pend && ri.x >= 0;
+    const int p1 = min(max(tk ? ri.y + 1 : ri.y, 0), a.st.max_pos - 1);
+    const int t1 = tk ? rx.y : ri.z;
+    const float* tt = a.q0_text + (size_t)(t1 < 0 ? 384 : t1) * (3 * D);
+    const float* tp = a.q0_pos + (size_t)p1 * (3 * D);
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      tq[i] = tt[tid + 256 * i];
+      tpo[i] = tp[tid + 256 * i];
+      gq[i] = a.q0_g[tid + 256 * i];
+    }
+  }
   Best bt{-INFINITY, -INFINITY, 0x7fffffff};
 #pragma unroll
   for (int k = 0; k < VOCAB / 1024; ++k) {
@@ -1625,16 +1655,16 @@ __global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_embed_select_kernel(Ge
   TS_MARK(1);
   if (lane == 0) { sv[wave] = bt.v; sv2[wave] = bt.v2; si[wave] = bt.i; }
   __syncthreads();
-  if (wave != 0) return;
+  if (!QKV && wave != 0) return;
   const bool take = pend && ri.x >= 0;
-  if (take) {
+  if (take) {  // (QKV: every wave merges the four partials, wave 0 commits)
     Best r{sv[0], sv2[0], si[0]};
 #pragma unroll
     for (int w = 1; w < 4; ++w) r = best_merge(r, Best{sv[w], sv2[w], si[w]});
     r = softmax_ties(a.st.logits + (size_t)b * VOCAB, r, lane);
     const int s = ri.x, p = ri.y + 1, j = rx.x;
     const int4 rn = make_int4(s, min(p, a.st.max_pos - 1), rx.y, min(max(r.i, 0), VOCAB - 1));
-    if (lane == 0) {  // argmax_commit
+    if (wave == 0 && lane == 0) {  // argmax_commit
       if (p >= a.st.max_pos) atomicOr(a.st.err, 1);
       if (j < a.st.plan_stride) {
         a.st.tok_plan[(size_t)b * a.st.plan_stride + j] = r.i;
@@ -1647,25 +1677,66 @@ __global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_embed_select_kernel(Ge
     }
     ri = rn;
   }
-  if (lane == 0) a.st.selrow[b] = 1u;  // this step's lm_head leaves the next pending select
-  float4 v[3];
-  embed_row(a, ri, lane, v);
+  if (wave == 0 && lane == 0) a.st.selrow[b] = 1u;  // this step's lm_head leaves the next pending select
+  float tc[NQ];
+  if constexpr (QKV) {
+    const float* tcp = a.q0_code + (size_t)min(max(ri.w, 0), VOCAB - 1) * (3 * D);
 #pragma unroll
-  for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = v[j];
-  wave_ln_regs(v, g);
-  if constexpr (F32OUT) {
+    for (int i = 0; i < NQ; ++i) tc[i] = tcp[tid + 256 * i];
+  }
+  if (wave == 0) {
+    float4 v[3];
+    float rden = 0.f;
+    embed_row(a, ri, lane, v, QKV ? &rden : nullptr);
 #pragma unroll
-    for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.h + (size_t)b * D + j * 256 + lane * 4) = v[j];
-  } else {
-    uint2* dst = reinterpret_cast<uint2*>(a.st.xn + (size_t)b * D);
+    for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = v[j];
+    if constexpr (QKV) {  // (mean, rstd) as wave_ln_regs computes them
+      float sm = 0.f;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      if (a.xpk) *reinterpret_cast<uint2*>(a.st.xn + xfrag(b, j * 256 + lane * 4, D)) = pack4_bf16(v[j]);
-      else dst[j * 64 + lane] = pack4_bf16(v[j]);
+      for (int j = 0; j < 3; ++j) sm += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+      const float mean = wave_sum(sm) * (1.0f / D);
+      float qs = 0.f;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const float4 d = make_float4(v[j].x - mean, v[j].y - mean, v[j].z - mean, v[j].w - mean);
+        qs += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+      }
+      const float rstd = 1.0f / sqrtf(wave_sum(qs) * (1.0f / D) + 1e-5f);
+      if (lane == 0) sst = make_float4(rden, mean, rstd, 0.f);
+    } else {
+      wave_ln_regs(v, g);
+      if constexpr (F32OUT) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.h + (size_t)b * D + j * 256 + lane * 4) = v[j];
+      } else {
+        uint2* dst = reinterpret_cast<uint2*>(a.st.xn + (size_t)b * D);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          if (a.xpk) *reinterpret_cast<uint2*>(a.st.xn + xfrag(b, j * 256 + lane * 4, D)) = pack4_bf16(v[j]);
+          else dst[j * 64 + lane] = pack4_bf16(v[j]);
+        }
+      }
+    }
+    // the plan load for the next text id last: waiting for it earlier held the embedding loads
+    if (take && lane == 0) a.st.rowx[b] = make_int2(rx.x + 1, plan_tok(a.st, b, rx.x + 2));
+  }
+  if constexpr (QKV) {
+    __syncthreads();
+    const float4 st = sst;
+    const float cz = ri.y == 0 ? 0.f : 1.f;  // position 0: the codebook half of the input is zero
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      const int n = tid + 256 * i;
+      const float o = ri.x < 0 ? 0.f : st.z * (((tq[i] + cz * tc[i]) * st.x + tpo[i]) - st.y * gq[i]);
+      if (n < D) {
+        a.st.q[(size_t)b * D + n] = o;
+      } else if (ri.x >= 0) {  // K / V append at the row's (slot, pos), as c_attn's epilogue
+        const int c = (n - D) % D, which = (n - D) / D;
+        const int head = c / HD, d = c - head * HD;
+        store_kv(a, which, kv_at(0, a.st.kv_chunks, a.st.max_streams, ri.x, head, ri.y) + d, o);
+      }
     }
   }
-  // the plan load for the next text id last: waiting for it earlier held the embedding loads
-  if (take && lane == 0) a.st.rowx[b] = make_int2(rx.x + 1, plan_tok(a.st, b, rx.x + 2));
   TS_SAVE(7, 0, b);
 }
 
@@ -2642,6 +2713,52 @@ static void launch_attn(const ArState& st, int kvdtype, int B, int l, hipStream_
     hipLaunchKernelGGL((ar_attn_v2_kernel<float, 2, 4>), grid, dim3(256), 0, s, st, l, ns_max, direct, selcopy);
 }
 
+// ArWeights q0_* tables (lvx_finalize, once): out[r][n] = sum_k<K (src[r][k] * g[k0 + k]) * W[n][k0 + k],
+// W = layer 0's bf16 c_attn weight [2304][768]; 64 x 64 output tiles, K staged 16 at a time through LDS
+// (fp32 FMAs in k order)
+__global__ __launch_bounds__(256) void q0_table_kernel(const float* __restrict__ src, int rows, int K, int k0,
+                                                       const float* __restrict__ g, const bf16_t* __restrict__ W,
+                                                       float* __restrict__ out) {
+  __shared__ float As[16][65], Bs[16][65];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int r0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  float acc[4][4] = {};
+  for (int kt = 0; kt < K; kt += 16) {
+    for (int e = threadIdx.x; e < 1024; e += 256) {
+      const int rr = e >> 4, kk = e & 15, r = r0 + rr;
+      As[kk][rr] = r < rows ? src[(size_t)r * K + kt + kk] * g[k0 + kt + kk] : 0.f;
+      Bs[kk][rr] = bf16_to_f32(W[(size_t)(n0 + rr) * D + k0 + kt + kk]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(As[kk][ty * 4 + i], Bs[kk][tx * 4 + j], acc[i][j]);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = r0 + ty * 4 + i;
+    if (r < rows)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) out[(size_t)r * (3 * D) + n0 + tx * 4 + j] = acc[i][j];
+  }
+}
+
+void ar_launch_q0_tables(const ArWeights& w, int max_pos, float* text, float* code, float* pos, hipStream_t s) {
+  static_assert((3 * D) % 64 == 0 && TEXT_DIM % 16 == 0 && SPEECH_DIM % 16 == 0 && D % 16 == 0, "q0 tiles");
+  const bf16_t* W = reinterpret_cast<const bf16_t*>(w.w_attn[0]);
+  const float* g = w.ln1[0];
+  hipLaunchKernelGGL(q0_table_kernel, dim3(3 * D / 64, (TEXT_VOCAB + 63) / 64), dim3(256), 0, s, w.text_table,
+                     TEXT_VOCAB, TEXT_DIM, 0, g, W, text);
+  hipLaunchKernelGGL(q0_table_kernel, dim3(3 * D / 64, (VOCAB + 63) / 64), dim3(256), 0, s, w.codebook, VOCAB,
+                     SPEECH_DIM, TEXT_DIM, g, W, code);
+  hipLaunchKernelGGL(q0_table_kernel, dim3(3 * D / 64, (max_pos + 63) / 64), dim3(256), 0, s, w.wpe, max_pos, D, 0,
+                     g, W, pos);
+}
+
 // one op of the decode step, with the B-dependent kernel choice (shared by the step and the probes)
 // op: 0 c_attn (layer 0: + embedding) 1 attention 2 c_proj (+ split merge) 3 c_fc 4 mlp c_proj 5 lm_head
 template <typename TW>
@@ -2821,6 +2938,9 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       a.W = w.w_attn[l]; a.Wf = w.f_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
       if (mf && l == 0 && a.defer_sel == 3) {  // the previous step's select + embedding in c_attn's prologue
         launch_mfma_ln<0, 7>(a, s);
+      } else if (mf && l == 0 && a.defer_sel == 2 && opts().l0q && a.q0_text && B > MFMA_LN_MAX) {
+        // embedding + the previous step's select + c_attn from the q0 tables, one launch
+        hipLaunchKernelGGL((ar_embed_select_kernel<false, true>), dim3(B), dim3(256), 0, s, a);
       } else if (mf && l == 0 && a.defer_sel == 2) {  // embedding + the previous step's select, then c_attn
         hipLaunchKernelGGL(ar_embed_select_kernel<>, dim3(B), dim3(256), 0, s, a);
         launch_mfma2<768, 0>(a, s);
@@ -2911,6 +3031,10 @@ static GemvArgs make_args(const ArWeights& w, const ArState& st, int kvdtype, in
   a.codebook = w.codebook;
   a.wpe = w.wpe;
   a.emb_row = emb_row;
+  a.q0_text = w.q0_text;
+  a.q0_code = w.q0_code;
+  a.q0_pos = w.q0_pos;
+  a.q0_g = w.q0_g;
   return a;
 }
 

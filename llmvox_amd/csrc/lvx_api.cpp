@@ -461,6 +461,33 @@ int lvx_finalize(lvx_ctx* c) {
   UP_W(c->H("lm_head.weight"), w.w_lm);
   if (c->cfg.weight_dtype == LVX_DTYPE_BF16) {
     UP_W(pack_frag(c->H("lm_head.weight"), VOCAB, D), w.f_lm);
+    // layer 0's c_attn as table rows (ArWeights q0_*): G on the host over the bf16 weights (as fc_gsum),
+    // the three tables by a device GEMM over the uploaded bf16 c_attn weight
+    const std::vector<float>& wa = c->H("transformer.h.0.attn.c_attn.weight");
+    const std::vector<float>& g1 = c->H("transformer.h.0.ln_1.weight");
+    std::vector<float> gq(3 * D);
+    for (int n = 0; n < 3 * D; ++n) {
+      double acc = 0.0;
+      for (int k = 0; k < D; ++k) {
+        const uint32_t hb = (uint32_t)f32_to_bf16(wa[(size_t)n * D + k]) << 16;
+        float wv;
+        std::memcpy(&wv, &hb, 4);
+        acc += (double)g1[k] * (double)wv;
+      }
+      gq[n] = (float)acc;
+    }
+    if ((r = c->upload_f32(gq, &w.q0_g))) return r;
+    float *tt, *tc, *tp;
+    const int P = c->cfg.max_positions;
+    if ((r = c->dalloc(&tt, (size_t)TEXT_VOCAB * 3 * D)) || (r = c->dalloc(&tc, (size_t)VOCAB * 3 * D)) ||
+        (r = c->dalloc(&tp, (size_t)P * 3 * D)))
+      return r;
+    ar_launch_q0_tables(w, P, tt, tc, tp, nullptr);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipDeviceSynchronize());
+    w.q0_text = tt;
+    w.q0_code = tc;
+    w.q0_pos = tp;
   } else {
     UP_W(pack_frag32(c->H("lm_head.weight"), VOCAB, D), w.f_lm);
   }
@@ -676,6 +703,7 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   else if (n == "exp") o.exp = value;
   else if (n == "f32b") o.f32b = value != 0;
   else if (n == "ln_max") o.ln_max = std::min(std::max(value, 2), 8);
+  else if (n == "l0q") o.l0q = value != 0;
   else return fail(LVX_E_NAME, "unknown option " + n);
   ++c->opt_epoch;  // this context's captured kernels change (checked in cached_graph)
   return LVX_OK;

@@ -39,6 +39,8 @@ struct Opts {
   int exp = 0;           // AR cross-check bits (fp32 tiles / one-launch forms: tests/test_gpu_f32b.py)
   int f32b = 1;          // fp32 batched steps on exact-fp32 MFMA; 0: the GEMV family
   int ln_max = 8;        // batched steps with the LayerNorm fused into the GEMM prologue for B <= ln_max
+  int l0q = 1;           // bf16, B > ln_max: layer 0's q / k / v from the precomputed tables (ArWeights q0_*)
+                         // in the embedding + select kernel; 0: that kernel + the c_attn GEMM (cross-check)
 };
 const Opts& opts();  // the calling thread's bound options (the defaults when none is bound)
 struct OptScope {    // binds `o` to this thread until the scope ends
@@ -66,6 +68,15 @@ struct ArWeights {
   const float* fc_gsum[N_LAYER] = {};    // bf16 only: G[n] = sum_k ln_2.weight[k] * bf16(c_fc W[n][k]) (batched
                                          // c_fc: LayerNorm applied after the GEMM, ar_mfma2_kernel XM 1)
   const void* w_lm = nullptr;         // [4096][768]
+  // bf16 only: layer 0's c_attn as table rows (ar_embed_select_kernel QKV). The step's input row is
+  // x = cat(text_table[t], codebook[c]) / den + wpe[p] and c_attn multiplies LN1(x) = (x - mean) * rstd
+  // * g, so W . LN1(x) = rstd * (W . (x * g) - mean * G) with W . (x * g) = (Tt[t] + Tc[c]) / den + Tp[p]:
+  // Tt[t][n] = sum_k<256 g[k] W[n][k] text_table[t][k], Tc over k = 256.. 767 with the codebook, Tp with
+  // wpe (bf16 W, fp32 sums), G[n] = sum_k g[k] W[n][k]
+  const float* q0_text = nullptr;     // [386][2304]
+  const float* q0_code = nullptr;     // [4096][2304]
+  const float* q0_pos = nullptr;      // [max_positions][2304]
+  const float* q0_g = nullptr;        // [2304]
   // MFMA-fragment-packed copies for the batched GEMMs, one contiguous KB per wave-wide 16-B load of
   // the A operand: bf16 [N / 16][K / 32][64][8] for v_mfma_f32_16x16x32_bf16 (pack_frag); fp32
   // [N / 16][K / 16][64][4] for v_mfma_f32_16x16x4_f32 (pack_frag32, the fp32 parity mode)
@@ -129,6 +140,8 @@ int ar_probe(const ArWeights& w, const ArState& st, int wdtype, int kvdtype, int
 void ar_launch_rowinfo_init(const ArState& st, int B, hipStream_t s);
 void ar_launch_steps_end(const ArState& st, int wdtype, int B, hipStream_t s);  // deferred select: commit the last step
 int ar_select_probe(const ArWeights& w, const ArState& st, int B, int path, hipStream_t s);  // test hook
+// ArWeights::q0_text / q0_code / q0_pos from the bf16 c_attn weight of layer 0 (lvx_finalize)
+void ar_launch_q0_tables(const ArWeights& w, int max_pos, float* text, float* code, float* pos, hipStream_t s);
 void launch_set_slot(int32_t* pos, int32_t* prev, int slot, int p, int tok, hipStream_t s);
 void launch_err_take(int32_t* words, int mask_ar, int mask_codec, int32_t* out, hipStream_t s);
 void launch_text_embed(const float* table, const int64_t* ids, int n, float* out, int32_t* err, hipStream_t s);

@@ -136,11 +136,14 @@ def test_v3_path_agrees_with_v2(eng, B):
 def test_rows_structure_at_small_b(B, kv):
     """Option ln_max below B runs a small batch on the rows-kernel structure (rows kernel + c_attn
     + 16-row-tile GEMMs) instead of the GEMMs that normalise in their own prologue: another
-    summation order, so the logits agree to bf16 rounding and the tokens where the margin allows."""
+    summation order, so the logits agree to bf16 rounding and the tokens where the margin allows.
+    (Layer 0's c_attn as the GEMM on both sides, option l0q 0: the tables are held to it in
+    test_layer0_tables_agree_with_the_gemm.)"""
     from llmvox_amd.engine import build_engine
     e = build_engine(0, "bf16", kv, max_streams=64, max_positions=512, max_codec_frames=256)
     try:
         e.set_option("fuse_mlp", 0)
+        e.set_option("l0q", 0)
         texts = _texts(B, 64, seed=21)
         order = list(np.random.default_rng(B + 7).permutation(B))
         res = []
@@ -152,6 +155,40 @@ def test_rows_structure_at_small_b(B, kv):
         ref, got = res[0][1], res[1][1]
         assert np.abs(got - ref).max() < 0.02 * np.abs(ref).max()
     finally:
+        e.close()
+
+
+@pytest.mark.parametrize("B,kv", [(9, "bf16"), (16, "bf16"), (32, "bf16"), (32, "fp8")])
+def test_layer0_tables_agree_with_the_gemm(B, kv):
+    """Layer 0's c_attn from the q0 tables inside the embedding + select kernel (option l0q, B > 8)
+    against the embedding kernel + the c_attn GEMM, after a shared ragged prefix: the same step up to
+    the GEMM's bf16 rounding of the LayerNorm'd operand (the tables multiply it unrounded), so the
+    logits agree within the bf16 path's bound, every row's state advances alike, and one step's
+    tokens agree wherever the margin exceeds twice the logit difference."""
+    from llmvox_amd.engine import build_engine
+    e = build_engine(0, "bf16", kv, max_streams=32, max_positions=512, max_codec_frames=256)
+    try:
+        texts = _texts(B, 64, seed=29)
+        order = list(np.random.default_rng(B + 3).permutation(B))
+        pre = set(range(0, B, 3))
+        res = []
+        for q in (0, 1):  # the prefix on the GEMM form both times: one step apart
+            e.set_option("l0q", 0)
+            res.append(_run(e, order, texts, pre, 24, 1, between=lambda q=q: e.set_option("l0q", q)))
+        (t0, ref), (t1, got) = res
+        col = np.array([24 if r in pre else 0 for r in range(B)])  # the main step's column (text order)
+        np.testing.assert_array_equal(t1[:, :24][col == 24], t0[:, :24][col == 24])  # same prefix
+        d = np.abs(got - ref).max()
+        # bf16 KV: bf16 rounding; fp8 KV: a k / v value that moves by rounding can land on the next e4m3
+        # step, so the fp8 mode's own bound (0.15 against the reference, test_gpu_teacher_forced.py)
+        assert d < (0.02 if kv == "bf16" else 0.06) * np.abs(ref).max(), d
+        srt = np.sort(ref, axis=1)
+        sure = (srt[:, -1] - srt[:, -2]) > 2 * d
+        assert sure.any()
+        main0, main1 = t0[np.arange(B), col], t1[np.arange(B), col]
+        np.testing.assert_array_equal(main1[sure], main0[sure])
+    finally:
+        e.set_option("l0q", 1)
         e.close()
 
 

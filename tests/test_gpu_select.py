@@ -115,8 +115,11 @@ def test_batched_deferred_select_matches_argmax_kernel(eng_batched, B, ref_mode)
     c_attn layer 0 reduces lm_head's granules; larger B: the embedding rows kernel), ar_argmax_kernel
     after the last step. Against the argmax kernel after every lm_head (ref_mode 0) and, at B <= 8,
     against the embedding + select kernel (option defer_select 2). These paths have no arrival-order
-    sums: bit-equal, with one idle row."""
+    sums: bit-equal, with one idle row. (Layer 0's c_attn as the GEMM on every path, option l0q 0:
+    the argmax-kernel path has no table form; the l0q kernel's select is this same code, held to
+    the reference's picks by tests/test_gpu_teacher_forced.py at B = 32.)"""
     e = eng_batched
+    e.set_option("l0q", 0)
     slots = list(range(B))
     slots[B // 2] = -1
     calls = [3, 17, 1, 16]
@@ -145,6 +148,7 @@ def test_batched_deferred_select_matches_argmax_kernel(eng_batched, B, ref_mode)
         got = run()
     finally:
         e.set_option("defer_select", 1)
+        e.set_option("l0q", 1)
     live = [b for b in range(B) if b != B // 2]  # the idle row's logits are whatever its garbage x gives
     for a, b, name in zip(got, ref, ["tokens", "margins", "rowstep", "positions", "logits"]):
         if name == "logits":
