@@ -1601,7 +1601,7 @@ __global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_rows_kernel(GemvArgs a
 // row's control records), wave 0 commits and builds the operand row.
 // F32OUT (the batched fp32 parity mode): the LayerNorm'd row in fp32 into st.h (ar_rows_kernel<6>'s
 // output, read by ar_qkv_ksplit_f32_kernel)
-// QKV (bf16, B > ln_max, option l0q): layer 0's c_attn is done here from the table rows of ArWeights
+// QKV (bf16, B >= 4, option l0q): layer 0's c_attn is done here from the table rows of ArWeights
 // q0_* (src/model.py:47-50 on the input of :222-226): q / k / v[n] = rstd * ((Tt[t][n] + Tc[c][n]) / den
 // + Tp[p][n] - mean * G[n]). Tt[t] and Tp[p] (t, p follow from the control records, not from the select)
 // are loaded with the logits, Tc[c] of the token just selected by all four waves while wave 0 loads the
@@ -2938,7 +2938,7 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       a.W = w.w_attn[l]; a.Wf = w.f_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
       if (mf && l == 0 && a.defer_sel == 3) {  // the previous step's select + embedding in c_attn's prologue
         launch_mfma_ln<0, 7>(a, s);
-      } else if (mf && l == 0 && a.defer_sel == 2 && opts().l0q && a.q0_text && B > MFMA_LN_MAX) {
+      } else if (mf && l == 0 && a.defer_sel == 2 && opts().l0q && a.q0_text) {
         // embedding + the previous step's select + c_attn from the q0 tables, one launch
         hipLaunchKernelGGL((ar_embed_select_kernel<false, true>), dim3(B), dim3(256), 0, s, a);
       } else if (mf && l == 0 && a.defer_sel == 2) {  // embedding + the previous step's select, then c_attn
@@ -3045,6 +3045,11 @@ static bool ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B,
                       int pos, float* logits_dst, bool select, hipStream_t s) {
   GemvArgs a = make_args<TW>(w, st, kvdtype, B, emb_row);
   a.defer_sel = (select && !emb_row) ? (defer_select<TW>(B) ? 1 : defer_select_batched<TW>(B) ? (defer_select_ln<TW>(B) ? 3 : 2) : 0) : 0;
+  // 4 <= B <= 8 with layer 0's c_attn from the q0 tables (option l0q): the embedding + select kernel
+  // computes q / k / v itself, so the select moves there from c_attn's prologue (round 6, tools/
+  // b8_l0q_ab.sh: B = 8 fp8 KV t = 384-639 98.3 -> 96.3 us per step, bf16 KV 101.0 -> 99.0, B = 4 93.8
+  // -> 92.5; the reference-agreement measures unchanged, profiles/r06/b8_l0q_ab.txt)
+  if (a.defer_sel == 3 && opts().l0q && w.q0_text) a.defer_sel = 2;
   if (emb_row) hipLaunchKernelGGL(ar_row_state_kernel, dim3(1), dim3(1), 0, s, st, slot, pos);
   for (int l = 0; l < N_LAYER; ++l)
     for (int op = 0; op < 5; ++op) launch_op<TW>(op, a, w, l, kvdtype, B, s);

@@ -158,10 +158,12 @@ def test_rows_structure_at_small_b(B, kv):
         e.close()
 
 
-@pytest.mark.parametrize("B,kv", [(9, "bf16"), (16, "bf16"), (32, "bf16"), (32, "fp8")])
+@pytest.mark.parametrize("B,kv", [(4, "bf16"), (8, "fp8"), (9, "bf16"), (16, "bf16"), (32, "bf16"), (32, "fp8")])
 def test_layer0_tables_agree_with_the_gemm(B, kv):
-    """Layer 0's c_attn from the q0 tables inside the embedding + select kernel (option l0q, B > 8)
-    against the embedding kernel + the c_attn GEMM, after a shared ragged prefix: the same step up to
+    """Layer 0's c_attn from the q0 tables inside the embedding + select kernel (option l0q, B >= 4)
+    against the c_attn GEMM (B > 8: after the embedding kernel; 4 <= B <= 8: the GEMM whose prologue
+    commits the select from lm_head's granules and builds the embedding rows), after a shared ragged
+    prefix: the same step up to
     the GEMM's bf16 rounding of the LayerNorm'd operand (the tables multiply it unrounded), so the
     logits agree within the bf16 path's bound, every row's state advances alike, and one step's
     tokens agree wherever the margin exceeds twice the logit difference."""

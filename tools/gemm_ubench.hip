@@ -5,6 +5,7 @@
 // hipcc -O3 --offload-arch=gfx950 tools/gemm_ubench.hip -o tools/gemm_ubench && tools/gemm_ubench
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
@@ -171,6 +172,16 @@ int main() {
   for (size_t i = 0; i < h.size(); ++i) h[i] = 0x3c00 + (unsigned short)((i * 2654435761u >> 7) & 0xff);  // ~[0.0078, 0.016)
   CK(hipMemcpy(A, h.data(), h.size() * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(W, h.data(), (size_t)2304 * 3584 * 2, hipMemcpyHostToDevice));
+  if (getenv("UB_EPI")) {  // round 6 (2nd session): the production pwconv1 epilogue (bias-free GELU erf, bf16 out) vs fp32 out
+    const int N = 2304, K = 768;
+    run<128, 192, 2, 32, 8, 2>("128x192 fp32 out", A, W, C, M, N, K);
+    run<128, 192, 2, 32 | 64, 8, 2>("128x192 bf16 out", A, W, C, M, N, K);
+    run<128, 192, 2, 32 | 128, 8, 2>("128x192 gelu bf16", A, W, C, M, N, K);
+    run<128, 192, 2, 32 | 512, 8, 2>("128x192 gelu~ bf16", A, W, C, M, N, K);
+    run<128, 192, 2, 32 | 256 | 128, 8, 2>("128x192 gelu bf16 lds", A, W, C, M, N, K);
+    run<128, 192, 2, 32 | 8, 8, 2>("128x192 no store", A, W, C, M, N, K);
+    return 0;
+  }
   // round 6: tile shapes for the 1.5-round quantisation of pwconv1 (768 tiles of 128 x 192 on 512 slots
   // of 2 blocks per CU) and pwconv2 (256 tiles, one block per CU), fp32 output, both k32 sub-steps' reads first
   for (int which = 0; which < 2; ++which) {

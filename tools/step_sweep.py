@@ -40,4 +40,4 @@ for spec in sys.argv[3:] or [""]:
     us = statistics.median(ts)
     print(f"B={B} P={P0}.. [{spec}]: {us:7.1f} us/step  {B / us * 1e6:9.0f} tok/s", flush=True)
     for k, v in opts:
-        e.set_option(k, {"bt": 1, "defer_select": 1, "fuse_mlp": 1, "codec_g2": 1, "codec_g3": 1, "codec_skinny": 1, "f32b": 1, "ln_max": 8}.get(k, 0))
+        e.set_option(k, {"bt": 1, "defer_select": 1, "fuse_mlp": 1, "codec_g2": 1, "codec_g3": 1, "codec_skinny": 1, "f32b": 1, "ln_max": 8, "l0q": 1}.get(k, 0))
