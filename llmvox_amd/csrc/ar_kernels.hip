@@ -2807,6 +2807,13 @@ static bool defer_select(int B) {
   static_assert(LM_SEL_BLOCKS <= LM_MAX_BLOCKS && LM_SEL_BLOCKS % 64 == 0, "deferred select granules");
   return opts().defer_select && B <= 2 && !use_mfma<TW>(B);
 }
+// B <= 2 with layer 0's c_attn from the q0 tables (option l0q, bf16): the deferred select runs in
+// ar_embed_select_kernel (defer_sel 2) and lm_head leaves plain logits; the call's last step is
+// committed by ar_argmax_kernel
+template <typename TW>
+static bool l0q_small(int B, bool tables) {
+  return sizeof(TW) == 2 && tables && opts().l0q && defer_select<TW>(B);
+}
 template <typename TW>
 static bool use_f32b(int B);
 static bool f32b_qsplit(int B);
@@ -2951,6 +2958,8 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
         if (l == 0) hipLaunchKernelGGL((ar_rows_kernel<3>), dim3(B), dim3(64), 0, s, a);
         else hipLaunchKernelGGL((ar_rows_kernel<4>), dim3(B), dim3(64), 0, s, a);
         launch_mfma2<768, 0>(a, s);
+      } else if (l == 0 && a.defer_sel == 2 && a.q0_text) {  // B <= 2 with the q0 tables (l0q_small)
+        hipLaunchKernelGGL((ar_embed_select_kernel<false, true>), dim3(B), dim3(256), 0, s, a);
       } else if (l == 0 && a.defer_sel) {
         launch_gemv<TW, 768, 1, 2, 5, 0>(a, s);  // + the previous step's select
       } else if (l == 0) {
@@ -3008,7 +3017,7 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       } else if (mf) {
         hipLaunchKernelGGL((ar_rows_kernel<4>), dim3(B), dim3(64), 0, s, a);
         launch_mfma2<768, 3>(a, s);
-      } else if (a.defer_sel) {
+      } else if (a.defer_sel == 1) {
         if (fm) launch_gemv<TW, 768, 1, 2, 4, 9>(a, s);
         else launch_gemv<TW, 768, 1, 2, 0, 9>(a, s);
       } else if (fm) {
@@ -3050,6 +3059,9 @@ static bool ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B,
   // b8_l0q_ab.sh: B = 8 fp8 KV t = 384-639 98.3 -> 96.3 us per step, bf16 KV 101.0 -> 99.0, B = 4 93.8
   // -> 92.5; the reference-agreement measures unchanged, profiles/r06/b8_l0q_ab.txt)
   if (a.defer_sel == 3 && opts().l0q && w.q0_text) a.defer_sel = 2;
+  // B <= 2 (GEMV steps) likewise: the embedding + select kernel (one block per row, the full logits)
+  // with the table rows instead of c_attn layer 0's granule select + embedding prologue (round 6)
+  if (a.defer_sel == 1 && l0q_small<TW>(B, w.q0_text != nullptr)) a.defer_sel = 2;
   if (emb_row) hipLaunchKernelGGL(ar_row_state_kernel, dim3(1), dim3(1), 0, s, st, slot, pos);
   for (int l = 0; l < N_LAYER; ++l)
     for (int op = 0; op < 5; ++op) launch_op<TW>(op, a, w, l, kvdtype, B, s);
@@ -3163,9 +3175,10 @@ int ar_select_probe(const ArWeights& w, const ArState& st, int B, int path, hipS
   return 0;
 }
 
-void ar_launch_steps_end(const ArState& st, int wdtype, int B, hipStream_t s) {
-  const bool d = wdtype == LVX_DTYPE_BF16 ? defer_select<bf16_t>(B) : defer_select<float>(B);
-  const bool db = wdtype == LVX_DTYPE_BF16 ? defer_select_batched<bf16_t>(B) : defer_select_batched<float>(B);
+void ar_launch_steps_end(const ArState& st, int wdtype, int B, bool q0_tables, hipStream_t s) {
+  const bool tq = wdtype == LVX_DTYPE_BF16 && l0q_small<bf16_t>(B, q0_tables);  // (its select: full logits)
+  const bool d = !tq && (wdtype == LVX_DTYPE_BF16 ? defer_select<bf16_t>(B) : defer_select<float>(B));
+  const bool db = tq || (wdtype == LVX_DTYPE_BF16 ? defer_select_batched<bf16_t>(B) : defer_select_batched<float>(B));
   if (d) hipLaunchKernelGGL(ar_select_final_kernel, dim3(B), dim3(64), 0, s, st);
   else if (db) hipLaunchKernelGGL(ar_argmax_kernel, dim3(B), dim3(256), 0, s, st);
 }

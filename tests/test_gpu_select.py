@@ -59,8 +59,11 @@ def _run(e, B, slots, calls, graphs):
 @pytest.mark.parametrize("graphs", [True, False], ids=["graphs", "eager"])
 @pytest.mark.parametrize("B,slots", [(1, [2]), (2, [0, 3]), (2, [1, -1])], ids=["B1", "B2", "B2-idle"])
 def test_deferred_select_matches_argmax_kernel(eng, B, slots, graphs, fuse_mlp):
+    # (layer 0's c_attn as the GEMV on both paths, option l0q 0: with the q0 tables the select runs
+    # in the embedding + select kernel, held to this form by test_small_b_tables_agree_with_the_gemv)
     calls = [3, 17, 1, 16]
     eng.set_option("fuse_mlp", fuse_mlp)
+    eng.set_option("l0q", 0)
     try:
         eng.set_option("defer_select", 0)
         try:
@@ -70,6 +73,7 @@ def test_deferred_select_matches_argmax_kernel(eng, B, slots, graphs, fuse_mlp):
         got = _run(eng, B, slots, calls, graphs)
     finally:
         eng.set_option("fuse_mlp", 1)
+        eng.set_option("l0q", 1)
     if fuse_mlp == 0 or eng.weight_dtype == "fp32":  # no arrival-order sums on this path
         live = [b for b, s in enumerate(slots) if s >= 0]  # (an idle row's logits are not outputs)
         for a, b, name in zip(got, ref, ["tokens", "margins", "rowstep", "positions", "logits"]):
@@ -157,6 +161,43 @@ def test_batched_deferred_select_matches_argmax_kernel(eng_batched, B, ref_mode)
     n = sum(calls)
     assert got[2][B // 2] == 0 and (got[0][B // 2] == -7).all()
     assert all(got[2][b] == n for b in range(B) if b != B // 2)
+
+
+@pytest.mark.parametrize("B,slots", [(1, [2]), (2, [0, 3]), (2, [1, -1])], ids=["B1", "B2", "B2-idle"])
+def test_small_b_tables_agree_with_the_gemv(eng, B, slots):
+    """B <= 2, bf16 (round 6): layer 0's c_attn from the q0 tables inside the embedding + select kernel
+    (the select over the full logits, lm_head leaving plain logits, ar_argmax_kernel committing the
+    call's last step) against the GEMV whose prologue commits lm_head's granules (option l0q 0), over
+    several calls with graph replays and eager launches: the same state machine (plan steps, positions,
+    idle rows untouched), the tokens equal up to the first step whose margin is within the bf16 path's
+    noise, the graph replay bit-equal to the eager launches, and the logits within the bf16 bound."""
+    if eng.weight_dtype != "bf16":
+        pytest.skip("the q0 tables are a bf16-weight form")
+    calls = [3, 17, 1, 16]
+    eng.set_option("l0q", 0)
+    try:
+        ref = _run(eng, B, slots, calls, True)
+    finally:
+        eng.set_option("l0q", 1)
+    got = _run(eng, B, slots, calls, True)
+    eager = _run(eng, B, slots, calls, False)
+    for a, b, name in zip(eager, got, ["tokens", "margins", "rowstep", "positions", "logits"]):
+        np.testing.assert_array_equal(np.asarray(a), np.asarray(b), err_msg=f"eager vs graphs: {name}")
+    n = sum(calls)
+    tied = False
+    for b, s in enumerate(slots):
+        if s < 0:
+            assert got[2][b] == 0 and (got[0][b] == -7).all()
+            continue
+        assert got[2][b] == n and (got[0][b] >= 0).all()
+        close = np.nonzero(ref[1][b] < 0.05)[0]
+        k = close[0] if len(close) else n
+        tied |= bool(len(close))
+        np.testing.assert_array_equal(got[0][b, :k], ref[0][b, :k])
+    assert got[3] == ref[3]
+    if not tied:
+        live = [b for b, s in enumerate(slots) if s >= 0]
+        assert np.abs(got[4][live] - ref[4][live]).max() < 0.02 * np.abs(ref[4][live]).max()
 
 
 @pytest.mark.parametrize("B,slots", [(1, [2]), (2, [0, 3]), (2, [1, -1])], ids=["B1", "B2", "B2-idle"])
