@@ -161,11 +161,11 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
  * an option set on one context never changes another context's kernels; each call binds a snapshot
  * of its context's options, and the context drops its captured graphs on its next call after a
  * change). Defaults are the measured-faster variants:
- *   "defer_select" 1: the greedy select is committed by the next step's first kernel (B <= 2: c_attn
- *                     layer 0 reduces lm_head's granules; 4 <= B <= 8: the same with "l0q" 0, else
- *                     ar_embed_select; larger B: ar_embed_select); 2: 4 <= B <= 8 through ar_embed_select
- *                     with "l0q" 0 too; 0: ar_argmax_kernel after every lm_head (bit-identical results
- *                     with "l0q" 0: tests/test_gpu_select.py);
+ *   "defer_select" 1: the greedy select is committed by the next step's first kernel (bf16 with "l0q"
+ *                     1: ar_embed_select at every B; otherwise B <= 2 and 4 <= B <= 8: c_attn layer 0
+ *                     reduces lm_head's granules, larger B: ar_embed_select); 2: 4 <= B <= 8 through
+ *                     ar_embed_select with "l0q" 0 too; 0: ar_argmax_kernel after every lm_head
+ *                     (bit-identical results with "l0q" 0: tests/test_gpu_select.py);
  *   "fuse_mlp"     1: bf16, B <= 2: c_fc + gelu + mlp c_proj in one kernel (2^-32 fixed-point int64
  *                     atomics: exact sums, reproducible run to run); 0: the two GEMV kernels;
  *   "bt"           1: batched path v3 for 32 < B <= 64; 2: v3 for every batched B; 0: never;
@@ -189,11 +189,13 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
  *                     0: the fp32 GEMV family (same ids against the reference: tests/test_gpu_f32b.py);
  *   "ln_max"       (2..8, default 8) largest B whose batched GEMMs normalise in their own prologue;
  *                  larger B run the rows kernel + batched GEMM structure;
- *   "l0q"          1: bf16 weights, 4 <= B <= 32 with the deferred select: layer 0's c_attn from
+ *   "l0q"          1: bf16 weights, B <= 32 (not 3) with the deferred select: layer 0's c_attn from
  *                     table rows precomputed at lvx_finalize (text / codebook / position x ln_1 x W),
- *                     inside the embedding + select kernel (one launch less per step; the operand is
- *                     not rounded to bf16, so the sums differ from the GEMM's in the last bits:
- *                     tests/test_gpu_batched.py); 0: the embedding + select kernel, then the GEMM. */
+ *                     inside the embedding + select kernel (B > 8: one launch less per step; B <= 8:
+ *                     the step's first launch reads three table rows instead of weight slices; the
+ *                     operand is not rounded to bf16, so the sums differ from the GEMM's in the last
+ *                     bits: tests/test_gpu_batched.py, test_gpu_select.py); 0: the c_attn GEMM / GEMV
+ *                     (B > 8 after the embedding + select kernel; B <= 8 with the granule select). */
 int lvx_set_option(lvx_ctx* ctx, const char* name, int value);
 /* Enable/disable HIP-graph replay of lvx_ar_step for a given B (default on). */
 int lvx_set_graphs(lvx_ctx* ctx, int enable);

@@ -1601,7 +1601,7 @@ __global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_rows_kernel(GemvArgs a
 // row's control records), wave 0 commits and builds the operand row.
 // F32OUT (the batched fp32 parity mode): the LayerNorm'd row in fp32 into st.h (ar_rows_kernel<6>'s
 // output, read by ar_qkv_ksplit_f32_kernel)
-// QKV (bf16, B >= 4, option l0q): layer 0's c_attn is done here from the table rows of ArWeights
+// QKV (bf16, B <= 32 but 3, option l0q): layer 0's c_attn is done here from the table rows of ArWeights
 // q0_* (src/model.py:47-50 on the input of :222-226): q / k / v[n] = rstd * ((Tt[t][n] + Tc[c][n]) / den
 // + Tp[p][n] - mean * G[n]). Tt[t] and Tp[p] (t, p follow from the control records, not from the select)
 // are loaded with the logits, Tc[c] of the token just selected by all four waves while wave 0 loads the

@@ -39,7 +39,7 @@ struct Opts {
   int exp = 0;           // AR cross-check bits (fp32 tiles / one-launch forms: tests/test_gpu_f32b.py)
   int f32b = 1;          // fp32 batched steps on exact-fp32 MFMA; 0: the GEMV family
   int ln_max = 8;        // batched steps with the LayerNorm fused into the GEMM prologue for B <= ln_max
-  int l0q = 1;           // bf16, 4 <= B <= 32: layer 0's q / k / v from the precomputed tables (ArWeights q0_*)
+  int l0q = 1;           // bf16, B <= 32 (not 3): layer 0's q / k / v from the precomputed tables (ArWeights q0_*)
                          // in the embedding + select kernel; 0: that kernel + the c_attn GEMM (cross-check)
 };
 const Opts& opts();  // the calling thread's bound options (the defaults when none is bound)
