@@ -1740,6 +1740,116 @@ __global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_embed_select_kernel(Ge
   TS_SAVE(7, 0, b);
 }
 
+// B <= 2 GEMV steps with the deferred granule select (defer_sel 1) and option l0q (bf16): layer 0's
+// c_attn from the q0 tables, as ar_embed_select_kernel<false, true> computes it, over 9 blocks of 256
+// outputs instead of one block per row: every block reduces the rows' lm_head granules (as the GEMV's
+// IN 5 prologue does; block 0 commits the select and leaves the new records in the shadow arrays that
+// attention layer 0 copies back), loads its 256-column slices of Tt[t], Tp[p], G and Tc[c], and one
+// wave per row builds the embedding row for (den, mean, rstd) (block 0 also stores x). Round 6: the
+// single-block form cost the B = 1 step 6.6 us per launch (kernel trace) against 4.6-4.8 for its
+// other kernels.
+__global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_q0_gran_kernel(GemvArgs a) {
+  constexpr int BM = 2;  // rows (the GEMV steps' B <= 2)
+  __shared__ int4 rn_s[BM];
+  __shared__ float4 sst[BM];  // {1 / den, mean, rstd} per row
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int n = blockIdx.x * 256 + tid;  // this thread's output column (3 * D = 9 x 256)
+  const int B = a.B;
+  TS_DECL;
+  TS_MARK(0);
+  // every wave (row clamped: no load under a branch), as the IN 5 prologue: the record, the
+  // {step, next text id}, the pending flag and the row's granules
+  const int rb = min(wave, B - 1);
+  const int4 ri = a.st.rowinfo[rb];
+  const int2 rx = a.st.rowx[rb];
+  const unsigned pend = *a.st.selp;
+  LmGran lmg;
+  lmg_issue(a.st, rb, lane, lmg);
+  // this step's (text id, position) of every row as the commit sets them (they follow from the
+  // records, not from the select): the Tt / Tp / G slices go out in the next round trip
+  int4 rib[BM];
+  int2 rxb[BM];
+#pragma unroll
+  for (int b = 0; b < BM; ++b) {
+    rib[b] = a.st.rowinfo[min(b, B - 1)];
+    rxb[b] = a.st.rowx[min(b, B - 1)];
+  }
+  float tq[BM], tpo[BM];
+#pragma unroll
+  for (int b = 0; b < BM; ++b) {
+    const bool tk = pend && rib[b].x >= 0;
+    const int p1 = min(max(tk ? rib[b].y + 1 : rib[b].y, 0), a.st.max_pos - 1);
+    const int t1 = tk ? rxb[b].y : rib[b].z;
+    tq[b] = a.q0_text[(size_t)(t1 < 0 ? 384 : t1) * (3 * D) + n];
+    tpo[b] = a.q0_pos[(size_t)p1 * (3 * D) + n];
+  }
+  const float gq = a.q0_g[n];
+  if (wave < B) {  // (wave-uniform) commit the previous step's greedy select of row `wave`
+    const Best r = softmax_ties(a.st.logits + (size_t)wave * VOCAB, lmg_reduce(lmg), lane);
+    const int sl = ri.x, j = rx.x, p = ri.y + 1;
+    const bool take = pend && sl >= 0;
+    const int4 rn = take ? make_int4(sl, min(p, a.st.max_pos - 1), rx.y, min(max(r.i, 0), VOCAB - 1)) : ri;
+    if (blockIdx.x == 0 && lane == 0) {
+      if (take) {
+        if (p >= a.st.max_pos) atomicOr(a.st.err, 1);
+        if (j < a.st.plan_stride) {
+          a.st.tok_plan[(size_t)wave * a.st.plan_stride + j] = r.i;
+          if (a.st.margin_plan) a.st.margin_plan[(size_t)wave * a.st.plan_stride + j] = r.v - r.v2;
+        }
+        a.st.prev[sl] = r.i;
+        a.st.pos[sl] = p;
+      }
+      a.st.rowx_n[wave] = make_int2(take ? j + 1 : j, 0);
+      a.st.rowinfo_n[wave] = rn;
+    }
+    if (lane == 0) rn_s[wave] = rn;
+  }
+  __syncthreads();
+  // the codebook slice of each row's new token (every thread) beside the embedding rows (one wave per row)
+  float tc[BM];
+#pragma unroll
+  for (int b = 0; b < BM; ++b) tc[b] = a.q0_code[(size_t)min(max(rn_s[min(b, B - 1)].w, 0), VOCAB - 1) * (3 * D) + n];
+  if (wave < B) {
+    const int4 rn = rn_s[wave];
+    float4 v[3];
+    float rden = 0.f;
+    embed_row(a, rn, lane, v, &rden);
+    if (blockIdx.x == 0) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)wave * D + j * 256 + lane * 4) = v[j];
+    }
+    float sm = 0.f;  // (mean, rstd) as wave_ln_regs computes them
+#pragma unroll
+    for (int j = 0; j < 3; ++j) sm += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+    const float mean = wave_sum(sm) * (1.0f / D);
+    float qs = 0.f;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const float4 d = make_float4(v[j].x - mean, v[j].y - mean, v[j].z - mean, v[j].w - mean);
+      qs += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(qs) * (1.0f / D) + 1e-5f);
+    if (lane == 0) sst[wave] = make_float4(rden, mean, rstd, 0.f);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < BM; ++b) {
+    if (b >= B) break;
+    const int4 rn = rn_s[b];
+    const float4 st = sst[b];
+    const float cz = rn.y == 0 ? 0.f : 1.f;  // position 0: the codebook half of the input is zero
+    const float o = rn.x < 0 ? 0.f : st.z * (((tq[b] + cz * tc[b]) * st.x + tpo[b]) - st.y * gq);
+    if (n < D) {
+      a.st.q[(size_t)b * D + n] = o;
+    } else if (rn.x >= 0) {  // K / V append at the row's (slot, pos), as c_attn's epilogue
+      const int c = (n - D) % D, which = (n - D) / D;
+      const int head = c / HD, d = c - head * HD;
+      store_kv(a, which, kv_at(0, a.st.kv_chunks, a.st.max_streams, rn.x, head, rn.y) + d, o);
+    }
+  }
+  TS_SAVE(7, 0, blockIdx.x);
+}
+
 // split-KV merge for the batched path: y[b] (bf16) into st.xn. NS = ns_max (the attention's split
 // count at this B): only the splits that can exist are loaded
 template <int NS>
@@ -2807,13 +2917,6 @@ static bool defer_select(int B) {
   static_assert(LM_SEL_BLOCKS <= LM_MAX_BLOCKS && LM_SEL_BLOCKS % 64 == 0, "deferred select granules");
   return opts().defer_select && B <= 2 && !use_mfma<TW>(B);
 }
-// B <= 2 with layer 0's c_attn from the q0 tables (option l0q, bf16): the deferred select runs in
-// ar_embed_select_kernel (defer_sel 2) and lm_head leaves plain logits; the call's last step is
-// committed by ar_argmax_kernel
-template <typename TW>
-static bool l0q_small(int B, bool tables) {
-  return sizeof(TW) == 2 && tables && opts().l0q && defer_select<TW>(B);
-}
 template <typename TW>
 static bool use_f32b(int B);
 static bool f32b_qsplit(int B);
@@ -2958,8 +3061,8 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
         if (l == 0) hipLaunchKernelGGL((ar_rows_kernel<3>), dim3(B), dim3(64), 0, s, a);
         else hipLaunchKernelGGL((ar_rows_kernel<4>), dim3(B), dim3(64), 0, s, a);
         launch_mfma2<768, 0>(a, s);
-      } else if (l == 0 && a.defer_sel == 2 && a.q0_text) {  // B <= 2 with the q0 tables (l0q_small)
-        hipLaunchKernelGGL((ar_embed_select_kernel<false, true>), dim3(B), dim3(256), 0, s, a);
+      } else if (l == 0 && a.defer_sel == 1 && opts().l0q && a.q0_text) {  // B <= 2, the q0 tables
+        hipLaunchKernelGGL(ar_q0_gran_kernel, dim3(3 * D / 256), dim3(256), 0, s, a);
       } else if (l == 0 && a.defer_sel) {
         launch_gemv<TW, 768, 1, 2, 5, 0>(a, s);  // + the previous step's select
       } else if (l == 0) {
@@ -3059,9 +3162,6 @@ static bool ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B,
   // b8_l0q_ab.sh: B = 8 fp8 KV t = 384-639 98.3 -> 96.3 us per step, bf16 KV 101.0 -> 99.0, B = 4 93.8
   // -> 92.5; the reference-agreement measures unchanged, profiles/r06/b8_l0q_ab.txt)
   if (a.defer_sel == 3 && opts().l0q && w.q0_text) a.defer_sel = 2;
-  // B <= 2 (GEMV steps) likewise: the embedding + select kernel (one block per row, the full logits)
-  // with the table rows instead of c_attn layer 0's granule select + embedding prologue (round 6)
-  if (a.defer_sel == 1 && l0q_small<TW>(B, w.q0_text != nullptr)) a.defer_sel = 2;
   if (emb_row) hipLaunchKernelGGL(ar_row_state_kernel, dim3(1), dim3(1), 0, s, st, slot, pos);
   for (int l = 0; l < N_LAYER; ++l)
     for (int op = 0; op < 5; ++op) launch_op<TW>(op, a, w, l, kvdtype, B, s);
@@ -3175,10 +3275,9 @@ int ar_select_probe(const ArWeights& w, const ArState& st, int B, int path, hipS
   return 0;
 }
 
-void ar_launch_steps_end(const ArState& st, int wdtype, int B, bool q0_tables, hipStream_t s) {
-  const bool tq = wdtype == LVX_DTYPE_BF16 && l0q_small<bf16_t>(B, q0_tables);  // (its select: full logits)
-  const bool d = !tq && (wdtype == LVX_DTYPE_BF16 ? defer_select<bf16_t>(B) : defer_select<float>(B));
-  const bool db = tq || (wdtype == LVX_DTYPE_BF16 ? defer_select_batched<bf16_t>(B) : defer_select_batched<float>(B));
+void ar_launch_steps_end(const ArState& st, int wdtype, int B, hipStream_t s) {
+  const bool d = wdtype == LVX_DTYPE_BF16 ? defer_select<bf16_t>(B) : defer_select<float>(B);
+  const bool db = wdtype == LVX_DTYPE_BF16 ? defer_select_batched<bf16_t>(B) : defer_select_batched<float>(B);
   if (d) hipLaunchKernelGGL(ar_select_final_kernel, dim3(B), dim3(64), 0, s, st);
   else if (db) hipLaunchKernelGGL(ar_argmax_kernel, dim3(B), dim3(256), 0, s, st);
 }

@@ -792,7 +792,7 @@ static int ar_step_impl(lvx_ctx* c, int n_steps, int B, const int32_t* slots, co
     OptScope os(&o);
     for (int i = 0; i < n_steps; ++i)
       ar_launch_step(c->arw, st, c->cfg.weight_dtype, c->cfg.kv_dtype, B, 0, nullptr, 0, 0, nullptr, s);
-    ar_launch_steps_end(st, c->cfg.weight_dtype, B, c->arw.q0_text != nullptr, s);
+    ar_launch_steps_end(st, c->cfg.weight_dtype, B, s);
     HIP_TRY(hipGetLastError());
     return LVX_OK;
   }
@@ -818,7 +818,7 @@ static int ar_step_impl(lvx_ctx* c, int n_steps, int B, const int32_t* slots, co
     if (int r = get_graph(1, &g1)) return r;
     for (; left > 0; --left) HIP_TRY(hipGraphLaunch(g1, s));
   }
-  ar_launch_steps_end(st, c->cfg.weight_dtype, B, c->arw.q0_text != nullptr, s);
+  ar_launch_steps_end(st, c->cfg.weight_dtype, B, s);
   HIP_TRY(hipGetLastError());
   return LVX_OK;
 }

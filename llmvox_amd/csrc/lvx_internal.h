@@ -138,7 +138,7 @@ void ar_launch_step(const ArWeights& w, const ArState& st, int wdtype, int kvdty
 int ar_probe(const ArWeights& w, const ArState& st, int wdtype, int kvdtype, int B, int which, int iters,
              hipStream_t s);
 void ar_launch_rowinfo_init(const ArState& st, int B, hipStream_t s);
-void ar_launch_steps_end(const ArState& st, int wdtype, int B, bool q0_tables, hipStream_t s);  // deferred select: commit the last step
+void ar_launch_steps_end(const ArState& st, int wdtype, int B, hipStream_t s);  // deferred select: commit the last step
 int ar_select_probe(const ArWeights& w, const ArState& st, int B, int path, hipStream_t s);  // test hook
 // ArWeights::q0_text / q0_code / q0_pos from the bf16 c_attn weight of layer 0 (lvx_finalize)
 void ar_launch_q0_tables(const ArWeights& w, int max_pos, float* text, float* code, float* pos, hipStream_t s);

@@ -165,12 +165,13 @@ def test_batched_deferred_select_matches_argmax_kernel(eng_batched, B, ref_mode)
 
 @pytest.mark.parametrize("B,slots", [(1, [2]), (2, [0, 3]), (2, [1, -1])], ids=["B1", "B2", "B2-idle"])
 def test_small_b_tables_agree_with_the_gemv(eng, B, slots):
-    """B <= 2, bf16 (round 6): layer 0's c_attn from the q0 tables inside the embedding + select kernel
-    (the select over the full logits, lm_head leaving plain logits, ar_argmax_kernel committing the
-    call's last step) against the GEMV whose prologue commits lm_head's granules (option l0q 0), over
-    several calls with graph replays and eager launches: the same state machine (plan steps, positions,
-    idle rows untouched), the tokens equal up to the first step whose margin is within the bf16 path's
-    noise, the graph replay bit-equal to the eager launches, and the logits within the bf16 bound."""
+    """B <= 2, bf16 (round 6): layer 0's c_attn from the q0 tables (ar_q0_gran_kernel: 9 blocks that
+    each commit-reduce lm_head's granules and compute 256 of the 2,304 outputs) against the GEMV whose
+    prologue does the same select before multiplying (option l0q 0), over several calls with graph
+    replays and eager launches: the same state machine (plan steps, positions, idle rows untouched),
+    the tokens equal up to the first step whose margin is within the noise (the two forms differ in
+    fp32 rounding only: the GEMV multiplies the fp32 LayerNorm'd row), the graph replay bit-equal to
+    the eager launches, and the logits within the bf16 bound."""
     if eng.weight_dtype != "bf16":
         pytest.skip("the q0 tables are a bf16-weight form")
     calls = [3, 17, 1, 16]
