@@ -1206,6 +1206,7 @@ __global__ __launch_bounds__(NW * 64) void ar_attn_v2_kernel(ArState st, int lay
   if (cp) {
     jn = st.rowx_n[b].x;
     st.rowinfo[b] = ri;
+    st.selrow[b] = 1u;  // (ar_q0_rows_kernel's pending select of the next step; unused by the granule forms)
     if (b == 0) *st.selp = 0u;
   }
   auto copy_tail = [&]() {
@@ -1601,17 +1602,13 @@ __global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_rows_kernel(GemvArgs a
 // row's control records), wave 0 commits and builds the operand row.
 // F32OUT (the batched fp32 parity mode): the LayerNorm'd row in fp32 into st.h (ar_rows_kernel<6>'s
 // output, read by ar_qkv_ksplit_f32_kernel)
-// QKV (bf16, B <= 32 but 3, option l0q): layer 0's c_attn is done here from the table rows of ArWeights
-// q0_* (src/model.py:47-50 on the input of :222-226): q / k / v[n] = rstd * ((Tt[t][n] + Tc[c][n]) / den
-// + Tp[p][n] - mean * G[n]). Tt[t] and Tp[p] (t, p follow from the control records, not from the select)
-// are loaded with the logits, Tc[c] of the token just selected by all four waves while wave 0 loads the
-// embedding rows for (den, mean, rstd): the c_attn GEMM launch and its boundary go (the operand is
-// never rounded to bf16, so the sums differ from the GEMM's in the last bits)
-template <bool F32OUT = false, bool QKV = false>
+// (With bf16 weights and option l0q the select runs in ar_q0_rows_kernel instead, which also computes
+// layer 0's q / k / v from the q0 tables; round 6's first form of that, one block per row inside this
+// kernel, took 1.1-1.7 us more per step and was removed.)
+template <bool F32OUT = false>
 __global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_embed_select_kernel(GemvArgs a) {
   __shared__ float sv[4], sv2[4];
   __shared__ int si[4];
-  __shared__ float4 sst;  // QKV: {1 / den, mean, rstd} of the row, wave 0 -> all
   const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   TS_DECL;
   TS_MARK(0);
@@ -1619,29 +1616,12 @@ __global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_embed_select_kernel(Ge
   const int2 rx = a.st.rowx[b];  // {plan step j, text id of step j + 1}
   const unsigned pend = a.st.selrow[b];
   float4 g[3];  // LN gamma first: the reduction's wait for the logits then covers it too
-  if constexpr (!QKV) {
 #pragma unroll
-    for (int j = 0; j < 3; ++j) g[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
-  }
+  for (int j = 0; j < 3; ++j) g[j] = *reinterpret_cast<const float4*>(a.ln_w + j * 256 + lane * 4);
   const float4* lg = reinterpret_cast<const float4*>(a.st.logits + (size_t)b * VOCAB);
   float4 lv[VOCAB / 1024];
 #pragma unroll
   for (int k = 0; k < VOCAB / 1024; ++k) lv[k] = lg[k * 256 + tid];
-  constexpr int NQ = QKV ? 3 * D / 256 : 1;  // outputs n = tid + 256 i of the row
-  float tq[NQ], tpo[NQ], gq[NQ];
-  if constexpr (QKV) {  // this step's (text id, position) as the commit below sets them
-    const bool tk = pend && ri.x >= 0;
-    const int p1 = min(max(tk ? ri.y + 1 : ri.y, 0), a.st.max_pos - 1);
-    const int t1 = tk ? rx.y : ri.z;
-    const float* tt = a.q0_text + (size_t)(t1 < 0 ? 384 : t1) * (3 * D);
-    const float* tp = a.q0_pos + (size_t)p1 * (3 * D);
-#pragma unroll
-    for (int i = 0; i < NQ; ++i) {
-      tq[i] = tt[tid + 256 * i];
-      tpo[i] = tp[tid + 256 * i];
-      gq[i] = a.q0_g[tid + 256 * i];
-    }
-  }
   Best bt{-INFINITY, -INFINITY, 0x7fffffff};
 #pragma unroll
   for (int k = 0; k < VOCAB / 1024; ++k) {
@@ -1655,16 +1635,16 @@ __global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_embed_select_kernel(Ge
   TS_MARK(1);
   if (lane == 0) { sv[wave] = bt.v; sv2[wave] = bt.v2; si[wave] = bt.i; }
   __syncthreads();
-  if (!QKV && wave != 0) return;
+  if (wave != 0) return;
   const bool take = pend && ri.x >= 0;
-  if (take) {  // (QKV: every wave merges the four partials, wave 0 commits)
+  if (take) {
     Best r{sv[0], sv2[0], si[0]};
 #pragma unroll
     for (int w = 1; w < 4; ++w) r = best_merge(r, Best{sv[w], sv2[w], si[w]});
     r = softmax_ties(a.st.logits + (size_t)b * VOCAB, r, lane);
     const int s = ri.x, p = ri.y + 1, j = rx.x;
     const int4 rn = make_int4(s, min(p, a.st.max_pos - 1), rx.y, min(max(r.i, 0), VOCAB - 1));
-    if (wave == 0 && lane == 0) {  // argmax_commit
+    if (lane == 0) {  // argmax_commit
       if (p >= a.st.max_pos) atomicOr(a.st.err, 1);
       if (j < a.st.plan_stride) {
         a.st.tok_plan[(size_t)b * a.st.plan_stride + j] = r.i;
@@ -1677,66 +1657,25 @@ __global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_embed_select_kernel(Ge
     }
     ri = rn;
   }
-  if (wave == 0 && lane == 0) a.st.selrow[b] = 1u;  // this step's lm_head leaves the next pending select
-  float tc[NQ];
-  if constexpr (QKV) {
-    const float* tcp = a.q0_code + (size_t)min(max(ri.w, 0), VOCAB - 1) * (3 * D);
+  if (lane == 0) a.st.selrow[b] = 1u;  // this step's lm_head leaves the next pending select
+  float4 v[3];
+  embed_row(a, ri, lane, v);
 #pragma unroll
-    for (int i = 0; i < NQ; ++i) tc[i] = tcp[tid + 256 * i];
-  }
-  if (wave == 0) {
-    float4 v[3];
-    float rden = 0.f;
-    embed_row(a, ri, lane, v, QKV ? &rden : nullptr);
+  for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = v[j];
+  wave_ln_regs(v, g);
+  if constexpr (F32OUT) {
 #pragma unroll
-    for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = v[j];
-    if constexpr (QKV) {  // (mean, rstd) as wave_ln_regs computes them
-      float sm = 0.f;
+    for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.h + (size_t)b * D + j * 256 + lane * 4) = v[j];
+  } else {
+    uint2* dst = reinterpret_cast<uint2*>(a.st.xn + (size_t)b * D);
 #pragma unroll
-      for (int j = 0; j < 3; ++j) sm += (v[j].x + v[j].y) + (v[j].z + v[j].w);
-      const float mean = wave_sum(sm) * (1.0f / D);
-      float qs = 0.f;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const float4 d = make_float4(v[j].x - mean, v[j].y - mean, v[j].z - mean, v[j].w - mean);
-        qs += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
-      }
-      const float rstd = 1.0f / sqrtf(wave_sum(qs) * (1.0f / D) + 1e-5f);
-      if (lane == 0) sst = make_float4(rden, mean, rstd, 0.f);
-    } else {
-      wave_ln_regs(v, g);
-      if constexpr (F32OUT) {
-#pragma unroll
-        for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.h + (size_t)b * D + j * 256 + lane * 4) = v[j];
-      } else {
-        uint2* dst = reinterpret_cast<uint2*>(a.st.xn + (size_t)b * D);
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          if (a.xpk) *reinterpret_cast<uint2*>(a.st.xn + xfrag(b, j * 256 + lane * 4, D)) = pack4_bf16(v[j]);
-          else dst[j * 64 + lane] = pack4_bf16(v[j]);
-        }
-      }
-    }
-    // the plan load for the next text id last: waiting for it earlier held the embedding loads
-    if (take && lane == 0) a.st.rowx[b] = make_int2(rx.x + 1, plan_tok(a.st, b, rx.x + 2));
-  }
-  if constexpr (QKV) {
-    __syncthreads();
-    const float4 st = sst;
-    const float cz = ri.y == 0 ? 0.f : 1.f;  // position 0: the codebook half of the input is zero
-#pragma unroll
-    for (int i = 0; i < NQ; ++i) {
-      const int n = tid + 256 * i;
-      const float o = ri.x < 0 ? 0.f : st.z * (((tq[i] + cz * tc[i]) * st.x + tpo[i]) - st.y * gq[i]);
-      if (n < D) {
-        a.st.q[(size_t)b * D + n] = o;
-      } else if (ri.x >= 0) {  // K / V append at the row's (slot, pos), as c_attn's epilogue
-        const int c = (n - D) % D, which = (n - D) / D;
-        const int head = c / HD, d = c - head * HD;
-        store_kv(a, which, kv_at(0, a.st.kv_chunks, a.st.max_streams, ri.x, head, ri.y) + d, o);
-      }
+    for (int j = 0; j < 3; ++j) {
+      if (a.xpk) *reinterpret_cast<uint2*>(a.st.xn + xfrag(b, j * 256 + lane * 4, D)) = pack4_bf16(v[j]);
+      else dst[j * 64 + lane] = pack4_bf16(v[j]);
     }
   }
+  // the plan load for the next text id last: waiting for it earlier held the embedding loads
+  if (take && lane == 0) a.st.rowx[b] = make_int2(rx.x + 1, plan_tok(a.st, b, rx.x + 2));
   TS_SAVE(7, 0, b);
 }
 
@@ -1848,6 +1787,109 @@ __global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_q0_gran_kernel(GemvArg
     }
   }
   TS_SAVE(7, 0, blockIdx.x);
+}
+
+// Batched steps (4 <= B <= 32, bf16, option l0q; defer_sel 4): the previous step's greedy select and
+// layer 0's c_attn from the q0 tables (as ar_embed_select_kernel<false, true> computes them) over a grid
+// of 9 column slices x B rows: every block reduces its row's 4,096 logits (four waves, as
+// ar_embed_select_kernel), loads 256-column slices of Tt[t], Tp[p], G and Tc[c] and builds the
+// embedding row for (den, mean, rstd) with wave 0. The select is committed by the row's first block
+// into the shadow records (rowinfo_n / rowx_n: the row's other blocks read rowinfo in this launch),
+// which attention layer 0 copies back (it also sets the row's pending flag). Round 6: one block per row
+// (ar_embed_select_kernel<false, true>) spent 4.7 us of the B = 32 step in this launch, its blocks
+// each loading the 27 KB of table rows with the 16 KB of logits.
+__global__ __launch_bounds__(256) LVX_LOADS_FIRST void ar_q0_rows_kernel(GemvArgs a) {
+  __shared__ float sv[4], sv2[4];
+  __shared__ int si[4];
+  __shared__ float4 sst;  // {1 / den, mean, rstd}
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int cx = blockIdx.x, b = blockIdx.y;
+  const int n = cx * 256 + tid;  // this thread's output column (3 * D = 9 x 256)
+  TS_DECL;
+  TS_MARK(0);
+  const int4 ri = a.st.rowinfo[b];
+  const int2 rx = a.st.rowx[b];
+  const unsigned pend = a.st.selrow[b];
+  const float4* lg = reinterpret_cast<const float4*>(a.st.logits + (size_t)b * VOCAB);
+  float4 lv[VOCAB / 1024];
+#pragma unroll
+  for (int k = 0; k < VOCAB / 1024; ++k) lv[k] = lg[k * 256 + tid];
+  const float gq = a.q0_g[n];
+  // this step's (text id, position) as the commit sets them (from the records, not the select)
+  const bool tk = pend && ri.x >= 0;
+  const int p1 = min(max(tk ? ri.y + 1 : ri.y, 0), a.st.max_pos - 1);
+  const int t1 = tk ? rx.y : ri.z;
+  const float tq = a.q0_text[(size_t)(t1 < 0 ? 384 : t1) * (3 * D) + n];
+  const float tpo = a.q0_pos[(size_t)p1 * (3 * D) + n];
+  Best bt{-INFINITY, -INFINITY, 0x7fffffff};
+#pragma unroll
+  for (int k = 0; k < VOCAB / 1024; ++k) {
+    const int i0 = (k * 256 + tid) * 4;
+    bt = best_merge(bt, Best{lv[k].x, -INFINITY, i0});
+    bt = best_merge(bt, Best{lv[k].y, -INFINITY, i0 + 1});
+    bt = best_merge(bt, Best{lv[k].z, -INFINITY, i0 + 2});
+    bt = best_merge(bt, Best{lv[k].w, -INFINITY, i0 + 3});
+  }
+  bt = best_wave(bt);
+  if (lane == 0) { sv[wave] = bt.v; sv2[wave] = bt.v2; si[wave] = bt.i; }
+  __syncthreads();
+  int4 rn = ri;
+  if (tk) {  // (block-uniform) every wave merges the four partials; the row's first block commits
+    Best r{sv[0], sv2[0], si[0]};
+#pragma unroll
+    for (int w = 1; w < 4; ++w) r = best_merge(r, Best{sv[w], sv2[w], si[w]});
+    r = softmax_ties(a.st.logits + (size_t)b * VOCAB, r, lane);
+    const int sl = ri.x, p = ri.y + 1, j = rx.x;
+    rn = make_int4(sl, min(p, a.st.max_pos - 1), rx.y, min(max(r.i, 0), VOCAB - 1));
+    if (cx == 0 && tid == 0) {  // argmax_commit, with the records into the shadow arrays
+      if (p >= a.st.max_pos) atomicOr(a.st.err, 1);
+      if (j < a.st.plan_stride) {
+        a.st.tok_plan[(size_t)b * a.st.plan_stride + j] = r.i;
+        if (a.st.margin_plan) a.st.margin_plan[(size_t)b * a.st.plan_stride + j] = r.v - r.v2;
+      }
+      a.st.prev[sl] = r.i;
+      a.st.pos[sl] = p;
+      a.st.rowstep[b] = j + 1;
+    }
+  }
+  if (cx == 0 && tid == 0) {
+    a.st.rowinfo_n[b] = rn;
+    a.st.rowx_n[b] = make_int2(tk ? rx.x + 1 : rx.x, 0);  // attention layer 0 looks up the next text id
+  }
+  const float tc = a.q0_code[(size_t)min(max(rn.w, 0), VOCAB - 1) * (3 * D) + n];
+  if (wave == 0) {
+    float4 v[3];
+    float rden = 0.f;
+    embed_row(a, rn, lane, v, &rden);
+    if (cx == 0) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = v[j];
+    }
+    float sm = 0.f;  // (mean, rstd) as wave_ln_regs computes them
+#pragma unroll
+    for (int j = 0; j < 3; ++j) sm += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+    const float mean = wave_sum(sm) * (1.0f / D);
+    float qs = 0.f;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const float4 d = make_float4(v[j].x - mean, v[j].y - mean, v[j].z - mean, v[j].w - mean);
+      qs += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(qs) * (1.0f / D) + 1e-5f);
+    if (lane == 0) sst = make_float4(rden, mean, rstd, 0.f);
+  }
+  __syncthreads();
+  const float4 st = sst;
+  const float cz = rn.y == 0 ? 0.f : 1.f;  // position 0: the codebook half of the input is zero
+  const float o = rn.x < 0 ? 0.f : st.z * (((tq + cz * tc) * st.x + tpo) - st.y * gq);
+  if (n < D) {
+    a.st.q[(size_t)b * D + n] = o;
+  } else if (rn.x >= 0) {  // K / V append at the row's (slot, pos), as c_attn's epilogue
+    const int c = (n - D) % D, which = (n - D) / D;
+    const int head = c / HD, d = c - head * HD;
+    store_kv(a, which, kv_at(0, a.st.kv_chunks, a.st.max_streams, rn.x, head, rn.y) + d, o);
+  }
+  TS_SAVE(7, 0, cx + 9 * b);
 }
 
 // split-KV merge for the batched path: y[b] (bf16) into st.xn. NS = ns_max (the attention's split
@@ -3048,9 +3090,8 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       a.W = w.w_attn[l]; a.Wf = w.f_attn[l]; a.N = 3 * D; a.ln_w = w.ln1[l];
       if (mf && l == 0 && a.defer_sel == 3) {  // the previous step's select + embedding in c_attn's prologue
         launch_mfma_ln<0, 7>(a, s);
-      } else if (mf && l == 0 && a.defer_sel == 2 && opts().l0q && a.q0_text) {
-        // embedding + the previous step's select + c_attn from the q0 tables, one launch
-        hipLaunchKernelGGL((ar_embed_select_kernel<false, true>), dim3(B), dim3(256), 0, s, a);
+      } else if (mf && l == 0 && a.defer_sel == 4) {  // select + c_attn from the q0 tables, 9 slices per row
+        hipLaunchKernelGGL(ar_q0_rows_kernel, dim3(3 * D / 256, B), dim3(256), 0, s, a);
       } else if (mf && l == 0 && a.defer_sel == 2) {  // embedding + the previous step's select, then c_attn
         hipLaunchKernelGGL(ar_embed_select_kernel<>, dim3(B), dim3(256), 0, s, a);
         launch_mfma2<768, 0>(a, s);
@@ -3074,7 +3115,8 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
       }
       break;
     case 1:
-      launch_attn(a.st, kvdtype, B, l, s, nsm, (mf && nsm == 1) ? 1 + a.xpk : 0, (a.defer_sel == 1 || a.defer_sel == 3) && l == 0,
+      launch_attn(a.st, kvdtype, B, l, s, nsm, (mf && nsm == 1) ? 1 + a.xpk : 0,
+                  (a.defer_sel == 1 || a.defer_sel == 3 || a.defer_sel == 4) && l == 0,
                   false, a8);
       break;
     case 2:
@@ -3157,11 +3199,14 @@ static bool ar_layers(const ArWeights& w, const ArState& st, int kvdtype, int B,
                       int pos, float* logits_dst, bool select, hipStream_t s) {
   GemvArgs a = make_args<TW>(w, st, kvdtype, B, emb_row);
   a.defer_sel = (select && !emb_row) ? (defer_select<TW>(B) ? 1 : defer_select_batched<TW>(B) ? (defer_select_ln<TW>(B) ? 3 : 2) : 0) : 0;
-  // 4 <= B <= 8 with layer 0's c_attn from the q0 tables (option l0q): the embedding + select kernel
-  // computes q / k / v itself, so the select moves there from c_attn's prologue (round 6, tools/
-  // b8_l0q_ab.sh: B = 8 fp8 KV t = 384-639 98.3 -> 96.3 us per step, bf16 KV 101.0 -> 99.0, B = 4 93.8
-  // -> 92.5; the reference-agreement measures unchanged, profiles/r06/b8_l0q_ab.txt)
-  if (a.defer_sel == 3 && opts().l0q && w.q0_text) a.defer_sel = 2;
+  // bf16 with option l0q, 4 <= B <= 32: the previous step's select and layer 0's c_attn from the q0
+  // tables in one launch, ar_q0_rows_kernel (9 column slices per row; defer_sel 4): at B > 8 the c_attn
+  // GEMM launch goes, at 4 <= B <= 8 the c_attn-with-select launch reads table rows instead of weight
+  // slices (round 6, us per step at t = 384-639, each A/B on one box: the tables in one block per row
+  // took B = 32 -2.9, B = 8 -1.8 / -2.5 (fp8 / bf16 KV), B = 4 -1.4 (l0q_ab.txt, b8_l0q_ab.txt); the 9
+  // slices per row a further -1.1 / -1.7 / -1.7 (q0rows_ab.txt); the reference-agreement measures
+  // unchanged). B <= 2 keep their granule select with the tables in ar_q0_gran_kernel.
+  if ((a.defer_sel == 2 || a.defer_sel == 3) && use_mfma<TW>(B) && B <= 32 && opts().l0q && w.q0_text) a.defer_sel = 4;
   if (emb_row) hipLaunchKernelGGL(ar_row_state_kernel, dim3(1), dim3(1), 0, s, st, slot, pos);
   for (int l = 0; l < N_LAYER; ++l)
     for (int op = 0; op < 5; ++op) launch_op<TW>(op, a, w, l, kvdtype, B, s);

@@ -160,7 +160,7 @@ def test_rows_structure_at_small_b(B, kv):
 
 @pytest.mark.parametrize("B,kv", [(4, "bf16"), (8, "fp8"), (9, "bf16"), (16, "bf16"), (32, "bf16"), (32, "fp8")])
 def test_layer0_tables_agree_with_the_gemm(B, kv):
-    """Layer 0's c_attn from the q0 tables inside the embedding + select kernel (option l0q, B >= 4)
+    """Layer 0's c_attn from the q0 tables with the select (ar_q0_rows_kernel, option l0q, B >= 4)
     against the c_attn GEMM (B > 8: after the embedding kernel; 4 <= B <= 8: the GEMM whose prologue
     commits the select from lm_head's granules and builds the embedding rows), after a shared ragged
     prefix: the same step up to

@@ -284,7 +284,7 @@ def test_granule_select_fp8_kv_matches_embed_select(B):
     and the argmax kernel after lm_head (0), across several lvx_ar_steps calls and graph replays on a
     side stream, with an idle row: tokens, margins, plan steps, positions and the live rows' logits
     bit-equal. (Layer 0's c_attn as the GEMM, option l0q 0: with the q0 tables the 4 <= B <= 8 select
-    runs in the embedding + select kernel, held to the GEMM form in
+    runs in ar_q0_rows_kernel, held to the GEMM form in
     tests/test_gpu_batched.py::test_layer0_tables_agree_with_the_gemm.)"""
     from llmvox_amd.engine import build_engine
     e = build_engine(0, "bf16", "fp8", max_streams=8, max_positions=512, max_codec_frames=64)
