@@ -1,6 +1,7 @@
 """Development check: an option A/B (lvx_set_option) must leave the decode bit-identical: tokens,
 margins and final logits of N steps from position 0, bf16 weights + bf16 KV.
-usage: python tools/ab_bitcheck.py OPT VALUE [B ...]   (LVX_AB_W=fp32: fp32 weights + fp32 KV, the parity mode)"""
+usage: python tools/ab_bitcheck.py OPT VALUE [B ...]   (LVX_AB_W=fp32: fp32 weights + fp32 KV, the parity mode;
+LVX_AB_KV=fp8: bf16 weights with the fp8 KV cache)"""
 import os
 import sys
 import torch
@@ -9,7 +10,8 @@ from llmvox_amd.engine import build_engine
 opt, val = sys.argv[1], int(sys.argv[2])
 Bs = [int(x) for x in sys.argv[3:]] or [4, 16, 17, 24, 32]
 W = os.environ.get("LVX_AB_W", "bf16")
-e = build_engine(0, W, W, max_streams=max(Bs), max_positions=1024, max_codec_frames=256)
+KV = os.environ.get("LVX_AB_KV", W)
+e = build_engine(0, W, KV, max_streams=max(Bs), max_positions=1024, max_codec_frames=256)
 e.set_option("fuse_mlp", 0)  # the fused MLP (B <= 2) adds with fp32 atomics: run-to-run noise
 dev = e.device
 n = 320
