@@ -214,3 +214,50 @@ def test_fragment_packed_rows_with_odd_engine_size(S):
             e.close()
     np.testing.assert_array_equal(res[0][0], res[1][0])
     np.testing.assert_array_equal(res[0][1], res[1][1])
+
+
+@pytest.mark.parametrize("B", [8, 32])
+def test_table_path_idle_row_and_batch_composition(B):
+    """The default bf16 path (layer 0 from the q0 tables inside the select launch, ar_q0_rows_kernel)
+    with an idle row (slot -1) in the batch, over several lvx_ar_steps calls replayed as graphs on a
+    side stream: the idle row's plan step and token buffer stay untouched, and the live rows' tokens
+    and last logits are bit-equal to the same rows decoded without the idle row (B - 1 rows: the rows
+    are independent of the batch they run in)."""
+    from llmvox_amd.engine import build_engine
+    e = build_engine(0, "bf16", "bf16", max_streams=B, max_positions=256, max_codec_frames=64)
+    dev = e.device
+    texts = _texts(B, 40, seed=41)
+    idle = B // 2
+    calls = [3, 17, 1, 16]
+    n = sum(calls)
+
+    def run(slots):
+        for s in range(B):
+            e.reset_slot(s)
+        plan = torch.from_numpy(texts[[max(s, 0) for s in slots], :n].copy()).to(dev)
+        st = torch.tensor(slots, dtype=torch.int32, device=dev)
+        rowstep = torch.zeros(len(slots), dtype=torch.int32, device=dev)
+        tok = torch.full((len(slots), n), -7, dtype=torch.int32, device=dev)
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for c in calls:
+                e.ar_steps(c, st, plan, rowstep, tok)
+            e.check_errors()
+            lg = e.last_logits(len(slots))
+        torch.cuda.current_stream(dev).wait_stream(side)
+        return tok.cpu().numpy(), rowstep.cpu().numpy(), lg.cpu().numpy()
+
+    try:
+        with_idle = list(range(B))
+        with_idle[idle] = -1
+        tok_i, rs_i, lg_i = run(with_idle)
+        live = [s for s in range(B) if s != idle]
+        tok_l, rs_l, lg_l = run(live)
+    finally:
+        e.close()
+    assert rs_i[idle] == 0 and (tok_i[idle] == -7).all()
+    rows = [b for b in range(B) if b != idle]
+    assert (rs_i[rows] == n).all() and (rs_l == n).all()
+    np.testing.assert_array_equal(tok_i[rows], tok_l)
+    np.testing.assert_array_equal(lg_i[rows], lg_l)
