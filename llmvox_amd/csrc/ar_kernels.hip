@@ -1500,6 +1500,15 @@ __device__ __forceinline__ uint2 pack4_bf16(float4 v) {
                     (uint32_t)f32_to_bf16(v.z) | ((uint32_t)f32_to_bf16(v.w) << 16));
 }
 
+#ifndef LVX_YCS
+#define LVX_YCS 2
+#endif
+// pending copies of the mlp c_proj K slices at B <= ln_max, which every block of the next LayerNorm-
+// prologue GEMM (c_attn, lm_head) folds for all B rows: 2 slices of 1,536 (96 blocks of 8 waves), so the
+// prologues load 3 instead of 5 KB-rows per batch row (round 6, tools/ycs_ab.sh against 4 slices of 768,
+// the LVX_YCS=4 build: B = 8 fp8 KV 94.8 / 95.1 -> 94.3 / 93.6 us per step, bf16 97.2 -> 96.7, B = 4
+// 90.9 -> 90.5; configs[4] 82.0k -> 82.7k). B > ln_max keeps 4 slices (YCOPIES) for the rows kernel.
+constexpr int YCS = LVX_YCS;
 constexpr int MFMA_BATCH_MIN = 3;  // smallest B on the batched MFMA path (measured B = 3: 117 vs 154 us, B = 2: 119 vs 114)
 // batched path: LayerNorm / embedding fused into the MFMA GEMM prologue for B <= this value
 // (measured: B = 8 147 vs 156 us/step; B = 32 slower, every block re-normalising 32 rows)
@@ -2001,14 +2010,14 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
       const int n = min(n0 + r, a.N - 1);
       float t = a.st.x[(size_t)b * D + n];
       // (a.yacc is set on every MFMA step; a null one reads x itself, never folded)
-      const float* yp = a.yacc ? a.yacc + (size_t)b * YCOPIES * D + n : a.st.x + (size_t)b * D + n;
+      const float* yp = a.yacc ? a.yacc + (size_t)b * YCS * D + n : a.st.x + (size_t)b * D + n;
       const int ys = a.yacc ? D : 0;
-      float yc[YCOPIES];
+      float yc[YCS];
 #pragma unroll
-      for (int c = 0; c < YCOPIES; ++c) yc[c] = yp[c * ys];
+      for (int c = 0; c < YCS; ++c) yc[c] = yp[c * ys];
       if (a.yacc && a.add_y)
 #pragma unroll
-        for (int c = 0; c < YCOPIES; ++c) t += yc[c];
+        for (int c = 0; c < YCS; ++c) t += yc[c];
       xpre[k] = t;
     }
   }
@@ -2119,7 +2128,7 @@ __global__ __launch_bounds__(K / 192 * 64) void ar_mfma2_kernel(GemvArgs a) {
       a.st.xb[a.xpk ? xfrag(b, n, D) : (size_t)b * D + n] = f32_to_bf16(xn * gpre[k]);
       xo[e] = xn;
     } else if (OUT == 6) {  // split-K partial of mlp c_proj (K slice by) -> pending copy
-      a.yacc[((size_t)b * YCOPIES + by) * D + n] = v;
+      a.yacc[((size_t)b * (KTOT / K) + by) * D + n] = v;
     } else if (OUT == 1) {  // x (+ the folded copies, prefetched) + v
       a.st.x[(size_t)b * D + n] = xpre[k] + v;
     } else {
@@ -2219,7 +2228,7 @@ __global__ __launch_bounds__(256) void ar_mfma_ln_kernel(GemvArgs a) {
   // (clamped rows, unconditional loads: a load under a branch drains everything in flight; the
   // pending copies of the first YR rows come with them, the rest are loaded in step 2)
   constexpr int YR = MODE == 4 ? (RW < 2 ? RW : 2) : 0;
-  float4 xv[RW][3], ya[YR > 0 ? YR : 1][YCOPIES][3];
+  float4 xv[RW][3], ya[YR > 0 ? YR : 1][YCS][3];
   int4 ri[RW];
   // MODE 7: the select's inputs with the control records (clamped rows, unconditional loads)
   LmGran8 lmg[SR];
@@ -2245,10 +2254,10 @@ __global__ __launch_bounds__(256) void ar_mfma_ln_kernel(GemvArgs a) {
     }
     if (i < YR)
 #pragma unroll
-      for (int c = 0; c < YCOPIES; ++c)
+      for (int c = 0; c < YCS; ++c)
 #pragma unroll
         for (int j = 0; j < 3; ++j)
-          ya[i < YR ? i : 0][c][j] = *reinterpret_cast<const float4*>(a.yacc + ((size_t)b * YCOPIES + c) * D + j * 256 + lane * 4);
+          ya[i < YR ? i : 0][c][j] = *reinterpret_cast<const float4*>(a.yacc + ((size_t)b * YCS + c) * D + j * 256 + lane * 4);
   }
   const int k0 = wave * 192 + 8 * (lane >> 4);
   float4 g[3];  // gamma ahead of the weights (the first LayerNorm waits for it)
@@ -2302,11 +2311,11 @@ __global__ __launch_bounds__(256) void ar_mfma_ln_kernel(GemvArgs a) {
           for (int j = 0; j < 3; ++j) *reinterpret_cast<float4*>(a.st.x + (size_t)b * D + j * 256 + lane * 4) = xv[i][j];
       } else if (MODE == 4) {  // + the pending split-K copies of the previous mlp c_proj
 #pragma unroll
-        for (int c = 0; c < YCOPIES; ++c)
+        for (int c = 0; c < YCS; ++c)
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
             const float4 y = i < YR ? ya[i < YR ? i : 0][c][j]
-                                    : *reinterpret_cast<const float4*>(a.yacc + ((size_t)b * YCOPIES + c) * D + j * 256 + lane * 4);
+                                    : *reinterpret_cast<const float4*>(a.yacc + ((size_t)b * YCS + c) * D + j * 256 + lane * 4);
             xv[i][j].x += y.x; xv[i][j].y += y.y; xv[i][j].z += y.z; xv[i][j].w += y.w;
           }
       }
@@ -3152,7 +3161,9 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
     case 4:
       a.W = w.w_mproj[l]; a.Wf = w.f_mproj[l]; a.N = D;
       if (fm) return false;
-      if (mf) launch_mproj_split<6>(a, s);
+      if (mf && YCS == 2 && B <= MFMA_LN_MAX)  // (A/B build) 2 K slices of 1,536 into YCS copies
+        hipLaunchKernelGGL((ar_mfma2_kernel<1536, 1, 6, DFF>), dim3(D / 16, 2), dim3(512), 0, s, a);
+      else if (mf) launch_mproj_split<6>(a, s);
       else launch_gemv<TW, 3072, 4, 2, 1, 1>(a, s);
       break;
     case 5:
