@@ -3161,8 +3161,8 @@ static bool launch_op(int op, GemvArgs& a, const ArWeights& w, int l, int kvdtyp
     case 4:
       a.W = w.w_mproj[l]; a.Wf = w.f_mproj[l]; a.N = D;
       if (fm) return false;
-      if (mf && YCS == 2 && B <= MFMA_LN_MAX)  // (A/B build) 2 K slices of 1,536 into YCS copies
-        hipLaunchKernelGGL((ar_mfma2_kernel<1536, 1, 6, DFF>), dim3(D / 16, 2), dim3(512), 0, s, a);
+      if (mf && YCS < YCOPIES && B <= MFMA_LN_MAX)  // YCS K slices of DFF / YCS into the YCS copies
+        hipLaunchKernelGGL((ar_mfma2_kernel<DFF / YCS, 1, 6, DFF>), dim3(D / 16, YCS), dim3(DFF / YCS / 192 * 64), 0, s, a);
       else if (mf) launch_mproj_split<6>(a, s);
       else launch_gemv<TW, 3072, 4, 2, 1, 1>(a, s);
       break;

@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 export PYTHONPATH=.
 O=gpurun_out/ycs.txt
 : > $O
-V=llmvox_amd/libllmvox_hip_ycs2.so
+V=${V:-llmvox_amd/libllmvox_hip_ycs2.so}
 for i in 1 2; do
 for lib in llmvox_amd/libllmvox_hip.so $V; do
 echo "## $lib" >> $O
