@@ -200,7 +200,7 @@ struct lvx_ctx {
   Opts opts;                 // this context's kernel options (lvx_set_option, under mu)
   unsigned opt_epoch = 0;    // bumped by every lvx_set_option on this context (under mu)
   unsigned graph_epoch = 0;  // opt_epoch when the cached graphs were captured
-  hipStream_t capture_stream = nullptr;  // graphs of null-stream callers are captured here
+  hipStream_t capture_stream = nullptr;  // every graph is captured here (cached_graph), then replayed on the caller's stream
   std::mutex mu;
 
   // a snapshot of the options, taken under mu: the caller binds it (OptScope) for its launches
@@ -734,9 +734,13 @@ int lvx_ar_forward_row(lvx_ctx* c, int slot, int pos, const float* emb_row, floa
   return LVX_OK;
 }
 
-// Capture `launch(stream)` into a graph cached under `key` (instantiated once). The legacy null
-// stream cannot be captured: its callers' graphs are captured on the context's own stream and
-// replayed on the null stream. Caller holds c->mu.
+// Capture `launch(stream)` into a graph cached under `key` (instantiated once), always on the context's
+// own capture stream, then replayed on the caller's stream. (The legacy null stream cannot be captured
+// at all; and capturing on the caller's stream broke on a process-group watchdog (round 6): torch's
+// synchronous collectives record their completion events on the current stream, the watchdog thread
+// queries them, and HIP refuses a query of an event last recorded in a stream that is capturing,
+// which aborted the process and failed the capture. No other code records on the private stream.)
+// Caller holds c->mu.
 static int cached_graph(lvx_ctx* c, const GraphKey& key, hipStream_t s,
                         const std::function<void(hipStream_t)>& launch, hipGraphExec_t* out) {
   const unsigned epoch = c->opt_epoch;  // (caller holds c->mu)
@@ -747,11 +751,9 @@ static int cached_graph(lvx_ctx* c, const GraphKey& key, hipStream_t s,
   }
   auto it = c->graphs.find(key);
   if (it == c->graphs.end()) {
-    hipStream_t cs = s;
-    if (!cs) {
-      if (!c->capture_stream) HIP_TRY(hipStreamCreateWithFlags(&c->capture_stream, hipStreamNonBlocking));
-      cs = c->capture_stream;
-    }
+    (void)s;
+    if (!c->capture_stream) HIP_TRY(hipStreamCreateWithFlags(&c->capture_stream, hipStreamNonBlocking));
+    hipStream_t cs = c->capture_stream;
     hipGraph_t g;
     HIP_TRY(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
     launch(cs);
