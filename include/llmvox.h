@@ -197,6 +197,12 @@ int lvx_stream_position(lvx_ctx* ctx, int slot, int* pos_out, void* stream);
  *                     bits: tests/test_gpu_batched.py, test_gpu_select.py); 0: the c_attn GEMM / GEMV
  *                     (B > 8 after the embedding + select kernel; B <= 8 with the granule select). */
 int lvx_set_option(lvx_ctx* ctx, const char* name, int value);
+/* The stream the decode graphs are captured on (then replayed on the caller's stream). NULL (default):
+ * the caller's stream. Name another one when something may query, from another thread, an event
+ * recorded on the caller's stream while lvx_ar_step* runs (a process group's watchdog after a
+ * synchronous collective on that stream): HIP refuses such a query during a capture. The stream
+ * named must not be the caller's and must outlive the context's use of it. */
+int lvx_set_capture_stream(lvx_ctx* ctx, void* stream);
 /* Enable/disable HIP-graph replay of lvx_ar_step for a given B (default on). */
 int lvx_set_graphs(lvx_ctx* ctx, int enable);
 

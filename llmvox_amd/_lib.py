@@ -90,6 +90,7 @@ _SIGS = {
     "lvx_select_probe": (_I, [_P, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P]),
     "lvx_stream_position": (_I, [_P, _I, ctypes.POINTER(_I), _P]),
     "lvx_set_graphs": (_I, [_P, _I]),
+    "lvx_set_capture_stream": (_I, [_P, _P]),
     "lvx_set_option": (_I, [_P, ctypes.c_char_p, _I]),
     "lvx_codec_decode_features": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "lvx_codec_decode_codes": (_I, [_P, _P, _I, _I, _I, _P, _P]),

@@ -7,6 +7,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 #include <atomic>
 #include <cstring>
@@ -200,7 +201,7 @@ struct lvx_ctx {
   Opts opts;                 // this context's kernel options (lvx_set_option, under mu)
   unsigned opt_epoch = 0;    // bumped by every lvx_set_option on this context (under mu)
   unsigned graph_epoch = 0;  // opt_epoch when the cached graphs were captured
-  hipStream_t capture_stream = nullptr;  // every graph is captured here (cached_graph), then replayed on the caller's stream
+  hipStream_t capture_stream = nullptr;  // lvx_set_capture_stream (not owned); null: capture on the caller's
   std::mutex mu;
 
   // a snapshot of the options, taken under mu: the caller binds it (OptScope) for its launches
@@ -367,7 +368,6 @@ void lvx_destroy(lvx_ctx* c) {
   (void)hipSetDevice(c->cfg.device);
   for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
   for (auto g : c->graph_defs) (void)hipGraphDestroy(g);
-  if (c->capture_stream) (void)hipStreamDestroy(c->capture_stream);
   for (void* p : c->allocs) (void)hipFree(p);
   delete c;
 }
@@ -709,6 +709,13 @@ int lvx_set_option(lvx_ctx* c, const char* name, int value) {
   return LVX_OK;
 }
 
+int lvx_set_capture_stream(lvx_ctx* c, void* stream) {
+  if (!c) return fail(LVX_E_ARG, "null ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->capture_stream = (hipStream_t)stream;
+  return LVX_OK;
+}
+
 int lvx_set_graphs(lvx_ctx* c, int enable) {
   if (!c) return fail(LVX_E_ARG, "null ctx");
   c->use_graphs = enable != 0;
@@ -734,12 +741,15 @@ int lvx_ar_forward_row(lvx_ctx* c, int slot, int pos, const float* emb_row, floa
   return LVX_OK;
 }
 
-// Capture `launch(stream)` into a graph cached under `key` (instantiated once), always on the context's
-// own capture stream, then replayed on the caller's stream. (The legacy null stream cannot be captured
-// at all; and capturing on the caller's stream broke on a process-group watchdog (round 6): torch's
-// synchronous collectives record their completion events on the current stream, the watchdog thread
-// queries them, and HIP refuses a query of an event last recorded in a stream that is capturing,
-// which aborted the process and failed the capture. No other code records on the private stream.)
+// Capture `launch(stream)` into a graph cached under `key` (instantiated once), then replay it on the
+// caller's stream. The capture runs on the caller's stream unless lvx_set_capture_stream named another:
+// torch's synchronous collectives record their completion events on the current stream, a process
+// group's watchdog thread queries them, and HIP refuses a query of an event last recorded in a stream
+// that is capturing (round 6: a configs[4] line with the one-rank RCCL group aborted mid-capture). The
+// Python engine therefore hands over a pooled stream once an RCCL group exists; without one it keeps
+// the caller's, since one more stream per process cost the two-ranks-on-one-GPU configs[3] rehearsal
+// 6.5x (22.4k -> 3.4k tokens/s, profiles/r06/capture_stream_ab.txt) while a single rank per GPU saw no
+// difference. (The legacy null stream cannot be captured: null-stream callers never reach here.)
 // Caller holds c->mu.
 static int cached_graph(lvx_ctx* c, const GraphKey& key, hipStream_t s,
                         const std::function<void(hipStream_t)>& launch, hipGraphExec_t* out) {
@@ -751,9 +761,7 @@ static int cached_graph(lvx_ctx* c, const GraphKey& key, hipStream_t s,
   }
   auto it = c->graphs.find(key);
   if (it == c->graphs.end()) {
-    (void)s;
-    if (!c->capture_stream) HIP_TRY(hipStreamCreateWithFlags(&c->capture_stream, hipStreamNonBlocking));
-    hipStream_t cs = c->capture_stream;
+    hipStream_t cs = c->capture_stream ? c->capture_stream : s;
     hipGraph_t g;
     HIP_TRY(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
     launch(cs);

@@ -10,6 +10,7 @@ from typing import Dict, Optional
 
 import numpy as np
 import torch
+import torch.distributed as dist
 
 from . import _lib
 from .weights import CODEBOOK_KEY, TEXT_EMBED_KEY
@@ -34,6 +35,7 @@ class Engine:
         with torch.cuda.device(self.device):
             _lib.check(self.lib.lvx_create(ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
+        self._capture_stream = None
         self.weight_dtype = weight_dtype
         self.kv_dtype = kv_dtype
         self.codec_dtype = codec_dtype or weight_dtype
@@ -99,10 +101,12 @@ class Engine:
     def ar_steps(self, n_steps: int, slots: torch.Tensor, text_plan: torch.Tensor, rowstep: torch.Tensor,
                  tok_plan: torch.Tensor, margin_plan: Optional[torch.Tensor] = None):
         B, stride = text_plan.shape
+        self._capture_guard()
         _lib.check(self.lib.lvx_ar_steps(self.h, n_steps, B, _ptr(slots), _ptr(text_plan), stride, _ptr(rowstep),
                                          _ptr(tok_plan), _ptr(margin_plan), self.stream_handle()))
 
     def probe_kernel(self, which: int, slots: torch.Tensor, iters: int):
+        self._capture_guard()
         _lib.check(self.lib.lvx_probe_kernel(self.h, which, slots.numel(), _ptr(slots), iters, self.stream_handle()))
 
     def select_probe(self, path: int, slots: torch.Tensor, logits: torch.Tensor, text_plan: torch.Tensor,
@@ -134,6 +138,28 @@ class Engine:
 
     def set_option(self, name: str, value: int):
         _lib.check(self.lib.lvx_set_option(self.h, name.encode(), int(value)))
+
+    def set_capture_stream(self, stream: Optional["torch.cuda.Stream"]):
+        """Capture the decode graphs on `stream` (None: on the caller's stream), lvx_set_capture_stream."""
+        self._capture_stream = stream
+        _lib.check(self.lib.lvx_set_capture_stream(self.h, ctypes.c_void_p(stream.cuda_stream if stream else None)))
+
+    def _capture_guard(self):
+        # Once an RCCL process group exists, its watchdog thread queries the events that synchronous
+        # collectives record on the current stream, and HIP refuses that query while the stream is
+        # capturing (lvx_api.cpp cached_graph): capture on a pooled stream of torch's that nothing else
+        # records on. Not before: one more stream per process cost two ranks sharing a GPU 6.5x.
+        # (a pooled stream may come round again as the caller's: never capture on the stream called on)
+        if self._capture_stream is None:
+            if not (dist.is_available() and dist.is_initialized() and "nccl" in str(dist.get_backend()).lower()):
+                return
+        elif self._capture_stream.cuda_stream != torch.cuda.current_stream(self.device).cuda_stream:
+            return
+        cur = torch.cuda.current_stream(self.device).cuda_stream
+        s = torch.cuda.Stream(device=self.device)
+        while s.cuda_stream == cur:
+            s = torch.cuda.Stream(device=self.device)
+        self.set_capture_stream(s)
 
     def set_graphs(self, enable: bool):
         _lib.check(self.lib.lvx_set_graphs(self.h, int(enable)))
