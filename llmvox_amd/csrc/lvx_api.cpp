@@ -202,6 +202,7 @@ struct lvx_ctx {
   unsigned opt_epoch = 0;    // bumped by every lvx_set_option on this context (under mu)
   unsigned graph_epoch = 0;  // opt_epoch when the cached graphs were captured
   hipStream_t capture_stream = nullptr;  // lvx_set_capture_stream (not owned); null: capture on the caller's
+  hipStream_t own_capture_stream = nullptr;  // created for null-stream callers only (cached_graph)
   std::mutex mu;
 
   // a snapshot of the options, taken under mu: the caller binds it (OptScope) for its launches
@@ -368,6 +369,7 @@ void lvx_destroy(lvx_ctx* c) {
   (void)hipSetDevice(c->cfg.device);
   for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
   for (auto g : c->graph_defs) (void)hipGraphDestroy(g);
+  if (c->own_capture_stream) (void)hipStreamDestroy(c->own_capture_stream);
   for (void* p : c->allocs) (void)hipFree(p);
   delete c;
 }
@@ -749,7 +751,8 @@ int lvx_ar_forward_row(lvx_ctx* c, int slot, int pos, const float* emb_row, floa
 // Python engine therefore hands over a pooled stream once an RCCL group exists; without one it keeps
 // the caller's, since one more stream per process cost the two-ranks-on-one-GPU configs[3] rehearsal
 // 6.5x (22.4k -> 3.4k tokens/s, profiles/r06/capture_stream_ab.txt) while a single rank per GPU saw no
-// difference. (The legacy null stream cannot be captured: null-stream callers never reach here.)
+// difference. (The legacy null stream cannot be captured: lvx_ar_step* null-stream callers launch the
+// steps one by one; lvx_probe_kernel's capture on a stream the context creates.)
 // Caller holds c->mu.
 static int cached_graph(lvx_ctx* c, const GraphKey& key, hipStream_t s,
                         const std::function<void(hipStream_t)>& launch, hipGraphExec_t* out) {
@@ -762,6 +765,10 @@ static int cached_graph(lvx_ctx* c, const GraphKey& key, hipStream_t s,
   auto it = c->graphs.find(key);
   if (it == c->graphs.end()) {
     hipStream_t cs = c->capture_stream ? c->capture_stream : s;
+    if (!cs) {  // the legacy null stream cannot be captured (lvx_probe_kernel's null-stream callers)
+      if (!c->own_capture_stream) HIP_TRY(hipStreamCreateWithFlags(&c->own_capture_stream, hipStreamNonBlocking));
+      cs = c->own_capture_stream;
+    }
     hipGraph_t g;
     HIP_TRY(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
     launch(cs);
